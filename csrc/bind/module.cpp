@@ -1,0 +1,352 @@
+// Python binding of the native core (pybind11).  The package's Python layer
+// (poisson_ellipse_openmp_mpi_cuda_amd) adds torch.distributed bootstrap,
+// the PyTorch fp64 oracle, the CLI/bench and reporting on top of this.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+
+#include "../hip/kernels.hpp"
+#include "pe/device.hpp"
+#include "pe/solver.hpp"
+
+namespace py = pybind11;
+using namespace pe;
+
+namespace {
+
+py::dict timers_dict(const Timers& t) {
+  py::dict d;
+  d["gpu"] = t.gpu;
+  d["copy"] = t.copy;
+  d["halo"] = t.halo;
+  d["reduce"] = t.reduce;
+  d["prec"] = t.prec;
+  d["dot"] = t.dot;
+  d["setup"] = t.setup;
+  d["solver"] = t.solver;
+  d["iterate"] = t.iterate;
+  return d;
+}
+
+py::array_t<double> to_array(std::vector<double>&& v, int64_t rows, int64_t cols) {
+  auto* heap = new std::vector<double>(std::move(v));
+  py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<double>*>(p); });
+  return py::array_t<double>({rows, cols}, {cols * int64_t(sizeof(double)), int64_t(sizeof(double))}, heap->data(),
+                             owner);
+}
+
+py::dict state_dict(const dev::DevState& s) {
+  py::dict d;
+  d["red_F"] = py::make_tuple(s.red_F[0], s.red_F[1]);
+  d["red_G"] = s.red_G[0];
+  d["err"] = py::make_tuple(s.err[0], s.err[1], s.err[2]);
+  d["rz_cur"] = s.rz_cur;
+  d["alpha"] = s.alpha;
+  d["beta"] = s.beta;
+  d["last_diff"] = s.last_diff;
+  d["iter"] = s.iter;
+  d["done"] = s.done;
+  d["status"] = s.status;
+  return d;
+}
+
+// Handle to a DeviceComm owned by Python.
+struct CommHandle {
+  std::unique_ptr<DeviceComm> comm;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(_native, m) {
+  m.doc() = "Native core of the MI355X Poisson/fictitious-domain PCG framework (C++ / HIP gfx950 / RCCL)";
+
+  py::enum_<Norm>(m, "Norm").value("Weighted", Norm::Weighted).value("Unweighted", Norm::Unweighted);
+  py::enum_<Init>(m, "Init").value("Zero", Init::Zero).value("Random", Init::Random);
+  py::enum_<DecompMode>(m, "DecompMode").value("Reference", DecompMode::Reference).value("Aspect", DecompMode::Aspect);
+
+  py::class_<Problem>(m, "Problem")
+      .def(py::init<>())
+      .def_readwrite("A1", &Problem::A1)
+      .def_readwrite("B1", &Problem::B1)
+      .def_readwrite("A2", &Problem::A2)
+      .def_readwrite("B2", &Problem::B2)
+      .def_readwrite("F", &Problem::F)
+      .def_readwrite("cx", &Problem::cx)
+      .def_readwrite("cy", &Problem::cy)
+      .def_readwrite("sx", &Problem::sx)
+      .def_readwrite("sy", &Problem::sy)
+      .def_readwrite("M", &Problem::M)
+      .def_readwrite("N", &Problem::N)
+      .def_readwrite("tol", &Problem::tol)
+      .def_readwrite("max_iter", &Problem::max_iter)
+      .def_readwrite("norm", &Problem::norm)
+      .def("h1", &Problem::h1)
+      .def("h2", &Problem::h2)
+      .def("eps", &Problem::eps)
+      .def("iter_cap", &Problem::iter_cap)
+      .def("u_scale", &Problem::u_scale);
+
+  py::class_<ProcessGrid>(m, "ProcessGrid")
+      .def(py::init<>())
+      .def_readwrite("Px", &ProcessGrid::Px)
+      .def_readwrite("Py", &ProcessGrid::Py);
+
+  py::class_<Block>(m, "Block")
+      .def_readonly("rank", &Block::rank)
+      .def_readonly("size", &Block::size)
+      .def_readonly("Px", &Block::Px)
+      .def_readonly("Py", &Block::Py)
+      .def_readonly("px", &Block::px)
+      .def_readonly("py", &Block::py)
+      .def_readonly("i0", &Block::i0)
+      .def_readonly("i1", &Block::i1)
+      .def_readonly("j0", &Block::j0)
+      .def_readonly("j1", &Block::j1)
+      .def_readonly("nx", &Block::nx)
+      .def_readonly("ny", &Block::ny)
+      .def_readonly("pitch", &Block::pitch)
+      .def_readonly("rows", &Block::rows)
+      .def_readonly("base", &Block::base)
+      .def_readonly("alloc", &Block::alloc)
+      .def_property_readonly("nbr", [](const Block& b) { return std::vector<int>(b.nbr, b.nbr + 4); })
+      .def("__repr__", &describe);
+
+  m.def("choose_process_grid", &choose_process_grid, py::arg("P"), py::arg("M"), py::arg("N"),
+        py::arg("mode") = DecompMode::Aspect);
+  m.def("choose_process_grid_reference", &choose_process_grid_reference);
+  m.def("halo_cost", &halo_cost);
+  m.def("decompose", &decompose, py::arg("M"), py::arg("N"), py::arg("pg"), py::arg("rank"), py::arg("align") = 8);
+
+  py::class_<SolveOptions>(m, "SolveOptions")
+      .def(py::init<>())
+      .def_readwrite("init", &SolveOptions::init)
+      .def_readwrite("seed", &SolveOptions::seed)
+      .def_readwrite("init_amp", &SolveOptions::init_amp)
+      .def_readwrite("threads", &SolveOptions::threads)
+      .def_readwrite("log_every", &SolveOptions::log_every)
+      .def_readwrite("keep_history", &SolveOptions::keep_history)
+      .def_readwrite("compute_error", &SolveOptions::compute_error)
+      .def_readwrite("verbose", &SolveOptions::verbose)
+      .def_readwrite("chunk", &SolveOptions::chunk)
+      .def_readwrite("use_graph", &SolveOptions::use_graph)
+      .def_readwrite("timing", &SolveOptions::timing)
+      .def_readwrite("check_tol", &SolveOptions::check_tol)
+      .def_readwrite("variant", &SolveOptions::variant);
+
+  py::class_<SolveResult>(m, "SolveResult")
+      .def_readonly("iters", &SolveResult::iters)
+      .def_readonly("converged", &SolveResult::converged)
+      .def_readonly("breakdown", &SolveResult::breakdown)
+      .def_readonly("last_diff", &SolveResult::last_diff)
+      .def_readonly("zr", &SolveResult::zr)
+      .def_readonly("l2_err", &SolveResult::l2_err)
+      .def_readonly("max_err", &SolveResult::max_err)
+      .def_readonly("max_outside", &SolveResult::max_outside)
+      .def_readonly("history", &SolveResult::history)
+      .def_readonly("Px", &SolveResult::Px)
+      .def_readonly("Py", &SolveResult::Py)
+      .def_readonly("backend", &SolveResult::backend)
+      .def_property_readonly("timers", [](const SolveResult& r) { return timers_dict(r.t); });
+
+  m.def("format_result_legacy", &format_result_legacy);
+
+  // ---- CPU backends ------------------------------------------------------
+  m.def(
+      "cpu_solve",
+      [](const Problem& P, int ranks, DecompMode mode, const SolveOptions& opt, bool return_w) {
+        std::vector<double> w;
+        SolveResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = cpu_pcg_threads(P, ranks, mode, opt, return_w ? &w : nullptr);
+        }
+        py::object wa = py::none();
+        if (return_w) wa = to_array(std::move(w), P.M - 1, P.N - 1);
+        return py::make_tuple(r, wa);
+      },
+      py::arg("prob"), py::arg("ranks") = 1, py::arg("mode") = DecompMode::Reference, py::arg("opt") = SolveOptions(),
+      py::arg("return_w") = false);
+
+  // One rank of a multi-process CPU run; the transport is Python callbacks
+  // (torch.distributed, typically gloo).  exchange_fn receives a list of
+  // (dir, peer, send: ndarray, recv: writable ndarray) valid during the call.
+  m.def(
+      "cpu_solve_rank",
+      [](const Problem& P, const Block& blk, py::function reduce_fn, py::function exchange_fn,
+         py::function barrier_fn, const SolveOptions& opt, bool return_w) {
+        auto reduce = [reduce_fn](double* buf, int n, bool is_max) {
+          py::gil_scoped_acquire g;
+          py::array_t<double> a({n}, {int64_t(sizeof(double))}, buf, py::none());
+          reduce_fn(a, is_max);
+        };
+        auto exch = [exchange_fn](const std::vector<Exchange>& ex) {
+          py::gil_scoped_acquire g;
+          py::list items;
+          for (const auto& e : ex) {
+            py::array_t<double> s({e.count}, {int64_t(sizeof(double))}, const_cast<double*>(e.send), py::none());
+            py::array_t<double> r({e.count}, {int64_t(sizeof(double))}, e.recv, py::none());
+            items.append(py::make_tuple(e.dir, e.peer, s, r));
+          }
+          exchange_fn(items);
+        };
+        auto bar = [barrier_fn]() {
+          py::gil_scoped_acquire g;
+          barrier_fn();
+        };
+        CallbackHostComm comm(blk.rank, blk.size, reduce, exch, bar);
+        std::vector<double> w;
+        SolveResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = cpu_pcg(P, blk, comm, opt, return_w ? &w : nullptr);
+        }
+        py::object wa = py::none();
+        if (return_w) wa = to_array(std::move(w), blk.nx, blk.ny);
+        return py::make_tuple(r, wa);
+      },
+      py::arg("prob"), py::arg("block"), py::arg("reduce_fn"), py::arg("exchange_fn"), py::arg("barrier_fn"),
+      py::arg("opt") = SolveOptions(), py::arg("return_w") = false);
+
+  // ---- device (HIP / RCCL) ----------------------------------------------
+  m.def("device_count", &device_count);
+  m.def("set_device", &set_device);
+  m.def("device_name", &device_name);
+  m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+
+  py::class_<CommHandle>(m, "DeviceComm")
+      .def_property_readonly("rank", [](const CommHandle& h) { return h.comm->rank(); })
+      .def_property_readonly("size", [](const CommHandle& h) { return h.comm->size(); })
+      .def_property_readonly("name", [](const CommHandle& h) { return h.comm->name(); });
+  m.def(
+      "make_rccl_comm",
+      [](py::bytes uid, int rank, int size) {
+        auto h = std::make_unique<CommHandle>();
+        std::string s = uid;
+        py::gil_scoped_release nogil;
+        h->comm = make_rccl_comm(s, rank, size);
+        return h;
+      },
+      py::arg("uid"), py::arg("rank"), py::arg("size"));
+  m.def(
+      "make_rccl_comm_from_handle",
+      [](uintptr_t handle) {
+        auto h = std::make_unique<CommHandle>();
+        h->comm = make_rccl_comm_from_handle(reinterpret_cast<void*>(handle));
+        return h;
+      },
+      py::arg("nccl_comm_ptr"));
+
+  py::class_<DeviceSolver>(m, "DeviceSolver")
+      .def(py::init([](const Problem& P, const Block& blk, CommHandle* comm, const SolveOptions& opt) {
+             return std::make_unique<DeviceSolver>(P, blk, comm ? comm->comm.get() : nullptr, opt);
+           }),
+           py::arg("prob"), py::arg("block"), py::arg("comm") = nullptr, py::arg("opt") = SolveOptions(),
+           py::keep_alive<1, 4>())
+      .def("solve",
+           [](DeviceSolver& s) {
+             py::gil_scoped_release nogil;
+             return s.solve();
+           })
+      .def("reset", [](DeviceSolver& s) {
+        py::gil_scoped_release nogil;
+        s.reset();
+        s.synchronize();
+      })
+      .def("run_iterations",
+           [](DeviceSolver& s, int64_t n, bool g) {
+             py::gil_scoped_release nogil;
+             s.run_iterations(n, g);
+           },
+           py::arg("iters"), py::arg("use_graph") = true)
+      .def("time_iterations",
+           [](DeviceSolver& s, int64_t n, bool g) {
+             py::gil_scoped_release nogil;
+             return s.time_iterations(n, g);
+           },
+           py::arg("iters"), py::arg("use_graph") = true)
+      .def("synchronize", [](DeviceSolver& s) {
+        py::gil_scoped_release nogil;
+        s.synchronize();
+      })
+      .def("state",
+           [](DeviceSolver& s) {
+             dev::DevState st;
+             s.read_state(&st);
+             return state_dict(st);
+           })
+      .def("w",
+           [](DeviceSolver& s) {
+             const Block& b = s.block();
+             std::vector<double> v(size_t(b.nx * b.ny));
+             s.copy_w(v.data());
+             return to_array(std::move(v), b.nx, b.ny);
+           })
+      .def("field",
+           [](DeviceSolver& s, int which) {
+             const Block& b = s.block();
+             std::vector<double> v(size_t(b.rows * b.pitch));
+             s.copy_field(which, v.data());
+             return to_array(std::move(v), b.rows, b.pitch);
+           })
+      .def_property_readonly("chunk", &DeviceSolver::chunk)
+      .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
+      .def_property_readonly("blocks", [](DeviceSolver& s) { return dev::grid_blocks(s.params()); })
+      .def_property_readonly("block", &DeviceSolver::block);
+
+  m.def(
+      "device_solve_group",
+      [](const Problem& P, int ranks, DecompMode mode, const SolveOptions& opt, bool return_w) {
+        std::vector<double> w;
+        SolveResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = device_solve_group(P, ranks, mode, opt, return_w ? &w : nullptr);
+        }
+        py::object wa = py::none();
+        if (return_w) wa = to_array(std::move(w), P.M - 1, P.N - 1);
+        return py::make_tuple(r, wa);
+      },
+      py::arg("prob"), py::arg("ranks"), py::arg("mode") = DecompMode::Aspect, py::arg("opt") = SolveOptions(),
+      py::arg("return_w") = false);
+
+  // Single-shot device ops for numerics tests: `p` is a full local field
+  // (rows × pitch, halo included); returns arrays of the same shape.
+  m.def("device_apply_A", [](const Problem& P, const Block& blk, py::array_t<double, py::array::c_style> p) {
+    if (p.size() != blk.rows * blk.pitch) throw std::invalid_argument("p must be rows x pitch");
+    SolveOptions opt;
+    DeviceSolver s(P, blk, nullptr, opt);
+    const size_t bytes = sizeof(double) * blk.rows * blk.pitch;
+    double *dp = nullptr, *dA = nullptr;
+    PE_HIP_CHECK(hipMalloc(&dp, bytes));
+    PE_HIP_CHECK(hipMalloc(&dA, bytes));
+    PE_HIP_CHECK(hipMemcpy(dp, p.data(), bytes, hipMemcpyHostToDevice));
+    PE_HIP_CHECK(hipMemset(dA, 0, bytes));
+    dev::launch_apply_A(s.params(), dp, dA, s.stream());
+    std::vector<double> out(blk.rows * blk.pitch);
+    PE_HIP_CHECK(hipStreamSynchronize(s.stream()));
+    PE_HIP_CHECK(hipMemcpy(out.data(), dA, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipFree(dp));
+    PE_HIP_CHECK(hipFree(dA));
+    return to_array(std::move(out), blk.rows, blk.pitch);
+  });
+  m.def("device_coefficients", [](const Problem& P, const Block& blk) {
+    SolveOptions opt;
+    DeviceSolver s(P, blk, nullptr, opt);
+    const size_t n = size_t(blk.rows * blk.pitch), bytes = sizeof(double) * n;
+    double* d = nullptr;
+    PE_HIP_CHECK(hipMalloc(&d, 3 * bytes));
+    PE_HIP_CHECK(hipMemset(d, 0, 3 * bytes));
+    dev::launch_coef(s.params(), d, d + n, d + 2 * n, s.stream());
+    PE_HIP_CHECK(hipStreamSynchronize(s.stream()));
+    std::vector<double> a(n), b(n), D(n);
+    PE_HIP_CHECK(hipMemcpy(a.data(), d, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipMemcpy(b.data(), d + n, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipMemcpy(D.data(), d + 2 * n, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipFree(d));
+    return py::make_tuple(to_array(std::move(a), blk.rows, blk.pitch), to_array(std::move(b), blk.rows, blk.pitch),
+                          to_array(std::move(D), blk.rows, blk.pitch));
+  });
+}

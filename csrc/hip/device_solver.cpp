@@ -1,0 +1,513 @@
+// Device-resident Jacobi-PCG driver (host side).
+//
+// Reference: gradient_solver_mpi (poisson_mpi_cuda2.cu:687-982).  Where the
+// reference assembles a/b/B on the CPU, copies them over, and then drives
+// every iteration from the host (6 cudaDeviceSynchronize, 3 × 256 KiB D2H
+// partial copies, 3 host MPI_Allreduce, host-staged halos), this driver:
+//   * builds two 1-D chord tables (O(M+N) bytes) instead of 3 full arrays,
+//   * keeps α, β, the stop test and the iteration count on the device,
+//   * enqueues chunks of iterations (captured once into a hipGraph when the
+//     transport allows it) and only looks at a pinned copy of the device
+//     state once per chunk, with two chunks in flight so the GPU never idles
+//     on the host,
+//   * talks to peers through a stream-ordered DeviceComm (RCCL over xGMI).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <deque>
+
+#include "../hip/kernels.hpp"
+#include "pe/device.hpp"
+
+namespace pe {
+
+using dev::DevState;
+using dev::KParams;
+
+namespace {
+using clk = std::chrono::steady_clock;
+double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
+}  // namespace
+
+DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* comm, const SolveOptions& opt)
+    : prob_(prob), blk_(blk), comm_(comm), opt_(opt), kp_(std::make_unique<KParams>()) {
+  if (!comm_) {
+    self_ = std::make_unique<SelfDeviceComm>();
+    comm_ = self_.get();
+  }
+  PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  const int64_t A = blk_.alloc;
+  PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * A * 4));
+  const int64_t ntab = (blk_.nx + 4) * 4 + (blk_.ny + 4) * 4;
+  PE_HIP_CHECK(hipMalloc(&tables_, sizeof(double) * ntab));
+  PE_HIP_CHECK(hipMalloc(&halo_, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4));
+  PE_HIP_CHECK(hipMalloc(&st_, sizeof(DevState)));
+  PE_HIP_CHECK(hipHostMalloc(&hst_, sizeof(DevState) * 2, hipHostMallocDefault));
+  std::memset(hst_, 0, sizeof(DevState) * 2);
+  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_[0], hipEventDisableTiming));
+  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_[1], hipEventDisableTiming));
+  PE_HIP_CHECK(hipEventCreate(&t0_));
+  PE_HIP_CHECK(hipEventCreate(&t1_));
+
+  KParams& k = *kp_;
+  std::memset(&k, 0, sizeof(KParams));
+  k.nx = blk_.nx;
+  k.ny = blk_.ny;
+  k.pitch = blk_.pitch;
+  k.M = prob_.M;
+  k.N = prob_.N;
+  k.gi0 = blk_.i0 - 1;
+  k.gj0 = blk_.j0 - 1;
+  k.A1 = prob_.A1;
+  k.A2 = prob_.A2;
+  k.h1 = prob_.h1();
+  k.h2 = prob_.h2();
+  k.eps = prob_.eps();
+  k.inv_eps = 1.0 / k.eps;
+  k.h1sq = k.h1 * k.h1;
+  k.h2sq = k.h2 * k.h2;
+  k.nih1 = -1.0 / k.h1;
+  k.nih2 = -1.0 / k.h2;
+  k.cx = prob_.cx;
+  k.cy = prob_.cy;
+  k.F = prob_.F;
+  k.u_scale = prob_.u_scale();
+  k.tol = prob_.tol;
+  k.weighted = prob_.norm == Norm::Weighted ? 1 : 0;
+  k.max_iter = prob_.iter_cap();
+  for (int d = 0; d < 4; ++d) k.has[d] = blk_.has(d) ? 1 : 0;
+  k.colT = tables_;
+  k.rowT = tables_ + (blk_.nx + 4) * 4;
+  k.r = fields_ + blk_.base;
+  k.w = fields_ + A + blk_.base;
+  k.p[0] = fields_ + 2 * A + blk_.base;
+  k.p[1] = fields_ + 3 * A + blk_.base;
+  const int64_t hx = std::max<int64_t>(1, blk_.nx);
+  k.send_dn = halo_;
+  k.send_up = halo_ + hx;
+  k.recv_dn = halo_ + 2 * hx;
+  k.recv_up = halo_ + 3 * hx;
+  k.st = st_;
+  k.check_tol = opt_.check_tol ? 1 : 0;
+  // Rows per marching block: enough blocks to fill 256 CUs several times
+  // over, long enough strips to amortise the 2 redundant halo rows.
+  int ti = 32;
+  const int64_t strips = (blk_.ny + dev::kTJ - 1) / dev::kTJ;
+  while (ti > 8 && strips * ((blk_.nx + ti - 1) / ti) < 2048) ti /= 2;
+  if (const char* e = std::getenv("PE_TI")) ti = std::max(1, std::min(dev::kTImax, std::atoi(e)));
+  k.ti = ti;
+  const int64_t npart = std::max<int64_t>(2 * int64_t(dev::grid_blocks(k)), 3 * 4096);
+  PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * npart));
+  k.partial = partial_;
+  build_tables();
+
+  // Iterations per host check: aim for ~0.5 ms of device work per chunk.
+  const double pts = double(blk_.nx) * double(blk_.ny);
+  const double t_iter = pts * 64.0 / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
+  int c = int(0.5e-3 / t_iter);
+  c = std::max(8, std::min(128, c));
+  c += c & 1;
+  chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
+}
+
+DeviceSolver::~DeviceSolver() {
+  if (graph_) (void)hipGraphExecDestroy(graph_);
+  (void)hipEventDestroy(ev_[0]);
+  (void)hipEventDestroy(ev_[1]);
+  (void)hipEventDestroy(t0_);
+  (void)hipEventDestroy(t1_);
+  (void)hipFree(fields_);
+  (void)hipFree(tables_);
+  (void)hipFree(halo_);
+  (void)hipFree(partial_);
+  (void)hipFree(st_);
+  (void)hipHostFree(hst_);
+  (void)hipStreamDestroy(stream_);
+}
+
+KParams& DeviceSolver::params() { return *kp_; }
+
+void DeviceSolver::build_tables() {
+  const Problem& P = prob_;
+  const double h1 = P.h1(), h2 = P.h2();
+  std::vector<double> t((blk_.nx + 4) * 4 + (blk_.ny + 4) * 4, 0.0);
+  double* col = t.data();
+  double* row = t.data() + (blk_.nx + 4) * 4;
+  for (int64_t li = -1; li <= blk_.nx + 2; ++li) {
+    const int64_t gi = blk_.i0 - 1 + li;
+    const double x = P.A1 + gi * h1;
+    double* c = col + (li + 1) * 4;
+    c[0] = chord_half_vertical(x - 0.5 * h1, P.cx, P.cy, P.sx);
+    c[1] = x - 0.5 * h1;
+    c[2] = x + 0.5 * h1;
+    c[3] = x;
+  }
+  for (int64_t lj = -1; lj <= blk_.ny + 2; ++lj) {
+    const int64_t gj = blk_.j0 - 1 + lj;
+    const double y = P.A2 + gj * h2;
+    double* r = row + (lj + 1) * 4;
+    r[0] = y - 0.5 * h2;
+    r[1] = y + 0.5 * h2;
+    r[2] = chord_half_horizontal(y - 0.5 * h2, P.cx, P.cy, P.sy);
+    r[3] = y;
+  }
+  PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
+}
+
+std::vector<Exchange> DeviceSolver::halo_plan() const {
+  const KParams& k = *kp_;
+  std::vector<Exchange> ex;
+  if (blk_.has(LEFT))
+    ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], k.r + 1 * k.pitch + 1, k.r + 0 * k.pitch + 1, blk_.ny});
+  if (blk_.has(RIGHT))
+    ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], k.r + blk_.nx * k.pitch + 1, k.r + (blk_.nx + 1) * k.pitch + 1,
+                          blk_.ny});
+  if (blk_.has(DOWN)) ex.push_back(Exchange{DOWN, blk_.nbr[DOWN], k.send_dn, const_cast<double*>(k.recv_dn), blk_.nx});
+  if (blk_.has(UP)) ex.push_back(Exchange{UP, blk_.nbr[UP], k.send_up, const_cast<double*>(k.recv_up), blk_.nx});
+  return ex;
+}
+
+double* DeviceSolver::red_F_dev() { return st_->red_F; }
+double* DeviceSolver::red_G_dev() { return st_->red_G; }
+double* DeviceSolver::err_dev() { return st_->err; }
+
+void DeviceSolver::enqueue_init() {
+  const int64_t A = blk_.alloc;
+  PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * A * 4, stream_));
+  PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4, stream_));
+  PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
+  dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, stream_);
+  PE_HIP_CHECK(hipGetLastError());
+}
+
+void DeviceSolver::enqueue_F(int par) { dev::launch_F(*kp_, par, opt_.variant, stream_); }
+void DeviceSolver::enqueue_G(int par) { dev::launch_G(*kp_, par, opt_.variant, stream_); }
+void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
+
+void DeviceSolver::enqueue_iteration(int par) {
+  dev::launch_F(*kp_, par, opt_.variant, stream_);
+  comm_->allreduce_sum(st_->red_F, 2, stream_);
+  dev::launch_G(*kp_, par, opt_.variant, stream_);
+  comm_->exchange(halo_plan(), stream_);
+  comm_->allreduce_sum(st_->red_G, 1, stream_);
+}
+
+bool DeviceSolver::graph_ready(int iters) {
+  if (graph_ && graph_iters_ == iters) return true;
+  if (graph_) {
+    PE_HIP_CHECK(hipGraphExecDestroy(graph_));
+    graph_ = nullptr;
+  }
+  hipGraph_t g = nullptr;
+  PE_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
+  for (int it = 0; it < iters; ++it) enqueue_iteration(it & 1);
+  PE_HIP_CHECK(hipStreamEndCapture(stream_, &g));
+  PE_HIP_CHECK(hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0));
+  PE_HIP_CHECK(hipGraphDestroy(g));
+  graph_iters_ = iters;
+  return true;
+}
+
+void DeviceSolver::enqueue_chunk(int iters) {
+  if (opt_.use_graph && comm_->capturable() && (iters % 2) == 0) {
+    graph_ready(iters);
+    PE_HIP_CHECK(hipGraphLaunch(graph_, stream_));
+  } else {
+    for (int it = 0; it < iters; ++it) enqueue_iteration(it & 1);
+  }
+  PE_HIP_CHECK(hipGetLastError());
+}
+
+void DeviceSolver::read_state(DevState* out) {
+  PE_HIP_CHECK(hipMemcpyAsync(out, st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void DeviceSolver::synchronize() { PE_HIP_CHECK(hipStreamSynchronize(stream_)); }
+
+void DeviceSolver::reset() {
+  enqueue_init();
+  comm_->exchange(halo_plan(), stream_);
+  comm_->allreduce_sum(st_->red_G, 1, stream_);
+}
+
+void DeviceSolver::run_iterations(int64_t iters, bool use_graph) {
+  const bool saved = opt_.use_graph;
+  opt_.use_graph = use_graph;
+  int64_t done = 0;
+  while (done < iters) {
+    int64_t n = std::min<int64_t>(chunk_, iters - done);
+    if (n >= 2) n -= (n & 1);
+    enqueue_chunk(int(n));
+    done += n;
+  }
+  opt_.use_graph = saved;
+}
+
+double DeviceSolver::time_iterations(int64_t iters, bool use_graph) {
+  PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+  run_iterations(iters, use_graph);
+  PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+  PE_HIP_CHECK(hipEventSynchronize(t1_));
+  float ms = 0;
+  PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+  return ms * 1e-3;
+}
+
+SolveResult DeviceSolver::solve() {
+  const auto t_start = clk::now();
+  SolveResult res;
+  res.backend = "hip";
+  res.Px = blk_.Px;
+  res.Py = blk_.Py;
+  reset();
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+  res.t.setup = secs(t_start, clk::now());
+
+  const int64_t cap = prob_.iter_cap();
+  const auto t_loop = clk::now();
+  PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+  if (opt_.timing) {
+    // Eager, per-phase event timing (host sync per chunk; diagnostic mode).
+    std::vector<hipEvent_t> ev(6);
+    for (auto& e : ev) PE_HIP_CHECK(hipEventCreate(&e));
+    int64_t k = 0;
+    DevState hs;
+    for (;;) {
+      for (int it = 0; it < chunk_; ++it, ++k) {
+        const int par = int(k & 1);
+        PE_HIP_CHECK(hipEventRecord(ev[0], stream_));
+        dev::launch_F(*kp_, par, opt_.variant, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[1], stream_));
+        comm_->allreduce_sum(st_->red_F, 2, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[2], stream_));
+        dev::launch_G(*kp_, par, opt_.variant, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[3], stream_));
+        comm_->exchange(halo_plan(), stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[4], stream_));
+        comm_->allreduce_sum(st_->red_G, 1, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[5], stream_));
+        PE_HIP_CHECK(hipEventSynchronize(ev[5]));
+        float t[5];
+        for (int q = 0; q < 5; ++q) PE_HIP_CHECK(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
+        res.t.gpu += (t[0] + t[2]) * 1e-3;
+        res.t.reduce += (t[1] + t[4]) * 1e-3;
+        res.t.halo += t[3] * 1e-3;
+      }
+      read_state(&hs);
+      if (hs.done || k >= cap) break;
+    }
+    for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
+  } else {
+    int64_t enq = 0;
+    int slot = 0;
+    std::deque<int> inflight;
+    bool stop = false;
+    for (;;) {
+      while (!stop && enq < cap && inflight.size() < 2) {
+        enqueue_chunk(chunk_);
+        enq += chunk_;
+        PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+        PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
+        inflight.push_back(slot);
+        slot ^= 1;
+      }
+      if (inflight.empty()) break;
+      const int s = inflight.front();
+      inflight.pop_front();
+      PE_HIP_CHECK(hipEventSynchronize(ev_[s]));
+      if (hst_[s].done) stop = true;
+    }
+  }
+  PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+  PE_HIP_CHECK(hipEventSynchronize(t1_));
+  float ms = 0;
+  PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+  res.t.iterate = secs(t_loop, clk::now());
+  if (!opt_.timing) res.t.gpu = ms * 1e-3;
+
+  DevState hs;
+  if (opt_.compute_error) {
+    dev::launch_error(*kp_, stream_);
+    comm_->allreduce_sum(st_->err, 1, stream_);
+    comm_->allreduce_max(st_->err + 1, 2, stream_);
+  }
+  read_state(&hs);
+  res.iters = hs.iter;
+  res.converged = hs.status == 1;
+  res.breakdown = hs.status == 2;
+  res.last_diff = hs.last_diff;
+  res.zr = hs.rz_cur;
+  if (opt_.compute_error) {
+    res.l2_err = std::sqrt(hs.err[0] * prob_.h1() * prob_.h2());
+    res.max_err = hs.err[1];
+    res.max_outside = hs.err[2];
+  }
+  res.t.solver = secs(t_start, clk::now());
+  // Timers: max over ranks (reference MPI_Reduce(MAX), :962-966).
+  double tv[8] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate, 0};
+  comm_->host_max(tv, 8, stream_);
+  res.t.gpu = tv[0];
+  res.t.copy = tv[1];
+  res.t.halo = tv[2];
+  res.t.reduce = tv[3];
+  res.t.setup = tv[4];
+  res.t.solver = tv[5];
+  res.t.iterate = tv[6];
+  return res;
+}
+
+void DeviceSolver::copy_w(double* host, bool owned_only) {
+  const KParams& k = *kp_;
+  if (owned_only) {
+    PE_HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * blk_.ny, k.w + k.pitch + 1, sizeof(double) * k.pitch,
+                                  sizeof(double) * blk_.ny, blk_.nx, hipMemcpyDeviceToHost, stream_));
+  } else {
+    PE_HIP_CHECK(hipMemcpyAsync(host, k.w, sizeof(double) * blk_.rows * k.pitch, hipMemcpyDeviceToHost, stream_));
+  }
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+void DeviceSolver::copy_field(int which, double* host) {
+  const KParams& k = *kp_;
+  const double* src = which == 0 ? k.r : which == 1 ? k.w : which == 2 ? k.p[0] : k.p[1];
+  PE_HIP_CHECK(hipMemcpyAsync(host, src, sizeof(double) * blk_.rows * k.pitch, hipMemcpyDeviceToHost, stream_));
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
+// ---------------------------------------------------------------------------
+// Virtual ranks on one device.
+// ---------------------------------------------------------------------------
+SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, const SolveOptions& opt,
+                               std::vector<double>* w_out) {
+  const auto t_start = clk::now();
+  const ProcessGrid pg = choose_process_grid(ranks, P.M, P.N, mode);
+  std::vector<std::unique_ptr<DeviceSolver>> s;
+  std::vector<Block> blks;
+  for (int r = 0; r < ranks; ++r) {
+    blks.push_back(decompose(P.M, P.N, pg, r));
+    s.push_back(std::make_unique<DeviceSolver>(P, blks.back(), nullptr, opt));
+  }
+  std::vector<std::vector<Exchange>> plan(ranks);
+  for (int r = 0; r < ranks; ++r) plan[r] = s[r]->halo_plan();
+  std::vector<hipEvent_t> ev(ranks);
+  for (auto& e : ev) PE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  // Device pointer tables for the cross-rank reduction kernel.
+  std::vector<double*> hp(3 * ranks);
+  for (int r = 0; r < ranks; ++r) {
+    hp[r] = s[r]->red_F_dev();
+    hp[ranks + r] = s[r]->red_G_dev();
+    hp[2 * ranks + r] = s[r]->err_dev();
+  }
+  double** dp = nullptr;
+  PE_HIP_CHECK(hipMalloc(&dp, sizeof(double*) * 3 * ranks));
+  PE_HIP_CHECK(hipMemcpy(dp, hp.data(), sizeof(double*) * 3 * ranks, hipMemcpyHostToDevice));
+  double* err1[64];
+  hipStream_t s0 = s[0]->stream();
+
+  auto join_all = [&]() {
+    for (int r = 0; r < ranks; ++r) PE_HIP_CHECK(hipEventRecord(ev[r], s[r]->stream()));
+    for (int r = 1; r < ranks; ++r) PE_HIP_CHECK(hipStreamWaitEvent(s0, ev[r], 0));
+  };
+  auto fork_all = [&]() {
+    PE_HIP_CHECK(hipEventRecord(ev[0], s0));
+    for (int r = 1; r < ranks; ++r) PE_HIP_CHECK(hipStreamWaitEvent(s[r]->stream(), ev[0], 0));
+  };
+  auto reduce = [&](double* const* table, int n, int is_max) {
+    join_all();
+    dev::launch_group_reduce(table, ranks, n, is_max, s0);
+    fork_all();
+  };
+  auto exchange = [&]() {
+    for (int r = 0; r < ranks; ++r) PE_HIP_CHECK(hipEventRecord(ev[r], s[r]->stream()));
+    for (int r = 0; r < ranks; ++r)
+      for (const auto& e : plan[r]) {
+        const auto& peer = plan[e.peer];
+        const Exchange* src = nullptr;
+        for (const auto& pe : peer)
+          if (pe.dir == opposite(e.dir)) src = &pe;
+        if (!src || src->count != e.count) throw std::runtime_error("group halo plan mismatch");
+        PE_HIP_CHECK(hipStreamWaitEvent(s[r]->stream(), ev[e.peer], 0));
+        PE_HIP_CHECK(hipMemcpyAsync(e.recv, src->send, sizeof(double) * e.count, hipMemcpyDeviceToDevice,
+                                    s[r]->stream()));
+      }
+  };
+  (void)err1;
+
+  for (int r = 0; r < ranks; ++r) s[r]->enqueue_init();
+  exchange();
+  reduce(dp + ranks, 1, 0);
+  PE_HIP_CHECK(hipStreamSynchronize(s0));
+  SolveResult res;
+  res.t.setup = secs(t_start, clk::now());
+  const auto t_loop = clk::now();
+  const int64_t cap = P.iter_cap();
+  const int chunk = s[0]->chunk();
+  DevState hs;
+  int64_t k = 0;
+  for (;;) {
+    for (int it = 0; it < chunk; ++it, ++k) {
+      const int par = int(k & 1);
+      for (int r = 0; r < ranks; ++r) s[r]->enqueue_F(par);
+      reduce(dp, 2, 0);
+      for (int r = 0; r < ranks; ++r) s[r]->enqueue_G(par);
+      exchange();
+      reduce(dp + ranks, 1, 0);
+    }
+    s[0]->read_state(&hs);
+    if (hs.done || k >= cap) break;
+  }
+  for (int r = 0; r < ranks; ++r) s[r]->synchronize();
+  res.t.iterate = secs(t_loop, clk::now());
+  res.t.gpu = res.t.iterate;
+  if (opt.compute_error) {
+    for (int r = 0; r < ranks; ++r) s[r]->enqueue_error();
+    reduce(dp + 2 * ranks, 1, 0);
+    // max over the two max slots: table entries point at err[0]; offset by one.
+    std::vector<double*> hm(ranks);
+    for (int r = 0; r < ranks; ++r) hm[r] = s[r]->err_dev() + 1;
+    double** dm = nullptr;
+    PE_HIP_CHECK(hipMalloc(&dm, sizeof(double*) * ranks));
+    PE_HIP_CHECK(hipMemcpy(dm, hm.data(), sizeof(double*) * ranks, hipMemcpyHostToDevice));
+    reduce(dm, 2, 1);
+    PE_HIP_CHECK(hipStreamSynchronize(s0));
+    PE_HIP_CHECK(hipFree(dm));
+  }
+  for (int r = 0; r < ranks; ++r) s[r]->synchronize();
+  s[0]->read_state(&hs);
+  res.iters = hs.iter;
+  res.converged = hs.status == 1;
+  res.breakdown = hs.status == 2;
+  res.last_diff = hs.last_diff;
+  res.zr = hs.rz_cur;
+  if (opt.compute_error) {
+    res.l2_err = std::sqrt(hs.err[0] * P.h1() * P.h2());
+    res.max_err = hs.err[1];
+    res.max_outside = hs.err[2];
+  }
+  if (w_out) {
+    const int64_t ny = P.N - 1;
+    w_out->assign(size_t((P.M - 1) * ny), 0.0);
+    for (int r = 0; r < ranks; ++r) {
+      const Block& b = blks[r];
+      std::vector<double> tmp(size_t(b.nx * b.ny));
+      s[r]->copy_w(tmp.data());
+      for (int64_t li = 0; li < b.nx; ++li)
+        std::copy(tmp.begin() + li * b.ny, tmp.begin() + (li + 1) * b.ny,
+                  w_out->begin() + (b.i0 - 1 + li) * ny + (b.j0 - 1));
+    }
+  }
+  PE_HIP_CHECK(hipFree(dp));
+  for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
+  res.backend = "hip-group";
+  res.Px = pg.Px;
+  res.Py = pg.Py;
+  res.t.solver = secs(t_start, clk::now());
+  return res;
+}
+
+}  // namespace pe

@@ -1,0 +1,83 @@
+// Host-visible interface of the gfx950 kernels (kernels.hip).  Plain C++ so
+// the host runtime (compiled by g++) can launch them.
+//
+// Per-iteration device work (replaces the reference's 7 kernels K1-K7,
+// poisson_mpi_cuda2.cu:507-676, and its host-side dot finalizers C16/C17):
+//
+//   F  (pcg_dir_stencil):  p_k = D⁻¹r_k + β_{k-1} p_{k-1}     (owned + halo ring)
+//                          S_den += (A p_k)·p_k,  S_pp += p_k·p_k
+//   G  (pcg_update):       α_k = (z,r)_{k-1} / den_k ; stop test on α²·S_pp
+//                          w += α p_k ; r -= α A p_k (A p_k recomputed)
+//                          S_zr += (D⁻¹r)·r ; strided halo strips → send buffers
+//
+// Both kernels march down i in column strips (wave64 lanes along contiguous
+// j), keep the 3-row stencil window in registers + one LDS row, compute the
+// fictitious-domain coefficients on the fly from two 1-D chord tables (no
+// a/b/D arrays in HBM), and finish their dot products with a deterministic
+// last-workgroup reduction into a device scalar.  Scalars (α, β, the
+// convergence flag, the iteration count) never leave the device.
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <cstdint>
+
+namespace pe {
+namespace dev {
+
+// Device-resident solver state (one per rank).
+struct DevState {
+  double red_F[2];   // Σ(Ap·p), Σ(p·p) — local, then global after allreduce
+  double red_G[2];   // Σ(z·r) — local, then global; [1] pad
+  double err[4];     // Σ(w-u)² in D, max|w-u| in D, max|w| outside D, pad
+  double rz_cur;     // (z, r) of the previous iteration, h-weighted
+  double alpha, beta, last_diff;
+  long long iter;    // completed iterations
+  int done;          // 1 → every later kernel is a no-op
+  int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap
+  unsigned ticket[4];
+  unsigned pad[4];
+};
+
+// Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
+// lj ∈ [0, ny+1], element = base + li*pitch + lj.
+struct KParams {
+  int64_t nx, ny, pitch;
+  int M, N;
+  int64_t gi0, gj0;              // global index of local (0, 0)  (= i0-1, j0-1)
+  double A1, A2, h1, h2, eps, inv_eps, h1sq, h2sq, nih1, nih2;
+  double cx, cy, F, u_scale;
+  double tol;
+  int weighted;
+  long long max_iter;
+  int has[4];                    // neighbour present (LEFT, RIGHT, DOWN, UP)
+  const double* colT;            // (nx+4) × 4: {halfA, sB, eB, x} at index li+1
+  const double* rowT;            // (ny+4) × 4: {sA, eA, halfB, y} at index lj+1
+  double* r;
+  double* w;
+  double* p[2];
+  double* send_dn; double* send_up;        // y-direction (strided) send strips, nx each
+  const double* recv_dn; const double* recv_up;
+  double* partial;               // ≥ 2 × blocks doubles
+  DevState* st;
+  int ti;                        // rows per marching block
+  int check_tol;                 // 0 → never stop on ‖Δw‖ (fixed-iteration runs)
+};
+
+constexpr int kTJ = 256;         // strip width = threads per block (4 waves)
+constexpr int kTImax = 64;       // max rows per marching block
+
+void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp,
+                 hipStream_t s);
+void launch_F(const KParams& k, int par, int variant, hipStream_t s);
+void launch_G(const KParams& k, int par, int variant, hipStream_t s);
+void launch_error(const KParams& k, hipStream_t s);
+// Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
+void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);
+// Debug/test ops (single-shot, no convergence logic).
+void launch_apply_A(const KParams& k, const double* p, double* Ap, hipStream_t s);
+void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t s);
+int grid_blocks(const KParams& k);
+
+}  // namespace dev
+}  // namespace pe

@@ -1,0 +1,58 @@
+// 2D block decomposition of the interior unknowns i = 1..M-1, j = 1..N-1
+// over a Px × Py process grid, plus the field memory layout.
+//
+// Reference parity:
+//   choose_process_grid   stage2-mpi/poisson_mpi_decomp.cpp:60-64 (DecompMode::Reference)
+//   decompose_2d          stage2-mpi/poisson_mpi_decomp.cpp:75-111 (identical partition)
+//   neighbour map         stage2-mpi/poisson_mpi_decomp.cpp:246-252
+// New: DecompMode::Aspect chooses Px×Py by minimising per-rank halo cost
+// (contiguous x-direction rows are cheaper than strided y-direction columns)
+// instead of ignoring the grid aspect (reference quirk A17).  All indices are
+// 64-bit (reference quirk A11: 32-bit `int idx` overflows past ~46k² blocks).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+namespace pe {
+
+enum class DecompMode : int { Reference = 0, Aspect = 1 };
+
+struct ProcessGrid {
+  int Px = 1, Py = 1;
+};
+
+// Direction indices: x-neighbours exchange contiguous rows (fixed i),
+// y-neighbours exchange strided columns (fixed j).
+enum Dir : int { LEFT = 0, RIGHT = 1, DOWN = 2, UP = 3 };
+inline int opposite(int d) { return d ^ 1; }
+
+struct Block {
+  int rank = 0, size = 1;
+  int Px = 1, Py = 1, px = 0, py = 0;
+  int64_t i0 = 1, i1 = 0, j0 = 1, j1 = 0;  // owned global interior range, inclusive
+  int64_t nx = 0, ny = 0;                  // owned extents
+  int64_t pitch = 0;                       // elements per local row li (>= ny + 2)
+  int64_t rows = 0;                        // nx + 2 local rows (halo included)
+  int64_t base = 0;                        // element offset of (li=0, lj=0) in the allocation
+  int64_t alloc = 0;                       // allocation length in elements
+  int nbr[4] = {-1, -1, -1, -1};           // neighbour rank or -1 at the global boundary
+
+  // Element offset of local (li, lj); li ∈ [0, nx+1], lj ∈ [0, ny+1].
+  int64_t at(int64_t li, int64_t lj) const { return base + li * pitch + lj; }
+  bool has(int d) const { return nbr[d] >= 0; }
+};
+
+ProcessGrid choose_process_grid(int P, int M, int N, DecompMode mode);
+ProcessGrid choose_process_grid_reference(int P);
+
+// `align` = alignment (in elements) of each row's first owned element (lj=1).
+Block decompose(int M, int N, const ProcessGrid& pg, int rank, int align = 8);
+
+// Halo cost model used by DecompMode::Aspect (exposed for tests/docs).
+double halo_cost(int M, int N, int Px, int Py);
+
+std::string describe(const Block& b);
+
+}  // namespace pe

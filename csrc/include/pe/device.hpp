@@ -1,0 +1,140 @@
+// Device (MI355X) runtime: stream-ordered communication + the device-resident
+// PCG solver.  Replaces the stage-4 driver gradient_solver_mpi
+// (poisson_mpi_cuda2.cu:687-982) and its host-staged halo exchange
+// exchange_halos_2d_gpu (:331-500).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "pe/comm.hpp"
+#include "pe/solver.hpp"
+
+#define PE_HIP_CHECK(expr)                                                                     \
+  do {                                                                                         \
+    hipError_t _e = (expr);                                                                    \
+    if (_e != hipSuccess) ::pe::hip_fail(_e, #expr, __FILE__, __LINE__);                       \
+  } while (0)
+
+namespace pe {
+
+[[noreturn]] void hip_fail(hipError_t e, const char* expr, const char* file, int line);
+int device_count();
+void set_device(int dev);
+std::string device_name(int dev);
+
+// Stream-ordered transport over device buffers.
+class DeviceComm {
+ public:
+  virtual ~DeviceComm() = default;
+  virtual int rank() const = 0;
+  virtual int size() const = 0;
+  virtual void allreduce_sum(double* dbuf, int n, hipStream_t s) = 0;
+  virtual void allreduce_max(double* dbuf, int n, hipStream_t s) = 0;
+  virtual void exchange(const std::vector<Exchange>& ex, hipStream_t s) = 0;
+  // Host-side max of a few doubles (timer reduction); may synchronize.
+  virtual void host_max(double* hbuf, int n, hipStream_t s) = 0;
+  virtual void barrier(hipStream_t s) = 0;
+  virtual bool capturable() const { return false; }
+  virtual std::string name() const = 0;
+};
+
+class SelfDeviceComm final : public DeviceComm {
+ public:
+  int rank() const override { return 0; }
+  int size() const override { return 1; }
+  void allreduce_sum(double*, int, hipStream_t) override {}
+  void allreduce_max(double*, int, hipStream_t) override {}
+  void exchange(const std::vector<Exchange>&, hipStream_t) override {}
+  void host_max(double*, int, hipStream_t) override {}
+  void barrier(hipStream_t) override {}
+  bool capturable() const override { return true; }
+  std::string name() const override { return "self"; }
+};
+
+// RCCL (NCCL API) over xGMI.  The 128-byte unique id is produced by rank 0
+// (rccl_unique_id) and distributed by the caller (torch.distributed store,
+// or the pe_launch bootstrap file).
+std::string rccl_unique_id();
+std::unique_ptr<DeviceComm> make_rccl_comm(const std::string& uid, int rank, int size);
+// Wrap an existing ncclComm_t (e.g. one owned by another runtime); not owned.
+std::unique_ptr<DeviceComm> make_rccl_comm_from_handle(void* nccl_comm);
+
+namespace dev {
+struct DevState;
+struct KParams;
+}  // namespace dev
+
+class DeviceSolver {
+ public:
+  DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* comm, const SolveOptions& opt);
+  ~DeviceSolver();
+  DeviceSolver(const DeviceSolver&) = delete;
+  DeviceSolver& operator=(const DeviceSolver&) = delete;
+
+  // Full solve: init + iterations until convergence / cap + error.
+  SolveResult solve();
+  // Benchmark helpers: reset to the initial state, then run exactly `iters`
+  // iterations (convergence test off when check_tol == false).
+  void reset();
+  void run_iterations(int64_t iters, bool use_graph);
+  double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
+  void synchronize();
+
+  // Phases (used by the virtual-rank group driver and tests).
+  void enqueue_init();
+  void enqueue_F(int par);
+  void enqueue_G(int par);
+  void enqueue_error();
+  double* red_F_dev();
+  double* red_G_dev();
+  double* err_dev();
+  std::vector<Exchange> halo_plan() const;  // device pointers of this rank's strips
+  hipStream_t stream() const { return stream_; }
+
+  // State / data access.
+  void read_state(dev::DevState* out);
+  void copy_w(double* host, bool owned_only = true);  // nx × ny row-major
+  void copy_field(int which, double* host);            // 0 r, 1 w, 2 p0, 3 p1: full (rows × pitch)
+  const Block& block() const { return blk_; }
+  const Problem& problem() const { return prob_; }
+  int chunk() const { return chunk_; }
+  dev::KParams& params();
+
+ private:
+  void build_tables();
+  void enqueue_iteration(int par);
+  void enqueue_chunk(int iters);
+  bool graph_ready(int iters);
+
+  Problem prob_;
+  Block blk_;
+  DeviceComm* comm_;
+  std::unique_ptr<DeviceComm> self_;
+  SolveOptions opt_;
+  hipStream_t stream_ = nullptr;
+  double* fields_ = nullptr;  // r, w, p0, p1 (alloc each)
+  double* tables_ = nullptr;
+  double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each)
+  double* partial_ = nullptr;
+  dev::DevState* st_ = nullptr;
+  dev::DevState* hst_ = nullptr;  // pinned, 2 slots
+  std::unique_ptr<dev::KParams> kp_;
+  hipGraphExec_t graph_ = nullptr;
+  int graph_iters_ = 0;
+  int chunk_ = 16;
+  hipEvent_t ev_[2] = {nullptr, nullptr};
+  hipEvent_t t0_ = nullptr, t1_ = nullptr;
+};
+
+// P virtual ranks on ONE device (LocalComm).  Every rank runs the
+// same kernels and the same halo plan as under RCCL; the transport is
+// device-to-device copies + a cross-stream reduction kernel.
+SolveResult device_solve_group(const Problem& prob, int ranks, DecompMode mode, const SolveOptions& opt,
+                               std::vector<double>* w_out = nullptr);
+
+}  // namespace pe

@@ -1,0 +1,82 @@
+// Solver options / results shared by every backend.
+//
+// Reference solvers: stage0 `solve` (Withoutopenmp1.cpp:106-172), stage1
+// OpenMP `solve` (Withopenmp1.cpp:133-199), stage2/3 `solve_mpi`
+// (poisson_mpi_decomp.cpp:356-460, main_hybrid.cpp:364-470) and the stage4
+// GPU driver `gradient_solver_mpi` (poisson_mpi_cuda2.cu:687-982).  All of
+// them are Jacobi-preconditioned CG with the stop rule ‖w^{k+1}-w^k‖_E < δ.
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "pe/comm.hpp"
+#include "pe/decomp.hpp"
+#include "pe/problem.hpp"
+
+namespace pe {
+
+// Stage timers (seconds, this rank).  Categories follow the reference's
+// stage-4 printout (poisson_mpi_cuda2.cu:968-979) with honest semantics:
+//   gpu     — device kernel time (stencil/update kernels, incl. fused prec/dot)
+//   copy    — host<->device copies (≈0: everything is device-resident)
+//   halo    — halo exchange (P2P) time
+//   reduce  — global allreduce time (the reference lumps this into "MPI")
+//   prec    — preconditioner time (separately timed on CPU; fused on GPU)
+//   dot     — local dot-product time (separately timed on CPU; fused on GPU)
+//   setup   — assembly / allocation before the first iteration
+//   solver  — wall time of the whole solve (setup + iterations + teardown)
+struct Timers {
+  double gpu = 0, copy = 0, halo = 0, reduce = 0, prec = 0, dot = 0, setup = 0, solver = 0;
+  double iterate = 0;  // wall time of the iteration loop only
+};
+
+struct SolveOptions {
+  Init init = Init::Zero;
+  uint64_t seed = 1234;
+  double init_amp = 0.05;
+  int threads = 1;           // CPU backends: OpenMP threads per rank
+  int log_every = 0;         // >0: print ‖Δw‖ every K iterations (rank 0)
+  bool keep_history = false; // record ‖Δw‖ of every iteration
+  bool compute_error = true; // L2 / max error against the analytic solution
+  bool verbose = false;
+  // Device backend knobs.
+  int chunk = 0;             // iterations enqueued per host check (0 = auto)
+  bool use_graph = true;     // capture a chunk of iterations into a hipGraph
+  bool timing = false;       // per-phase hipEvent timing (adds host sync)
+  bool check_tol = true;     // false: never stop on ‖Δw‖ (fixed-iteration benchmarking)
+  int variant = 0;           // device kernel variant (0 = default fused marching)
+};
+
+struct SolveResult {
+  int64_t iters = 0;
+  bool converged = false;
+  bool breakdown = false;
+  double last_diff = 0;  // ‖w^{k+1}-w^k‖ at the last iteration
+  double zr = 0;         // final (z, r)
+  Timers t;
+  double l2_err = -1, max_err = -1, max_outside = -1;
+  std::vector<double> history;
+  int Px = 1, Py = 1;
+  std::string backend;
+};
+
+// ---- CPU backends (reference stage0..3 equivalents) -----------------------
+// Reference-faithful PCG on one block of the decomposition; `comm` supplies
+// halo exchange + reductions (SelfHostComm for serial/OpenMP runs).  When
+// `w_out` is non-null the owned block of w is copied out row-major (nx × ny).
+SolveResult cpu_pcg(const Problem& prob, const Block& blk, HostComm& comm,
+                    const SolveOptions& opt, std::vector<double>* w_out = nullptr);
+
+// Run P thread-ranks (ThreadHostComm) × `opt.threads` OpenMP threads each and
+// return rank 0's result; `w_out` receives the gathered global interior
+// ((M-1) × (N-1), row-major in i) when non-null.
+SolveResult cpu_pcg_threads(const Problem& prob, int ranks, DecompMode mode,
+                            const SolveOptions& opt, std::vector<double>* w_out = nullptr);
+
+// Legacy-format report lines (reference stdout formats, §2.9 of SURVEY).
+std::string format_result_legacy(const Problem& prob, const SolveResult& r, int nranks,
+                                 const std::string& stage);
+
+}  // namespace pe
