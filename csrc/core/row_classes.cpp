@@ -1,0 +1,116 @@
+// Per-row coefficient class intervals for the on-the-fly fictitious-domain
+// coefficients (used by the gfx950 kernels).
+//
+// For local row q the kernels need a(q,j), a(q+1,j), b(q,j), b(q,j+1).
+// A vertical face {x = c, y ∈ [s_j, e_j]} lies fully inside D iff
+// s_j ≥ -half(q) and e_j ≤ half(q) (half = ellipse chord half-width at c);
+// then chord_len = e_j - s_j ≈ h2 and face_coef returns exactly 1.  It is
+// fully outside iff e_j ≤ -half or s_j ≥ half; then chord_len = 0 and
+// face_coef returns exactly 1/eps.  s_j, e_j are monotone in j, and the
+// horizontal-face half-width halfB(j) is unimodal in j, so every such set is
+// an interval found by binary search: O(nx log ny) setup instead of the
+// reference's O(nx·ny) coefficient arrays (fic_reg_local,
+// stage2-mpi/poisson_mpi_decomp.cpp:124-170).  The intervals are
+// conservative — anything not provably interior/exterior is classified
+// "boundary band" and evaluated exactly — so the classification never
+// changes a coefficient value.
+#include <algorithm>
+#include <climits>
+#include <vector>
+
+#include "pe/device.hpp"
+
+namespace pe {
+namespace {
+
+struct Iv {
+  int64_t lo = 1, hi = 0;  // empty when lo > hi
+  bool empty() const { return lo > hi; }
+};
+
+Iv meet(Iv a, Iv b) { return Iv{std::max(a.lo, b.lo), std::min(a.hi, b.hi)}; }
+Iv shift(Iv a, int64_t d) { return a.empty() ? a : Iv{a.lo + d, a.hi + d}; }
+
+// First index in [lo, hi] where pred turns true (pred monotone F..T); hi+1 if never.
+template <class P>
+int64_t first_true(int64_t lo, int64_t hi, P pred) {
+  int64_t a = lo, b = hi + 1;
+  while (a < b) {
+    const int64_t m = a + (b - a) / 2;
+    if (pred(m)) b = m;
+    else a = m + 1;
+  }
+  return a;
+}
+// Last index in [lo, hi] where pred is true (pred monotone T..F); lo-1 if never.
+template <class P>
+int64_t last_true(int64_t lo, int64_t hi, P pred) {
+  int64_t a = lo - 1, b = hi;
+  while (a < b) {
+    const int64_t m = b - (b - a) / 2;
+    if (pred(m)) a = m;
+    else b = m - 1;
+  }
+  return a;
+}
+
+}  // namespace
+
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx, int64_t ny) {
+  const int64_t L = -1, H = ny + 2;  // row-table index range
+  auto sA = [&](int64_t j) { return rowT[(j + 1) * 4 + 0]; };
+  auto eA = [&](int64_t j) { return rowT[(j + 1) * 4 + 1]; };
+  auto hB = [&](int64_t j) { return rowT[(j + 1) * 4 + 2]; };
+  // Peak of the unimodal halfB(j).
+  int64_t peak = L;
+  for (int64_t j = L; j <= H; ++j)
+    if (hB(j) > hB(peak)) peak = j;
+
+  auto a_in = [&](int64_t q) {
+    const double half = colT[(q + 1) * 4 + 0];
+    if (half < 0) return Iv{};
+    return Iv{first_true(L, H, [&](int64_t j) { return sA(j) >= -half; }),
+              last_true(L, H, [&](int64_t j) { return eA(j) <= half; })};
+  };
+  auto a_notout = [&](int64_t q) {
+    const double half = colT[(q + 1) * 4 + 0];
+    if (half < 0) return Iv{};
+    return Iv{first_true(L, H, [&](int64_t j) { return eA(j) > -half; }),
+              last_true(L, H, [&](int64_t j) { return sA(j) < half; })};
+  };
+  // {j : halfB(j) ≥ T} (strict: >) for the unimodal halfB.
+  auto b_level = [&](double T, bool strict) {
+    auto ok = [&](int64_t j) { return strict ? hB(j) > T : hB(j) >= T; };
+    if (!ok(peak)) return Iv{};
+    return Iv{first_true(L, peak, ok), last_true(peak, H, ok)};
+  };
+  auto b_in = [&](int64_t q) {
+    const double sB = colT[(q + 1) * 4 + 1], eB = colT[(q + 1) * 4 + 2];
+    return b_level(std::max(-sB, eB), false);
+  };
+  auto b_notout = [&](int64_t q) {
+    const double sB = colT[(q + 1) * 4 + 1], eB = colT[(q + 1) * 4 + 2];
+    return b_level(std::max(-eB, sB), true);
+  };
+
+  std::vector<int> out(size_t(nx + 4) * 4, 0);
+  for (int64_t q = -1; q <= nx + 1; ++q) {
+    const Iv bi = b_in(q);
+    const Iv in = meet(meet(a_in(q), a_in(q + 1)), meet(bi, shift(bi, -1)));
+    const Iv bn = b_notout(q);
+    int64_t olo = INT_MAX / 2, ohi = INT_MIN / 2;
+    for (const Iv& v : {a_notout(q), a_notout(q + 1), bn, shift(bn, -1)})
+      if (!v.empty()) {
+        olo = std::min(olo, v.lo);
+        ohi = std::max(ohi, v.hi);
+      }
+    int* o = out.data() + (q + 1) * 4;
+    o[0] = in.empty() ? 1 : int(in.lo);
+    o[1] = in.empty() ? 0 : int(in.hi);
+    o[2] = int(olo);
+    o[3] = int(ohi);
+  }
+  return out;
+}
+
+}  // namespace pe

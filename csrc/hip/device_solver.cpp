@@ -44,6 +44,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * A * 4));
   const int64_t ntab = (blk_.nx + 4) * 4 + (blk_.ny + 4) * 4;
   PE_HIP_CHECK(hipMalloc(&tables_, sizeof(double) * ntab));
+  PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * (blk_.nx + 4) * 4));
   PE_HIP_CHECK(hipMalloc(&halo_, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4));
   PE_HIP_CHECK(hipMalloc(&st_, sizeof(DevState)));
   PE_HIP_CHECK(hipHostMalloc(&hst_, sizeof(DevState) * 2, hipHostMallocDefault));
@@ -81,6 +82,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.max_iter = prob_.iter_cap();
   for (int d = 0; d < 4; ++d) k.has[d] = blk_.has(d) ? 1 : 0;
   k.colT = tables_;
+  k.rowcls = rowcls_;
   k.rowT = tables_ + (blk_.nx + 4) * 4;
   k.r = fields_ + blk_.base;
   k.w = fields_ + A + blk_.base;
@@ -93,16 +95,30 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.recv_up = halo_ + 3 * hx;
   k.st = st_;
   k.check_tol = opt_.check_tol ? 1 : 0;
-  // Rows per marching block: enough blocks to fill 256 CUs several times
-  // over, long enough strips to amortise the 2 redundant halo rows.
-  int ti = 32;
-  const int64_t strips = (blk_.ny + dev::kTJ - 1) / dev::kTJ;
-  while (ti > 8 && strips * ((blk_.nx + ti - 1) / ti) < 2048) ti /= 2;
+  // Work decomposition: 128-column wave strips × `ti`-row chunks, dealt to a
+  // persistent grid.  ti is the largest of 64/32/16/8 that still yields
+  // ≥ 4096 items (≥ 16 waves per CU on 256 CUs); waves get equal item counts.
+  const int64_t strips = (blk_.ny + dev::kSW - 1) / dev::kSW;
+  int ti = 64;
+  while (ti > 8 && strips * ((blk_.nx + ti - 1) / ti) < 4096) ti /= 2;
   if (const char* e = std::getenv("PE_TI")) ti = std::max(1, std::min(dev::kTImax, std::atoi(e)));
   k.ti = ti;
-  const int64_t npart = std::max<int64_t>(2 * int64_t(dev::grid_blocks(k)), 3 * 4096);
+  k.nstrips = int(strips);
+  k.nitems = int(strips * ((blk_.nx + ti - 1) / ti));
+  int wave_cap = 256 * 16;
+  if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
+  const int per = (k.nitems + wave_cap - 1) / wave_cap;
+  const int waves = (k.nitems + per - 1) / per;
+  k.nblocks = std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
+  const int64_t npart = std::max<int64_t>(3 * int64_t(k.nblocks), 3 * 4096);
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * npart));
   k.partial = partial_;
+  k.ih1sq = 1.0 / k.h1sq;
+  k.ih2sq = 1.0 / k.h2sq;
+  k.D_in = (1.0 + 1.0) / k.h1sq + (1.0 + 1.0) / k.h2sq;
+  k.D_out = (k.inv_eps + k.inv_eps) / k.h1sq + (k.inv_eps + k.inv_eps) / k.h2sq;
+  k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
+  k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables();
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
@@ -122,6 +138,7 @@ DeviceSolver::~DeviceSolver() {
   (void)hipEventDestroy(t1_);
   (void)hipFree(fields_);
   (void)hipFree(tables_);
+  (void)hipFree(rowcls_);
   (void)hipFree(halo_);
   (void)hipFree(partial_);
   (void)hipFree(st_);
@@ -156,6 +173,8 @@ void DeviceSolver::build_tables() {
     r[3] = y;
   }
   PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
+  const std::vector<int> rc = row_classes(col, row, blk_.nx, blk_.ny);
+  PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
 }
 
 std::vector<Exchange> DeviceSolver::halo_plan() const {
@@ -180,7 +199,7 @@ void DeviceSolver::enqueue_init() {
   PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * A * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
-  dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, stream_);
+  dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
   PE_HIP_CHECK(hipGetLastError());
 }
 

@@ -12,18 +12,23 @@
 //   kG  (stop test ⊕ w,r update ⊕ recomputed stencil ⊕ (z,r) dot)
 //                                        reads p_k, r, w; writes r, w
 //
-// Layout: row-major, j (y) contiguous, rows padded to 64 B.  A block of
-// 256 threads (4 wave64s) owns a strip of 256 consecutive j and marches
-// down `ti` rows of i.  Each thread keeps the i-1 / i / i+1 values of its
-// own column in registers, the row's j±1 neighbours come from a
-// double-buffered LDS row (one barrier per row), and the two strip-edge
-// columns are produced once per block in a prologue.  The face
-// coefficients a_ij, b_ij and the Jacobi diagonal D_ij are recomputed from
-// two 1-D chord tables, which costs ALU (idle in this HBM-bound loop) and
-// saves 3-4 array streams of HBM traffic.  Dot products end in a
-// deterministic last-workgroup reduction (agent-scope release/acquire
-// ticket; partials summed in block order), so results are bitwise
-// reproducible run to run.
+// Execution shape (measured: the first LDS-row version spent 85 % of its
+// wave cycles in s_waitcnt/s_barrier — latency-bound, not HBM- or
+// ALU-bound).  Every wave64 is independent: it owns a strip of 128
+// consecutive j (2 per lane, 16-byte loads/stores) and marches down ≤ 64
+// rows of i with the NEXT TWO rows' loads already in flight.  The i±1
+// stencil neighbours stay in registers, j±1 come from DPP wave shifts
+// (v_mov_b32_dpp wave_shl/shr:1), and the two strip-edge columns are
+// computed once per work item, one row per lane, and broadcast with
+// v_readlane — no LDS and no barrier inside the loop.  Work items
+// (strip × row chunk) are dealt to a persistent grid.
+//
+// Coefficients are never stored: a per-row class table (interior interval,
+// exterior hull) gives a_ij = b_ij = 1 or 1/eps with two integer compares;
+// only the boundary band evaluates the fictitious-domain face lengths from
+// the 1-D chord tables.  Dot products end in a deterministic last-workgroup
+// reduction (agent-scope release/acquire ticket; partials summed in block
+// order), so results are bitwise reproducible run to run.
 #include <hip/hip_runtime.h>
 
 #include "kernels.hpp"
@@ -36,6 +41,15 @@ namespace dev {
 namespace {
 
 constexpr int TJ = kTJ;
+constexpr int SW = kSW;
+
+// Read-only table access through the constant address space: uniform
+// addresses lower to s_load (lgkmcnt), so a table read inside the marching
+// loop never waits on the vector-memory prefetch queue (vmcnt).
+template <class T>
+__device__ __forceinline__ T cload(const T* p) {
+  return *(const __attribute__((address_space(4))) T*)((uintptr_t)p);
+}
 
 __device__ __forceinline__ double fcoef(double l, double h, double eps, double inv_eps) {
   if (fabs(l - h) < 1e-9) return 1.0;
@@ -43,62 +57,91 @@ __device__ __forceinline__ double fcoef(double l, double h, double eps, double i
   return (l / h) + (1.0 - l / h) / eps;
 }
 
-struct RowV {
-  double sA, eA, halfB, halfB1;  // own column j: face y-range, chord of b_{·,j} and b_{·,j+1}
+// Per-column chord-table values of one node column lj: the vertical-face
+// y-range (sA, eA) and the horizontal-face half-widths of columns lj, lj+1.
+// Kept in registers by the marching kernels (no table loads in the loop).
+struct TV {
+  double sA, eA, hB, hB1;
+};
+__device__ __forceinline__ TV tv_at(const KParams& k, int64_t lj) {
+  const double* t = k.rowT + (lj + 1) * 4;
+  return TV{t[0], t[1], t[2], t[6]};
+}
+
+// a_{q, lj}: vertical face left of node q.  colT is indexed by the
+// wave-uniform row q → scalar loads, which do not drain vector-memory prefetch.
+__device__ __forceinline__ double coefA(const KParams& k, int64_t q, const TV& t) {
+  const double half = cload(k.colT + (q + 1) * 4 + 0);
+  return fcoef(chord_len(half, t.sA, t.eA), k.h2, k.eps, k.inv_eps);
+}
+// b_{q, ·}: horizontal face below the node, chord half-width `half`.
+__device__ __forceinline__ double coefB(const KParams& k, int64_t q, double half) {
+  const double sB = cload(k.colT + (q + 1) * 4 + 1);
+  const double eB = cload(k.colT + (q + 1) * 4 + 2);
+  return fcoef(chord_len(half, sB, eB), k.h1, k.eps, k.inv_eps);
+}
+
+// Coefficients of node (q, lj): a(q), a(q+1), b(q, lj), b(q, lj+1), and the
+// Jacobi diagonal (EXACT: D, used as r / D; fast: 1/D, used as r * dinv).
+struct CS {
+  double a0, a1, b0, b1, d;
 };
 
-__device__ __forceinline__ RowV rowv(const KParams& k, int64_t lj) {
-  const double* t = k.rowT + (lj + 1) * 4;
-  RowV v;
-  v.sA = t[0];
-  v.eA = t[1];
-  v.halfB = t[2];
-  v.halfB1 = t[6];  // halfB of lj + 1
-  return v;
+template <bool EXACT>
+__device__ __forceinline__ CS cset(const KParams& k, const int* rc, int64_t q, int64_t lj, const TV& t) {
+  CS c;
+  const int in_lo = cload(rc), in_hi = cload(rc + 1), out_lo = cload(rc + 2), out_hi = cload(rc + 3);
+  if (lj >= in_lo && lj <= in_hi) {  // interior: every face fully inside D
+    c.a0 = c.a1 = c.b0 = c.b1 = 1.0;
+    c.d = EXACT ? k.D_in : k.dinv_in;
+  } else if (lj < out_lo || lj > out_hi) {  // exterior: every face fully outside D
+    c.a0 = c.a1 = c.b0 = c.b1 = k.inv_eps;
+    c.d = EXACT ? k.D_out : k.dinv_out;
+  } else {  // boundary band: evaluate the face lengths
+    c.a0 = coefA(k, q, t);
+    c.a1 = coefA(k, q + 1, t);
+    c.b0 = coefB(k, q, t.hB);
+    c.b1 = coefB(k, q, t.hB1);
+    // D = (a_{i+1} + a_i)/h1² + (b_{j+1} + b_j)/h2²  (reference mat_D, same order)
+    if constexpr (EXACT) c.d = (c.a1 + c.a0) / k.h1sq + (c.b1 + c.b0) / k.h2sq;
+    else c.d = 1.0 / ((c.a1 + c.a0) * k.ih1sq + (c.b1 + c.b0) * k.ih2sq);
+  }
+  return c;
 }
-
-// a_{q, j}: vertical face left of node q.
-__device__ __forceinline__ double coefA(const KParams& k, int64_t q, const RowV& rv) {
-  const double half = k.colT[(q + 1) * 4 + 0];
-  return fcoef(chord_len(half, rv.sA, rv.eA), k.h2, k.eps, k.inv_eps);
-}
-// b_{q, j} (halfB) or b_{q, j+1} (halfB1): horizontal face below the node.
-__device__ __forceinline__ double coefB(const KParams& k, int64_t q, double halfB) {
-  const double sB = k.colT[(q + 1) * 4 + 1];
-  const double eB = k.colT[(q + 1) * 4 + 2];
-  return fcoef(chord_len(halfB, sB, eB), k.h1, k.eps, k.inv_eps);
+template <bool EXACT>
+__device__ __forceinline__ CS cset_mem(const KParams& k, int64_t q, int64_t lj) {
+  return cset<EXACT>(k, k.rowcls + (q + 1) * 4, q, lj, tv_at(k, lj));
 }
 
 template <bool EXACT>
-__device__ __forceinline__ double diag(const KParams& k, double a0, double a1, double b0, double b1) {
-  // D = (a_{i+1} + a_i)/h1² + (b_{j+1} + b_j)/h2²  (reference mat_D, same order)
-  if constexpr (EXACT) return (a1 + a0) / k.h1sq + (b1 + b0) / k.h2sq;
-  else return (a1 + a0) * (1.0 / k.h1sq) + (b1 + b0) * (1.0 / k.h2sq);
+__device__ __forceinline__ double zval(const CS& c, double r) {
+  if constexpr (EXACT) return (c.d != 0.0) ? r / c.d : 0.0;
+  else return r * c.d;
 }
 
 template <bool EXACT>
-__device__ __forceinline__ double stencil(const KParams& k, double pm, double p0, double pn, double pl,
-                                          double pr, double a0, double a1, double b0, double b1) {
-  // Reference apply_A (poisson_mpi_cuda2.cu:526-535), same expression tree.
+__device__ __forceinline__ double stencil(const KParams& k, const CS& c, double pm, double p0, double pn, double pl,
+                                          double pr) {
   if constexpr (EXACT) {
-    const double Ax = k.nih1 * (a1 * (pn - p0) / k.h1 - a0 * (p0 - pm) / k.h1);
-    const double Ay = k.nih2 * (b1 * (pr - p0) / k.h2 - b0 * (p0 - pl) / k.h2);
+    // Reference apply_A (poisson_mpi_cuda2.cu:526-535), same expression tree.
+    const double Ax = k.nih1 * (c.a1 * (pn - p0) / k.h1 - c.a0 * (p0 - pm) / k.h1);
+    const double Ay = k.nih2 * (c.b1 * (pr - p0) / k.h2 - c.b0 * (p0 - pl) / k.h2);
     return Ax + Ay;
   } else {
-    const double Ax = (a1 * (pn - p0) - a0 * (p0 - pm)) * (-1.0 / k.h1sq);
-    const double Ay = (b1 * (pr - p0) - b0 * (p0 - pl)) * (-1.0 / k.h2sq);
-    return Ax + Ay;
+    return (c.a0 * (p0 - pm) - c.a1 * (pn - p0)) * k.ih1sq + (c.b0 * (p0 - pl) - c.b1 * (pr - p0)) * k.ih2sq;
   }
 }
 
+__device__ __forceinline__ bool row_valid(const KParams& k, int64_t q) {
+  return (q >= 1 && q <= k.nx) || (q == 0 && k.has[LEFT]) || (q == k.nx + 1 && k.has[RIGHT]);
+}
 // Is local node (q, lj) a value this rank computes (owned, or a halo node
 // whose neighbour exists)?  Global-boundary halos and halo corners are not.
 __device__ __forceinline__ bool valid_node(const KParams& k, int64_t q, int64_t lj) {
   const bool rin = q >= 1 && q <= k.nx;
-  const bool rh = (q == 0 && k.has[LEFT]) || (q == k.nx + 1 && k.has[RIGHT]);
   const bool cin = lj >= 1 && lj <= k.ny;
   const bool ch = (lj == 0 && k.has[DOWN]) || (lj == k.ny + 1 && k.has[UP]);
-  return (rin && (cin || ch)) || (rh && cin);
+  return (rin && (cin || ch)) || (row_valid(k, q) && !rin && cin);
 }
 
 __device__ __forceinline__ double load_r(const KParams& k, int64_t q, int64_t lj) {
@@ -107,10 +150,24 @@ __device__ __forceinline__ double load_r(const KParams& k, int64_t q, int64_t lj
   return k.r[q * k.pitch + lj];
 }
 
-template <bool EXACT>
-__device__ __forceinline__ double zval(const KParams& k, double r, double D) {
-  (void)k;
-  return (D != 0.0) ? r / D : 0.0;
+// ---- wave-level helpers -------------------------------------------------
+__device__ __forceinline__ double dpp_shr1(double v) {  // lane l ← lane l-1 (lane 0 ← 0)
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(x), 0x138, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), 0x138, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+__device__ __forceinline__ double dpp_shl1(double v) {  // lane l ← lane l+1 (lane 63 ← 0)
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(x), 0x130, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), 0x130, 0xF, 0xF, true);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+__device__ __forceinline__ double readlane(double v, int l) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_readlane(int(x), l);
+  const int hi = __builtin_amdgcn_readlane(int(x >> 32), l);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
 }
 
 // Deterministic block reduction of N sums (or maxima) → thread 0.
@@ -157,19 +214,58 @@ __device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, 
 }
 
 // Sum N-tuples of partials [nblocks][N] in block order (deterministic).
-template <int N, bool MAX>
-__device__ __forceinline__ void reduce_partials(const double* partial, unsigned nblocks, double (&v)[N],
-                                                double* sm) {
+template <int N>
+__device__ __forceinline__ void reduce_partials(const double* partial, unsigned nblocks, double (&v)[N], double* sm) {
 #pragma unroll
   for (int n = 0; n < N; ++n) v[n] = 0.0;
   for (unsigned m = threadIdx.x; m < nblocks; m += TJ)
 #pragma unroll
-    for (int n = 0; n < N; ++n) {
-      const double t = partial[size_t(m) * N + n];
-      v[n] = MAX ? fmax(v[n], t) : v[n] + t;
-    }
-  block_reduce<N, MAX>(v, sm);
+    for (int n = 0; n < N; ++n) v[n] += partial[size_t(m) * N + n];
+  block_reduce<N, false>(v, sm);
 }
+
+// Work item geometry of one wave.
+struct Item {
+  int64_t j0, ib, ie, c0;
+  int nrows;
+};
+__device__ __forceinline__ Item item_geo(const KParams& k, int item, int lane) {
+  Item it;
+  const int s = item % k.nstrips, c = item / k.nstrips;
+  it.j0 = 1 + int64_t(s) * SW;
+  it.ib = 1 + int64_t(c) * k.ti;
+  it.ie = min(it.ib + int64_t(k.ti) - 1, k.nx);
+  it.nrows = int(it.ie - it.ib + 1);
+  it.c0 = it.j0 + 2 * lane;
+  return it;
+}
+
+// Column predicates of a lane's two elements.
+struct Cols {
+  bool own0, own1;      // owned column (stencil / dot / update)
+  bool live0, live1;    // column whose p this rank produces (owned or UP halo column)
+  bool any;             // lane touches memory at all
+};
+__device__ __forceinline__ Cols cols_of(const KParams& k, int64_t c0) {
+  Cols c;
+  c.own0 = c0 <= k.ny;
+  c.own1 = c0 + 1 <= k.ny;
+  c.live0 = c.own0 || (c0 == k.ny + 1 && k.has[UP]);
+  c.live1 = c.own1 || (c0 + 1 == k.ny + 1 && k.has[UP]);
+  c.any = c0 <= k.ny + 1;
+  return c;
+}
+
+// One p_k value at a single node (strip-edge columns, prologue only).
+template <bool EXACT>
+__device__ __forceinline__ double p_point(const KParams& k, int64_t q, int64_t lj, double beta, const double* pold) {
+  return zval<EXACT>(cset_mem<EXACT>(k, q, lj), load_r(k, q, lj)) + beta * pold[q * k.pitch + lj];
+}
+
+// Unconditional 16-byte load (address already clamped in range): a
+// predicated load would make hipcc branch around it and drain vmcnt(0),
+// which serialises the row prefetch (measured in the .s).
+__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
 
 // ---------------------------------------------------------------------------
 // F: p_k = D⁻¹ r_k + β p_{k-1} on owned nodes and the halo ring, then
@@ -179,9 +275,7 @@ template <bool EXACT>
 __global__ __launch_bounds__(TJ) void kF(KParams k, int par) {
   DevState* st = k.st;
   if (st->done) return;
-  __shared__ double srow[2][TJ];
-  __shared__ double hc[2][kTImax];
-  __shared__ double sm[16];
+  __shared__ double sm[8];
   __shared__ int sflag;
 
   const double rz_new = (st->red_G[0] * k.h1) * k.h2;
@@ -189,94 +283,121 @@ __global__ __launch_bounds__(TJ) void kF(KParams k, int par) {
   const double* __restrict__ pold = k.p[par ^ 1];
   double* __restrict__ pnew = k.p[par];
   const int64_t pitch = k.pitch;
-
-  const int tx = threadIdx.x;
-  const int64_t jb = int64_t(blockIdx.x) * TJ + 1;
-  const int64_t lj = jb + tx;
-  const int64_t ib = int64_t(blockIdx.y) * k.ti + 1;
-  const int64_t ie = min(ib + int64_t(k.ti) - 1, k.nx);
-  const int nrows = int(ie - ib + 1);
-
-  // Strip-edge columns jb-1 and jb+TJ for rows ib..ie.
-  if (tx < 2 * nrows) {
-    const int side = tx / nrows;
-    const int64_t q = ib + tx % nrows;
-    const int64_t c = side ? jb + TJ : jb - 1;
-    double v = 0.0;
-    if (c <= k.ny + 1 && valid_node(k, q, c)) {
-      const RowV rv = rowv(k, c);
-      const double D = diag<EXACT>(k, coefA(k, q, rv), coefA(k, q + 1, rv), coefB(k, q, rv.halfB),
-                                   coefB(k, q, rv.halfB1));
-      v = zval<EXACT>(k, load_r(k, q, c), D) + beta * pold[q * pitch + c];
-      if (c == 0 || c == k.ny + 1) pnew[q * pitch + c] = v;  // rank-halo column: ours to write
-    }
-    hc[side][tx % nrows] = v;
-  }
-
-  const bool own = lj <= k.ny;
-  const bool live = lj <= k.ny + 1;
-  const RowV rv = rowv(k, live ? lj : k.ny + 1);
-
-  double a0 = coefA(k, ib, rv), a1 = coefA(k, ib + 1, rv);
-  double b0 = coefB(k, ib, rv.halfB), b1 = coefB(k, ib, rv.halfB1);
-  double pm = 0.0, p0 = 0.0;
-  if (live) {
-    if (valid_node(k, ib - 1, lj)) {
-      const double D = diag<EXACT>(k, coefA(k, ib - 1, rv), a0, coefB(k, ib - 1, rv.halfB),
-                                   coefB(k, ib - 1, rv.halfB1));
-      pm = zval<EXACT>(k, load_r(k, ib - 1, lj), D) + beta * pold[(ib - 1) * pitch + lj];
-      if (ib - 1 == 0) pnew[lj] = pm;  // rank-halo row 0
-    }
-    if (valid_node(k, ib, lj)) {
-      const double D = diag<EXACT>(k, a0, a1, b0, b1);
-      p0 = zval<EXACT>(k, load_r(k, ib, lj), D) + beta * pold[ib * pitch + lj];
-      pnew[ib * pitch + lj] = p0;
-    }
-  }
-  srow[0][tx] = p0;
-  __syncthreads();
-
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * kWPB;
   double sden = 0.0, spp = 0.0;
-  for (int64_t i = ib; i <= ie; ++i) {
-    const int s = int(i - ib) & 1;
-    const int64_t q = i + 1;
-    const double a2 = coefA(k, q + 1, rv);
-    const double bn0 = coefB(k, q, rv.halfB), bn1 = coefB(k, q, rv.halfB1);
-    double pn = 0.0;
-    if (live && valid_node(k, q, lj)) {
-      const double D = diag<EXACT>(k, a1, a2, bn0, bn1);
-      pn = zval<EXACT>(k, load_r(k, q, lj), D) + beta * pold[q * pitch + lj];
-      if (q <= ie || q == k.nx + 1) pnew[q * pitch + lj] = pn;
+
+  // Wave id made provably uniform so row-indexed tables load through SMEM.
+  const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  for (int item = blockIdx.x * kWPB + wid; item < k.nitems; item += nw) {
+    const Item it = item_geo(k, item, lane);
+    const int64_t c0 = it.c0, c1 = c0 + 1;
+    const Cols cl = cols_of(k, c0);
+    const int64_t ib = it.ib, ie = it.ie;
+    const int64_t ca = cl.any ? c0 : 1;  // clamped column for loads
+    const double* rbase = k.r + ca;
+    const double* pbase = pold + ca;
+
+    // ---- prologue (loads allowed to drain here) ----
+    const TV t0 = tv_at(k, cl.any ? c0 : 1), t1 = tv_at(k, cl.any ? c1 : 1);
+    double hL = 0.0, hR = 0.0, rup = 0.0;
+    if (lane < it.nrows) {
+      const int64_t q = ib + lane;
+      const int64_t jl = it.j0 - 1, jr = it.j0 + SW;
+      if (valid_node(k, q, jl)) {
+        hL = p_point<EXACT>(k, q, jl, beta, pold);
+        if (jl == 0) pnew[q * pitch] = hL;  // rank-halo column: ours to write
+      }
+      if (jr <= k.ny + 1 && valid_node(k, q, jr)) {
+        hR = p_point<EXACT>(k, q, jr, beta, pold);
+        if (jr == k.ny + 1) pnew[q * pitch + jr] = hR;
+      }
+      if (k.has[UP]) rup = k.recv_up[q - 1];  // r of an in-strip halo column ny+1
     }
-    if (own) {
-      const double pl = (tx == 0) ? hc[0][i - ib] : srow[s][tx - 1];
-      const double pr = (tx == TJ - 1) ? hc[1][i - ib] : srow[s][tx + 1];
-      const double Ap = stencil<EXACT>(k, pm, p0, pn, pl, pr, a0, a1, b0, b1);
-      sden += Ap * p0;
-      spp += p0 * p0;
+    const double2 rA = ld2(rbase + (ib - 1) * pitch), pA = ld2(pbase + (ib - 1) * pitch);
+    const double2 rB = ld2(rbase + ib * pitch), pB = ld2(pbase + ib * pitch);
+    const double rupA = k.has[UP] && ib >= 2 ? k.recv_up[ib - 2] : 0.0;
+
+    // p(q) for both elements from r(q), p_{k-1}(q); rh = r of the halo column.
+    auto prow = [&](int64_t q, double2 rr, double2 po, double rh, double& v0, double& v1) {
+      const bool rv = row_valid(k, q);
+      const bool rin = q >= 1 && q <= k.nx;
+      const int* rc = k.rowcls + (q + 1) * 4;
+      v0 = 0.0;
+      v1 = 0.0;
+      if (rv && cl.live0 && (c0 <= k.ny || rin))
+        v0 = zval<EXACT>(cset<EXACT>(k, rc, q, c0, t0), (c0 == k.ny + 1) ? rh : rr.x) + beta * po.x;
+      if (rv && cl.live1 && (c1 <= k.ny || rin))
+        v1 = zval<EXACT>(cset<EXACT>(k, rc, q, c1, t1), (c1 == k.ny + 1) ? rh : rr.y) + beta * po.y;
+    };
+    auto store_row = [&](int64_t q, double v0, double v1) {
+      const bool rin = q >= 1 && q <= k.nx;
+      const bool w0 = cl.live0 && (c0 <= k.ny || rin);
+      const bool w1 = cl.live1 && (c1 <= k.ny || rin);
+      double* dst = pnew + q * pitch + c0;
+      if (w0 && w1) *reinterpret_cast<double2*>(dst) = make_double2(v0, v1);
+      else {
+        if (w0) dst[0] = v0;
+        if (w1) dst[1] = v1;
+      }
+    };
+
+    double pm0, pm1, p00, p01;
+    prow(ib - 1, rA, pA, rupA, pm0, pm1);
+    prow(ib, rB, pB, readlane(rup, 0), p00, p01);
+    if (ib - 1 == 0 && k.has[LEFT]) store_row(0, pm0, pm1);
+    store_row(ib, p00, p01);
+    const int64_t qmax = ie + 1;
+    double2 rN = ld2(rbase + (ib + 1) * pitch), pN = ld2(pbase + (ib + 1) * pitch);
+
+    // ---- march: only the prefetch stream touches vector memory ----
+    for (int64_t i = ib; i <= ie; ++i) {
+      const int64_t q = i + 1;
+      const int64_t qf = min(i + 2, qmax);  // clamped prefetch row
+      const double2 rNN = ld2(rbase + qf * pitch), pNN = ld2(pbase + qf * pitch);
+
+      const int rl = int(i - ib);
+      const double rh = (q <= ie) ? readlane(rup, rl + 1) : 0.0;
+      double pn0, pn1;
+      prow(q, rN, pN, rh, pn0, pn1);
+      if (q <= ie || (q == k.nx + 1 && k.has[RIGHT])) store_row(q, pn0, pn1);
+
+      // j±1 neighbours of row i: DPP wave shifts, strip edges from hL/hR.
+      const double eL = readlane(hL, rl), eR = readlane(hR, rl);
+      double pl0 = dpp_shr1(p01);
+      double pr1 = dpp_shl1(p00);
+      if (lane == 0) pl0 = eL;
+      if (lane == 63) pr1 = eR;
+      const int* rc = k.rowcls + (i + 1) * 4;
+      if (cl.own0) {
+        const double Ap = stencil<EXACT>(k, cset<EXACT>(k, rc, i, c0, t0), pm0, p00, pn0, pl0, p01);
+        sden += Ap * p00;
+        spp += p00 * p00;
+      }
+      if (cl.own1) {
+        const double Ap = stencil<EXACT>(k, cset<EXACT>(k, rc, i, c1, t1), pm1, p01, pn1, p00, pr1);
+        sden += Ap * p01;
+        spp += p01 * p01;
+      }
+      pm0 = p00;
+      pm1 = p01;
+      p00 = pn0;
+      p01 = pn1;
+      rN = rNN;
+      pN = pNN;
     }
-    srow[s ^ 1][tx] = pn;
-    pm = p0;
-    p0 = pn;
-    a0 = a1;
-    a1 = a2;
-    b0 = bn0;
-    b1 = bn1;
-    __syncthreads();
   }
 
   double v[2] = {sden, spp};
   block_reduce<2, false>(v, sm);
-  const unsigned nb = gridDim.x * gridDim.y;
-  const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
-  if (tx == 0) {
-    k.partial[2 * size_t(bid)] = v[0];
-    k.partial[2 * size_t(bid) + 1] = v[1];
+  if (threadIdx.x == 0) {
+    k.partial[2 * size_t(blockIdx.x)] = v[0];
+    k.partial[2 * size_t(blockIdx.x) + 1] = v[1];
   }
-  if (arrive_last(&st->ticket[0], nb, &sflag)) {
+  if (arrive_last(&st->ticket[0], gridDim.x, &sflag)) {
     double t[2];
-    reduce_partials<2, false>(k.partial, nb, t, sm);
-    if (tx == 0) {
+    reduce_partials<2>(k.partial, gridDim.x, t, sm);
+    if (threadIdx.x == 0) {
       st->red_F[0] = t[0];
       st->red_F[1] = t[1];
       st->rz_cur = rz_new;
@@ -293,15 +414,13 @@ template <bool EXACT>
 __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
   DevState* st = k.st;
   if (st->done) return;
-  __shared__ double srow[2][TJ];
-  __shared__ double hc[2][kTImax];
-  __shared__ double sm[16];
+  __shared__ double sm[8];
   __shared__ int sflag;
 
   const double den = (st->red_F[0] * k.h1) * k.h2;
   const long long kiter = st->iter + 1;
   if (fabs(den) < 1e-15) {  // breakdown: stop before touching w (reference :413)
-    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) {
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
       st->status = 2;
       st->iter = kiter;
       st->done = 1;
@@ -316,69 +435,93 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
   double* __restrict__ r = k.r;
   double* __restrict__ w = k.w;
   const int64_t pitch = k.pitch;
-  const int tx = threadIdx.x;
-  const int64_t jb = int64_t(blockIdx.x) * TJ + 1;
-  const int64_t lj = jb + tx;
-  const int64_t ib = int64_t(blockIdx.y) * k.ti + 1;
-  const int64_t ie = min(ib + int64_t(k.ti) - 1, k.nx);
-  const int nrows = int(ie - ib + 1);
-
-  if (tx < 2 * nrows) {
-    const int side = tx / nrows;
-    const int64_t q = ib + tx % nrows;
-    const int64_t c = side ? jb + TJ : jb - 1;
-    hc[side][tx % nrows] = (c <= k.ny + 1) ? p[q * pitch + c] : 0.0;
-  }
-  const bool own = lj <= k.ny;
-  const bool live = lj <= k.ny + 1;
-  const RowV rv = rowv(k, live ? lj : k.ny + 1);
-  double a0 = coefA(k, ib, rv), a1 = coefA(k, ib + 1, rv);
-  double b0 = coefB(k, ib, rv.halfB), b1 = coefB(k, ib, rv.halfB1);
-  double pm = live ? p[(ib - 1) * pitch + lj] : 0.0;
-  double p0 = live ? p[ib * pitch + lj] : 0.0;
-  srow[0][tx] = p0;
-  __syncthreads();
-
+  const int lane = threadIdx.x & 63;
+  const int nw = gridDim.x * kWPB;
   double szr = 0.0;
-  for (int64_t i = ib; i <= ie; ++i) {
-    const int s = int(i - ib) & 1;
-    const int64_t q = i + 1;
-    const double pn = live ? p[q * pitch + lj] : 0.0;
-    const double a2 = coefA(k, q + 1, rv);
-    const double bn0 = coefB(k, q, rv.halfB), bn1 = coefB(k, q, rv.halfB1);
-    if (own) {
-      const double pl = (tx == 0) ? hc[0][i - ib] : srow[s][tx - 1];
-      const double pr = (tx == TJ - 1) ? hc[1][i - ib] : srow[s][tx + 1];
-      const double Ap = stencil<EXACT>(k, pm, p0, pn, pl, pr, a0, a1, b0, b1);
-      const int64_t c = i * pitch + lj;
-      const double wv = w[c];
-      w[c] = wv + alpha * p0;
-      const double rn = r[c] - alpha * Ap;
-      r[c] = rn;
-      const double D = diag<EXACT>(k, a0, a1, b0, b1);
-      szr += zval<EXACT>(k, rn, D) * rn;
-      if (lj == 1 && k.has[DOWN]) k.send_dn[i - 1] = rn;
-      if (lj == k.ny && k.has[UP]) k.send_up[i - 1] = rn;
+
+  // Wave id made provably uniform so row-indexed tables load through SMEM.
+  const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  for (int item = blockIdx.x * kWPB + wid; item < k.nitems; item += nw) {
+    const Item it = item_geo(k, item, lane);
+    const int64_t c0 = it.c0, c1 = c0 + 1;
+    const Cols cl = cols_of(k, c0);
+    const int64_t ib = it.ib, ie = it.ie;
+    const int64_t ca = cl.any ? c0 : 1;
+    const double* pb = p + ca;
+    const double* rb = r + ca;
+    const double* wb = w + ca;
+    const TV t0 = tv_at(k, cl.any ? c0 : 1), t1 = tv_at(k, cl.any ? c1 : 1);
+    double hL = 0.0, hR = 0.0;
+    if (lane < it.nrows) {
+      const int64_t q = ib + lane;
+      hL = p[q * pitch + it.j0 - 1];
+      if (it.j0 + SW <= k.ny + 1) hR = p[q * pitch + it.j0 + SW];
     }
-    srow[s ^ 1][tx] = pn;
-    pm = p0;
-    p0 = pn;
-    a0 = a1;
-    a1 = a2;
-    b0 = bn0;
-    b1 = bn1;
-    __syncthreads();
+    const double2 pA = ld2(pb + (ib - 1) * pitch);
+    double2 pB = ld2(pb + ib * pitch);
+    double2 pN = ld2(pb + (ib + 1) * pitch);
+    double2 rC = ld2(rb + ib * pitch);
+    double2 wC = ld2(wb + ib * pitch);
+    double pm0 = pA.x, pm1 = pA.y;
+
+    for (int64_t i = ib; i <= ie; ++i) {
+      const int64_t qn = min(i + 1, ie), qp = min(i + 2, ie + 1);  // clamped prefetch rows
+      const double2 pNN = ld2(pb + qp * pitch);
+      const double2 rNx = ld2(rb + qn * pitch);
+      const double2 wNx = ld2(wb + qn * pitch);
+
+      const int rl = int(i - ib);
+      const double eL = readlane(hL, rl), eR = readlane(hR, rl);
+      double pl0 = dpp_shr1(pB.y);
+      double pr1 = dpp_shl1(pB.x);
+      if (lane == 0) pl0 = eL;
+      if (lane == 63) pr1 = eR;
+      const int* rc = k.rowcls + (i + 1) * 4;
+      double rn0 = 0.0, rn1 = 0.0, wn0 = 0.0, wn1 = 0.0;
+      if (cl.own0) {
+        const CS c = cset<EXACT>(k, rc, i, c0, t0);
+        const double Ap = stencil<EXACT>(k, c, pm0, pB.x, pN.x, pl0, pB.y);
+        wn0 = wC.x + alpha * pB.x;
+        rn0 = rC.x - alpha * Ap;
+        szr += zval<EXACT>(c, rn0) * rn0;
+      }
+      if (cl.own1) {
+        const CS c = cset<EXACT>(k, rc, i, c1, t1);
+        const double Ap = stencil<EXACT>(k, c, pm1, pB.y, pN.y, pB.x, pr1);
+        wn1 = wC.y + alpha * pB.y;
+        rn1 = rC.y - alpha * Ap;
+        szr += zval<EXACT>(c, rn1) * rn1;
+      }
+      double* rd = r + i * pitch + c0;
+      double* wd = w + i * pitch + c0;
+      if (cl.own1) {
+        *reinterpret_cast<double2*>(rd) = make_double2(rn0, rn1);
+        *reinterpret_cast<double2*>(wd) = make_double2(wn0, wn1);
+      } else if (cl.own0) {
+        rd[0] = rn0;
+        wd[0] = wn0;
+      }
+      if (c0 == 1 && k.has[DOWN]) k.send_dn[i - 1] = rn0;
+      if (k.has[UP]) {
+        if (c0 == k.ny) k.send_up[i - 1] = rn0;
+        if (c1 == k.ny) k.send_up[i - 1] = rn1;
+      }
+      pm0 = pB.x;
+      pm1 = pB.y;
+      pB = pN;
+      pN = pNN;
+      rC = rNx;
+      wC = wNx;
+    }
   }
 
   double v[1] = {szr};
   block_reduce<1, false>(v, sm);
-  const unsigned nb = gridDim.x * gridDim.y;
-  const unsigned bid = blockIdx.y * gridDim.x + blockIdx.x;
-  if (tx == 0) k.partial[bid] = v[0];
-  if (arrive_last(&st->ticket[1], nb, &sflag)) {
+  if (threadIdx.x == 0) k.partial[blockIdx.x] = v[0];
+  if (arrive_last(&st->ticket[1], gridDim.x, &sflag)) {
     double t[1];
-    reduce_partials<1, false>(k.partial, nb, t, sm);
-    if (tx == 0) {
+    reduce_partials<1>(k.partial, gridDim.x, t, sm);
+    if (threadIdx.x == 0) {
       st->red_G[0] = t[0];
       st->alpha = alpha;
       st->last_diff = diff;
@@ -398,8 +541,9 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
 // ---------------------------------------------------------------------------
 // Init: r⁰ = B - A w⁰ (w⁰ = 0 or a global-index hash), S_zr⁰ = Σ (D⁻¹r⁰)·r⁰.
 // ---------------------------------------------------------------------------
+template <bool EXACT>
 __global__ __launch_bounds__(TJ) void kInit(KParams k, int init_random, unsigned long long seed, double amp) {
-  __shared__ double sm[16];
+  __shared__ double sm[8];
   __shared__ int sflag;
   DevState* st = k.st;
   const int64_t n = k.nx * k.ny;
@@ -408,32 +552,29 @@ __global__ __launch_bounds__(TJ) void kInit(KParams k, int init_random, unsigned
     const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
     const int64_t gi = k.gi0 + li, gj = k.gj0 + lj;
     const double x = k.A1 + gi * k.h1, y = k.A2 + gj * k.h2;
-    const RowV rv = rowv(k, lj);
-    const double a0 = coefA(k, li, rv), a1 = coefA(k, li + 1, rv);
-    const double b0 = coefB(k, li, rv.halfB), b1 = coefB(k, li, rv.halfB1);
+    const CS c = cset_mem<EXACT>(k, li, lj);
     double rr = in_ellipse(x, y, k.cx, k.cy) ? k.F : 0.0;
-    const int64_t c = li * k.pitch + lj;
+    const int64_t at = li * k.pitch + lj;
     if (init_random) {
       const double w0 = random_w0(gi, gj, k.M, k.N, seed, amp);
-      const double Aw = stencil<true>(k, random_w0(gi - 1, gj, k.M, k.N, seed, amp), w0,
-                                      random_w0(gi + 1, gj, k.M, k.N, seed, amp),
-                                      random_w0(gi, gj - 1, k.M, k.N, seed, amp),
-                                      random_w0(gi, gj + 1, k.M, k.N, seed, amp), a0, a1, b0, b1);
+      const double Aw = stencil<EXACT>(k, c, random_w0(gi - 1, gj, k.M, k.N, seed, amp), w0,
+                                       random_w0(gi + 1, gj, k.M, k.N, seed, amp),
+                                       random_w0(gi, gj - 1, k.M, k.N, seed, amp),
+                                       random_w0(gi, gj + 1, k.M, k.N, seed, amp));
       rr = rr - Aw;
-      k.w[c] = w0;
+      k.w[at] = w0;
     }
-    k.r[c] = rr;
+    k.r[at] = rr;
     if (lj == 1 && k.has[DOWN]) k.send_dn[li - 1] = rr;
     if (lj == k.ny && k.has[UP]) k.send_up[li - 1] = rr;
-    const double D = diag<true>(k, a0, a1, b0, b1);
-    szr += zval<true>(k, rr, D) * rr;
+    szr += zval<EXACT>(c, rr) * rr;
   }
   double v[1] = {szr};
   block_reduce<1, false>(v, sm);
   if (threadIdx.x == 0) k.partial[blockIdx.x] = v[0];
   if (arrive_last(&st->ticket[2], gridDim.x, &sflag)) {
     double t[1];
-    reduce_partials<1, false>(k.partial, gridDim.x, t, sm);
+    reduce_partials<1>(k.partial, gridDim.x, t, sm);
     if (threadIdx.x == 0) {
       st->red_G[0] = t[0];
       st->rz_cur = 1.0;
@@ -447,7 +588,7 @@ __global__ __launch_bounds__(TJ) void kInit(KParams k, int init_random, unsigned
 
 // Error against the analytic solution u = F(1 - cx x² - cy y²)/(2cx + 2cy).
 __global__ __launch_bounds__(TJ) void kError(KParams k) {
-  __shared__ double sm[16];
+  __shared__ double sm[8];
   __shared__ int sflag;
   DevState* st = k.st;
   const int64_t n = k.nx * k.ny;
@@ -503,66 +644,59 @@ __global__ void kGroupReduce(double* const* bufs, int nranks, int n, int is_max)
   for (int r = 0; r < nranks; ++r) bufs[r][i] = acc;
 }
 
-// Test op: Ap = A p on owned nodes (p halo must be valid), exact arithmetic.
+// Test op: Ap = A p on owned nodes (p halo must be valid).
+template <bool EXACT>
 __global__ void kApplyA(KParams k, const double* p, double* Ap) {
   const int64_t n = k.nx * k.ny;
   for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n;
        idx += int64_t(gridDim.x) * blockDim.x) {
     const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
-    const RowV rv = rowv(k, lj);
     const int64_t c = li * k.pitch + lj;
-    Ap[c] = stencil<true>(k, p[c - k.pitch], p[c], p[c + k.pitch], p[c - 1], p[c + 1], coefA(k, li, rv),
-                          coefA(k, li + 1, rv), coefB(k, li, rv.halfB), coefB(k, li, rv.halfB1));
+    const CS cs = cset_mem<EXACT>(k, li, lj);
+    Ap[c] = stencil<EXACT>(k, cs, p[c - k.pitch], p[c], p[c + k.pitch], p[c - 1], p[c + 1]);
   }
 }
 
-// Test op: a_ij, b_ij, D_ij on owned nodes.
+// Test op: a_ij, b_ij, D_ij through the class table (checks the classification).
 __global__ void kCoef(KParams k, double* a, double* b, double* D) {
-  const int64_t n = k.nx * k.ny;
+  const int64_t n = (k.nx + 2) * (k.ny + 2);
   for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n;
        idx += int64_t(gridDim.x) * blockDim.x) {
-    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
-    const RowV rv = rowv(k, lj);
+    const int64_t li = idx / (k.ny + 2), lj = idx % (k.ny + 2);
+    const CS cs = cset_mem<true>(k, li, lj);
     const int64_t c = li * k.pitch + lj;
-    const double a0 = coefA(k, li, rv), a1 = coefA(k, li + 1, rv);
-    const double b0 = coefB(k, li, rv.halfB), b1 = coefB(k, li, rv.halfB1);
-    a[c] = a0;
-    b[c] = b0;
-    D[c] = diag<true>(k, a0, a1, b0, b1);
+    a[c] = cs.a0;
+    b[c] = cs.b0;
+    D[c] = cs.d;
   }
 }
 
 }  // namespace
 
-int grid_blocks(const KParams& k) {
-  const int64_t gx = (k.ny + TJ - 1) / TJ, gy = (k.nx + k.ti - 1) / k.ti;
-  return int(gx * gy);
-}
-
-static dim3 march_grid(const KParams& k) {
-  return dim3(unsigned((k.ny + TJ - 1) / TJ), unsigned((k.nx + k.ti - 1) / k.ti), 1);
-}
+int grid_blocks(const KParams& k) { return k.nblocks; }
 
 static unsigned flat_blocks(const KParams& k) {
-  const int64_t n = k.nx * k.ny;
+  const int64_t n = (k.nx + 2) * (k.ny + 2);
   int64_t b = (n + TJ - 1) / TJ;
   if (b > 4096) b = 4096;
   if (b < 1) b = 1;
   return unsigned(b);
 }
 
-void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, hipStream_t s) {
-  hipLaunchKernelGGL(kInit, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, init_random, seed, amp);
+void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
+                 hipStream_t s) {
+  if (variant == 1) hipLaunchKernelGGL(kInit<true>, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, init_random, seed, amp);
+  else hipLaunchKernelGGL(kInit<false>, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, init_random, seed, amp);
 }
 
 void launch_F(const KParams& k, int par, int variant, hipStream_t s) {
-  if (variant == 1) hipLaunchKernelGGL(kF<false>, march_grid(k), dim3(TJ), 0, s, k, par);
-  else hipLaunchKernelGGL(kF<true>, march_grid(k), dim3(TJ), 0, s, k, par);
+  if (variant == 1) hipLaunchKernelGGL(kF<true>, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
+  else hipLaunchKernelGGL(kF<false>, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
 }
 
 void launch_G(const KParams& k, int par, int variant, hipStream_t s) {
-  if (variant == 1) hipLaunchKernelGGL(kG<false>, march_grid(k), dim3(TJ), 0, s, k, par);
-  else hipLaunchKernelGGL(kG<true>, march_grid(k), dim3(TJ), 0, s, k, par);
+  if (variant == 1) hipLaunchKernelGGL(kG<true>, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
+  else hipLaunchKernelGGL(kG<false>, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
 }
 
 void launch_error(const KParams& k, hipStream_t s) {
@@ -574,7 +708,7 @@ void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hip
 }
 
 void launch_apply_A(const KParams& k, const double* p, double* Ap, hipStream_t s) {
-  hipLaunchKernelGGL(kApplyA, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, p, Ap);
+  hipLaunchKernelGGL(kApplyA<false>, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, p, Ap);
 }
 
 void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t s) {

@@ -58,16 +58,25 @@ struct KParams {
   double* p[2];
   double* send_dn; double* send_up;        // y-direction (strided) send strips, nx each
   const double* recv_dn; const double* recv_up;
-  double* partial;               // ≥ 2 × blocks doubles
+  const int* rowcls;             // (nx+4) × 4 ints at index q+1: {in_lo, in_hi, out_lo, out_hi}
+  double* partial;               // ≥ 3 × blocks doubles
   DevState* st;
-  int ti;                        // rows per marching block
+  int ti;                        // rows per work item (≤ 64)
+  int nstrips;                   // 128-column wave strips across ny (+ halo column)
+  int nitems;                    // nstrips × ceil(nx / ti)
+  int nblocks;                   // persistent grid size of the marching kernels
   int check_tol;                 // 0 → never stop on ‖Δw‖ (fixed-iteration runs)
+  double D_in, D_out;            // exact-arithmetic diagonal in the interior / exterior class
+  double dinv_in, dinv_out;      // fast-arithmetic 1/D in the interior / exterior class
+  double ih1sq, ih2sq;           // 1/h1², 1/h2² (fast arithmetic)
 };
 
-constexpr int kTJ = 256;         // strip width = threads per block (4 waves)
-constexpr int kTImax = 64;       // max rows per marching block
+constexpr int kTJ = 256;         // threads per block (4 wave64s)
+constexpr int kWPB = 4;          // waves per block
+constexpr int kSW = 128;         // columns per wave strip (2 per lane, 16-B accesses)
+constexpr int kTImax = 64;       // max rows per work item (halo rows live in one lane each)
 
-void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp,
+void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
                  hipStream_t s);
 void launch_F(const KParams& k, int par, int variant, hipStream_t s);
 void launch_G(const KParams& k, int par, int variant, hipStream_t s);

@@ -119,6 +119,7 @@ class DeviceSolver {
   hipStream_t stream_ = nullptr;
   double* fields_ = nullptr;  // r, w, p0, p1 (alloc each)
   double* tables_ = nullptr;
+  int* rowcls_ = nullptr;
   double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each)
   double* partial_ = nullptr;
   dev::DevState* st_ = nullptr;
@@ -130,6 +131,13 @@ class DeviceSolver {
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
 };
+
+// Per-row coefficient classes from the chord tables (see row_classes.cpp):
+// for each local row q ∈ [-1, nx+1], {in_lo, in_hi, out_lo, out_hi} such that
+// every face coefficient of node (q, lj) is exactly 1 for lj ∈ [in_lo, in_hi]
+// and exactly 1/eps for lj ∉ [out_lo, out_hi].  Conservative: anything else is
+// evaluated exactly.
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx, int64_t ny);
 
 // P virtual ranks on ONE device (LocalComm).  Every rank runs the
 // same kernels and the same halo plan as under RCCL; the transport is
