@@ -76,7 +76,9 @@ Block decompose(int M, int N, const ProcessGrid& pg, int rank, int align) {
   // Pad the pitch so every row's first owned element (lj = 1) is aligned.
   b.pitch = ((b.ny + 2 + align - 1) / align) * align;
   b.base = align - 1;  // (li, 1) → base + li*pitch + 1 ≡ 0 (mod align)
-  b.alloc = b.base + b.rows * b.pitch + align;
+  // Two padding rows past the halo: the marching kernels prefetch up to
+  // row nx+3 without clamping the address.
+  b.alloc = b.base + (b.rows + 2) * b.pitch + align;
   b.nbr[LEFT] = b.px > 0 ? rank - 1 : -1;
   b.nbr[RIGHT] = b.px < pg.Px - 1 ? rank + 1 : -1;
   b.nbr[DOWN] = b.py > 0 ? rank - pg.Px : -1;

@@ -224,38 +224,6 @@ __device__ __forceinline__ void reduce_partials(const double* partial, unsigned 
   block_reduce<N, false>(v, sm);
 }
 
-// Work item geometry of one wave.
-struct Item {
-  int64_t j0, ib, ie, c0;
-  int nrows;
-};
-__device__ __forceinline__ Item item_geo(const KParams& k, int item, int lane) {
-  Item it;
-  const int s = item % k.nstrips, c = item / k.nstrips;
-  it.j0 = 1 + int64_t(s) * SW;
-  it.ib = 1 + int64_t(c) * k.ti;
-  it.ie = min(it.ib + int64_t(k.ti) - 1, k.nx);
-  it.nrows = int(it.ie - it.ib + 1);
-  it.c0 = it.j0 + 2 * lane;
-  return it;
-}
-
-// Column predicates of a lane's two elements.
-struct Cols {
-  bool own0, own1;      // owned column (stencil / dot / update)
-  bool live0, live1;    // column whose p this rank produces (owned or UP halo column)
-  bool any;             // lane touches memory at all
-};
-__device__ __forceinline__ Cols cols_of(const KParams& k, int64_t c0) {
-  Cols c;
-  c.own0 = c0 <= k.ny;
-  c.own1 = c0 + 1 <= k.ny;
-  c.live0 = c.own0 || (c0 == k.ny + 1 && k.has[UP]);
-  c.live1 = c.own1 || (c0 + 1 == k.ny + 1 && k.has[UP]);
-  c.any = c0 <= k.ny + 1;
-  return c;
-}
-
 // One p_k value at a single node (strip-edge columns, prologue only).
 template <bool EXACT>
 __device__ __forceinline__ double p_point(const KParams& k, int64_t q, int64_t lj, double beta, const double* pold) {
@@ -266,6 +234,42 @@ __device__ __forceinline__ double p_point(const KParams& k, int64_t q, int64_t l
 // predicated load would make hipcc branch around it and drain vmcnt(0),
 // which serialises the row prefetch (measured in the .s).
 __device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
+
+// Row class (interior interval / exterior hull) of one row, in SGPRs.
+struct RowCls {
+  int in_lo, in_hi, out_lo, out_hi;
+};
+__device__ __forceinline__ RowCls rcl_read(const int4& v, int l) {
+  return RowCls{__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l),
+                __builtin_amdgcn_readlane(v.z, l), __builtin_amdgcn_readlane(v.w, l)};
+}
+// Does columns [jlo, jhi] of this row contain a boundary-band node?  (scalar)
+__device__ __forceinline__ bool has_gen(const RowCls& c, int64_t jlo, int64_t jhi) {
+  const int64_t lo = max(jlo, int64_t(c.out_lo)), hi = min(jhi, int64_t(c.out_hi));
+  if (lo > hi) return false;
+  if (c.in_lo > c.in_hi) return true;
+  return lo < c.in_lo || hi > c.in_hi;
+}
+// Coefficients of a node in a row without boundary-band nodes in this strip.
+template <bool EXACT>
+__device__ __forceinline__ CS cset_fast(const KParams& k, const RowCls& c, int64_t lj) {
+  const bool in = lj >= c.in_lo && lj <= c.in_hi;
+  const double f = in ? 1.0 : k.inv_eps;
+  CS cs;
+  cs.a0 = cs.a1 = cs.b0 = cs.b1 = f;
+  cs.d = EXACT ? (in ? k.D_in : k.D_out) : (in ? k.dinv_in : k.dinv_out);
+  return cs;
+}
+
+constexpr int SEG = 60;  // rows per segment: rows seg-1 .. seg+SEG live one per lane
+
+// Per-segment lane-resident data of a strip: row classes (lane t ↔ row
+// s0-1+t), strip-edge p columns (lane t ↔ row s0+t) and, for F, r of an
+// in-strip halo column ny+1 (lane t ↔ row s0+t).
+struct SegData {
+  int4 rcv;
+  double hL, hR, rup;
+};
 
 // ---------------------------------------------------------------------------
 // F: p_k = D⁻¹ r_k + β p_{k-1} on owned nodes and the halo ring, then
@@ -283,108 +287,151 @@ __global__ __launch_bounds__(TJ) void kF(KParams k, int par) {
   const double* __restrict__ pold = k.p[par ^ 1];
   double* __restrict__ pnew = k.p[par];
   const int64_t pitch = k.pitch;
+  const int nx = int(k.nx), ny = int(k.ny);
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * kWPB;
   double sden = 0.0, spp = 0.0;
 
-  // Wave id made provably uniform so row-indexed tables load through SMEM.
+  // Wave id made provably uniform so item geometry lives in SGPRs.
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   for (int item = blockIdx.x * kWPB + wid; item < k.nitems; item += nw) {
-    const Item it = item_geo(k, item, lane);
-    const int64_t c0 = it.c0, c1 = c0 + 1;
-    const Cols cl = cols_of(k, c0);
-    const int64_t ib = it.ib, ie = it.ie;
-    const int64_t ca = cl.any ? c0 : 1;  // clamped column for loads
-    const double* rbase = k.r + ca;
-    const double* pbase = pold + ca;
+    // item → (strip, row range); strip-major so a wave's consecutive items
+    // continue down the same strip.
+    // order 0 (default): chunk-major — concurrently running waves cover a
+    // compact window of rows (TLB/L2/MALL locality); order 1: strip-major.
+    const int nchunks = (nx + k.ti - 1) / k.ti;
+    const int s = k.order ? item / nchunks : item % k.nstrips;
+    const int ch = k.order ? item % nchunks : item / k.nstrips;
+    const int j0 = 1 + s * SW;
+    const int ib = 1 + ch * k.ti, ie = min(ib + k.ti - 1, nx);
+    const int c0 = j0 + 2 * lane, c1 = c0 + 1;
+    const int jhi = min(j0 + SW - 1, ny + 1);
+    const bool own0 = c0 <= ny, own1 = c1 <= ny;
+    const bool live0 = own0 || (c0 == ny + 1 && k.has[UP]);
+    const bool live1 = own1 || (c1 == ny + 1 && k.has[UP]);
+    const int ca = (c0 <= ny + 1) ? c0 : 1;  // clamped column for loads
 
-    // ---- prologue (loads allowed to drain here) ----
-    const TV t0 = tv_at(k, cl.any ? c0 : 1), t1 = tv_at(k, cl.any ? c1 : 1);
-    double hL = 0.0, hR = 0.0, rup = 0.0;
-    if (lane < it.nrows) {
-      const int64_t q = ib + lane;
-      const int64_t jl = it.j0 - 1, jr = it.j0 + SW;
-      if (valid_node(k, q, jl)) {
-        hL = p_point<EXACT>(k, q, jl, beta, pold);
-        if (jl == 0) pnew[q * pitch] = hL;  // rank-halo column: ours to write
+    auto seg_load = [&](int s0, int s1) {
+      SegData d;
+      const int t = lane;
+      d.rcv = (t <= s1 - s0 + 2) ? *reinterpret_cast<const int4*>(k.rowcls + (s0 + t) * 4) : make_int4(1, 0, 0, -1);
+      d.hL = d.hR = d.rup = 0.0;
+      if (t <= s1 - s0) {
+        const int q = s0 + t;
+        const int jl = j0 - 1, jr = j0 + SW;
+        if (valid_node(k, q, jl)) {
+          d.hL = p_point<EXACT>(k, q, jl, beta, pold);
+          if (jl == 0) pnew[q * pitch] = d.hL;  // rank-halo column: ours to write
+        }
+        if (jr <= ny + 1 && valid_node(k, q, jr)) {
+          d.hR = p_point<EXACT>(k, q, jr, beta, pold);
+          if (jr == ny + 1) pnew[q * pitch + jr] = d.hR;
+        }
       }
-      if (jr <= k.ny + 1 && valid_node(k, q, jr)) {
-        hR = p_point<EXACT>(k, q, jr, beta, pold);
-        if (jr == k.ny + 1) pnew[q * pitch + jr] = hR;
-      }
-      if (k.has[UP]) rup = k.recv_up[q - 1];  // r of an in-strip halo column ny+1
-    }
-    const double2 rA = ld2(rbase + (ib - 1) * pitch), pA = ld2(pbase + (ib - 1) * pitch);
-    const double2 rB = ld2(rbase + ib * pitch), pB = ld2(pbase + ib * pitch);
-    const double rupA = k.has[UP] && ib >= 2 ? k.recv_up[ib - 2] : 0.0;
+      if (t <= s1 - s0 + 1 && s0 + t <= nx && k.has[UP]) d.rup = k.recv_up[s0 + t - 1];
+      return d;
+    };
 
     // p(q) for both elements from r(q), p_{k-1}(q); rh = r of the halo column.
-    auto prow = [&](int64_t q, double2 rr, double2 po, double rh, double& v0, double& v1) {
-      const bool rv = row_valid(k, q);
-      const bool rin = q >= 1 && q <= k.nx;
-      const int* rc = k.rowcls + (q + 1) * 4;
-      v0 = 0.0;
-      v1 = 0.0;
-      if (rv && cl.live0 && (c0 <= k.ny || rin))
-        v0 = zval<EXACT>(cset<EXACT>(k, rc, q, c0, t0), (c0 == k.ny + 1) ? rh : rr.x) + beta * po.x;
-      if (rv && cl.live1 && (c1 <= k.ny || rin))
-        v1 = zval<EXACT>(cset<EXACT>(k, rc, q, c1, t1), (c1 == k.ny + 1) ? rh : rr.y) + beta * po.y;
+    auto prow = [&](int q, const RowCls& rc, bool fast, double2 rr, double2 po, double rh, double& v0, double& v1) {
+      const bool rin = q >= 1 && q <= nx;
+      const bool rv = rin || (q == 0 && k.has[LEFT]) || (q == nx + 1 && k.has[RIGHT]);
+      const double r0 = (c0 == ny + 1) ? rh : rr.x;
+      const double r1 = (c1 == ny + 1) ? rh : rr.y;
+      CS s0, s1;
+      if (fast) {
+        s0 = cset_fast<EXACT>(k, rc, c0);
+        s1 = cset_fast<EXACT>(k, rc, c1);
+      } else {
+        const int* rcp = k.rowcls + (q + 1) * 4;
+        s0 = cset<EXACT>(k, rcp, q, c0, tv_at(k, ca));
+        s1 = cset<EXACT>(k, rcp, q, c1, tv_at(k, ca + 1));
+      }
+      const bool e0 = rv && (rin ? live0 : own0), e1 = rv && (rin ? live1 : own1);
+      v0 = e0 ? zval<EXACT>(s0, r0) + beta * po.x : 0.0;
+      v1 = e1 ? zval<EXACT>(s1, r1) + beta * po.y : 0.0;
     };
-    auto store_row = [&](int64_t q, double v0, double v1) {
-      const bool rin = q >= 1 && q <= k.nx;
-      const bool w0 = cl.live0 && (c0 <= k.ny || rin);
-      const bool w1 = cl.live1 && (c1 <= k.ny || rin);
+    auto store_row = [&](int q, double v0, double v1) {
+      const bool rin = q >= 1 && q <= nx;
+      const bool w0 = rin ? live0 : own0, w1 = rin ? live1 : own1;
       double* dst = pnew + q * pitch + c0;
       if (w0 && w1) *reinterpret_cast<double2*>(dst) = make_double2(v0, v1);
-      else {
-        if (w0) dst[0] = v0;
-        if (w1) dst[1] = v1;
-      }
+      else if (w0) dst[0] = v0;
     };
 
+    const double* rptr = k.r + (ib - 1) * pitch + ca;  // row ib-1
+    const double* pptr = pold + (ib - 1) * pitch + ca;
+    const double2 rA = ld2(rptr), pA = ld2(pptr);
+    const double2 rB = ld2(rptr + pitch), pB = ld2(pptr + pitch);
+    double2 rN = ld2(rptr + 2 * pitch), pN = ld2(pptr + 2 * pitch);  // row ib+1
+    rptr += 3 * pitch;                                                // → row ib+2
+    pptr += 3 * pitch;
+    SegData sd = seg_load(ib, min(ib + SEG - 1, ie));
+
     double pm0, pm1, p00, p01;
-    prow(ib - 1, rA, pA, rupA, pm0, pm1);
-    prow(ib, rB, pB, readlane(rup, 0), p00, p01);
-    if (ib - 1 == 0 && k.has[LEFT]) store_row(0, pm0, pm1);
+    RowCls ci = rcl_read(sd.rcv, 1);  // row ib
+    bool gi = has_gen(ci, j0, jhi);
+    {
+      const RowCls cm = rcl_read(sd.rcv, 0);  // row ib-1
+      const double rupA = (k.has[UP] && ib >= 2) ? k.recv_up[ib - 2] : 0.0;
+      prow(ib - 1, cm, !has_gen(cm, j0, jhi), rA, pA, rupA, pm0, pm1);
+      prow(ib, ci, !gi, rB, pB, readlane(sd.rup, 0), p00, p01);
+    }
+    if (ib == 1 && k.has[LEFT]) store_row(0, pm0, pm1);
     store_row(ib, p00, p01);
-    const int64_t qmax = ie + 1;
-    double2 rN = ld2(rbase + (ib + 1) * pitch), pN = ld2(pbase + (ib + 1) * pitch);
 
-    // ---- march: only the prefetch stream touches vector memory ----
-    for (int64_t i = ib; i <= ie; ++i) {
-      const int64_t q = i + 1;
-      const int64_t qf = min(i + 2, qmax);  // clamped prefetch row
-      const double2 rNN = ld2(rbase + qf * pitch), pNN = ld2(pbase + qf * pitch);
+    for (int s0 = ib; s0 <= ie; s0 += SEG) {
+      const int s1 = min(s0 + SEG - 1, ie);
+      if (s0 != ib) sd = seg_load(s0, s1);
+      // ---- march: only the prefetch stream touches vector memory ----
+      for (int i = s0; i <= s1; ++i) {
+        const int q = i + 1;
+        const double2 rNN = ld2(rptr), pNN = ld2(pptr);  // row i+2 (≤ nx+3: padded)
+        rptr += pitch;
+        pptr += pitch;
 
-      const int rl = int(i - ib);
-      const double rh = (q <= ie) ? readlane(rup, rl + 1) : 0.0;
-      double pn0, pn1;
-      prow(q, rN, pN, rh, pn0, pn1);
-      if (q <= ie || (q == k.nx + 1 && k.has[RIGHT])) store_row(q, pn0, pn1);
+        const int rl = i - s0;
+        const RowCls cq = rcl_read(sd.rcv, rl + 2);
+        const bool gq = has_gen(cq, j0, jhi);
+        const double rh = readlane(sd.rup, rl + 1);
+        double pn0, pn1;
+        prow(q, cq, !gq, rN, pN, rh, pn0, pn1);
+        if (q <= ie || (q == nx + 1 && k.has[RIGHT])) store_row(q, pn0, pn1);
 
-      // j±1 neighbours of row i: DPP wave shifts, strip edges from hL/hR.
-      const double eL = readlane(hL, rl), eR = readlane(hR, rl);
-      double pl0 = dpp_shr1(p01);
-      double pr1 = dpp_shl1(p00);
-      if (lane == 0) pl0 = eL;
-      if (lane == 63) pr1 = eR;
-      const int* rc = k.rowcls + (i + 1) * 4;
-      if (cl.own0) {
-        const double Ap = stencil<EXACT>(k, cset<EXACT>(k, rc, i, c0, t0), pm0, p00, pn0, pl0, p01);
-        sden += Ap * p00;
-        spp += p00 * p00;
+        // j±1 neighbours of row i: DPP wave shifts, strip edges from hL/hR.
+        const double eL = readlane(sd.hL, rl), eR = readlane(sd.hR, rl);
+        double pl0 = dpp_shr1(p01);
+        double pr1 = dpp_shl1(p00);
+        if (lane == 0) pl0 = eL;
+        if (lane == 63) pr1 = eR;
+        CS x0, x1;
+        if (!gi) {
+          x0 = cset_fast<EXACT>(k, ci, c0);
+          x1 = cset_fast<EXACT>(k, ci, c1);
+        } else {
+          const int* rcp = k.rowcls + (i + 1) * 4;
+          x0 = cset<EXACT>(k, rcp, i, c0, tv_at(k, ca));
+          x1 = cset<EXACT>(k, rcp, i, c1, tv_at(k, ca + 1));
+        }
+        const double Ap0 = stencil<EXACT>(k, x0, pm0, p00, pn0, pl0, p01);
+        const double Ap1 = stencil<EXACT>(k, x1, pm1, p01, pn1, p00, pr1);
+        if (own0) {
+          sden += Ap0 * p00;
+          spp += p00 * p00;
+        }
+        if (own1) {
+          sden += Ap1 * p01;
+          spp += p01 * p01;
+        }
+        pm0 = p00;
+        pm1 = p01;
+        p00 = pn0;
+        p01 = pn1;
+        rN = rNN;
+        pN = pNN;
+        ci = cq;
+        gi = gq;
       }
-      if (cl.own1) {
-        const double Ap = stencil<EXACT>(k, cset<EXACT>(k, rc, i, c1, t1), pm1, p01, pn1, p00, pr1);
-        sden += Ap * p01;
-        spp += p01 * p01;
-      }
-      pm0 = p00;
-      pm1 = p01;
-      p00 = pn0;
-      p01 = pn1;
-      rN = rNN;
-      pN = pNN;
     }
   }
 
@@ -435,83 +482,105 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
   double* __restrict__ r = k.r;
   double* __restrict__ w = k.w;
   const int64_t pitch = k.pitch;
+  const int nx = int(k.nx), ny = int(k.ny);
   const int lane = threadIdx.x & 63;
   const int nw = gridDim.x * kWPB;
   double szr = 0.0;
 
-  // Wave id made provably uniform so row-indexed tables load through SMEM.
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   for (int item = blockIdx.x * kWPB + wid; item < k.nitems; item += nw) {
-    const Item it = item_geo(k, item, lane);
-    const int64_t c0 = it.c0, c1 = c0 + 1;
-    const Cols cl = cols_of(k, c0);
-    const int64_t ib = it.ib, ie = it.ie;
-    const int64_t ca = cl.any ? c0 : 1;
-    const double* pb = p + ca;
-    const double* rb = r + ca;
-    const double* wb = w + ca;
-    const TV t0 = tv_at(k, cl.any ? c0 : 1), t1 = tv_at(k, cl.any ? c1 : 1);
-    double hL = 0.0, hR = 0.0;
-    if (lane < it.nrows) {
-      const int64_t q = ib + lane;
-      hL = p[q * pitch + it.j0 - 1];
-      if (it.j0 + SW <= k.ny + 1) hR = p[q * pitch + it.j0 + SW];
-    }
-    const double2 pA = ld2(pb + (ib - 1) * pitch);
-    double2 pB = ld2(pb + ib * pitch);
-    double2 pN = ld2(pb + (ib + 1) * pitch);
-    double2 rC = ld2(rb + ib * pitch);
-    double2 wC = ld2(wb + ib * pitch);
+    // order 0 (default): chunk-major — concurrently running waves cover a
+    // compact window of rows (TLB/L2/MALL locality); order 1: strip-major.
+    const int nchunks = (nx + k.ti - 1) / k.ti;
+    const int s = k.order ? item / nchunks : item % k.nstrips;
+    const int ch = k.order ? item % nchunks : item / k.nstrips;
+    const int j0 = 1 + s * SW;
+    const int ib = 1 + ch * k.ti, ie = min(ib + k.ti - 1, nx);
+    const int c0 = j0 + 2 * lane, c1 = c0 + 1;
+    const int jhi = min(j0 + SW - 1, ny + 1);
+    const bool own0 = c0 <= ny, own1 = c1 <= ny;
+    const int ca = (c0 <= ny + 1) ? c0 : 1;
+
+    auto seg_load = [&](int s0, int s1) {
+      SegData d;
+      const int t = lane;
+      d.rcv = (t <= s1 - s0) ? *reinterpret_cast<const int4*>(k.rowcls + (s0 + 1 + t) * 4) : make_int4(1, 0, 0, -1);
+      d.hL = d.hR = d.rup = 0.0;
+      if (t <= s1 - s0) {
+        const int q = s0 + t;
+        d.hL = p[q * pitch + j0 - 1];
+        if (j0 + SW <= ny + 1) d.hR = p[q * pitch + j0 + SW];
+      }
+      return d;
+    };
+
+    const double* pptr = p + (ib - 1) * pitch + ca;
+    const double* rptr = r + ib * pitch + ca;
+    const double* wptr = w + ib * pitch + ca;
+    const double2 pA = ld2(pptr);
+    double2 pB = ld2(pptr + pitch);
+    double2 pN = ld2(pptr + 2 * pitch);
+    double2 rC = ld2(rptr), wC = ld2(wptr);
+    pptr += 3 * pitch;  // → row ib+2
+    rptr += pitch;      // → row ib+1
+    wptr += pitch;
     double pm0 = pA.x, pm1 = pA.y;
+    SegData sd;
 
-    for (int64_t i = ib; i <= ie; ++i) {
-      const int64_t qn = min(i + 1, ie), qp = min(i + 2, ie + 1);  // clamped prefetch rows
-      const double2 pNN = ld2(pb + qp * pitch);
-      const double2 rNx = ld2(rb + qn * pitch);
-      const double2 wNx = ld2(wb + qn * pitch);
+    for (int s0 = ib; s0 <= ie; s0 += SEG) {
+      const int s1 = min(s0 + SEG - 1, ie);
+      sd = seg_load(s0, s1);
+      for (int i = s0; i <= s1; ++i) {
+        const double2 pNN = ld2(pptr);  // row i+2 (padded)
+        const double2 rNx = ld2(rptr);  // row i+1
+        const double2 wNx = ld2(wptr);
+        pptr += pitch;
+        rptr += pitch;
+        wptr += pitch;
 
-      const int rl = int(i - ib);
-      const double eL = readlane(hL, rl), eR = readlane(hR, rl);
-      double pl0 = dpp_shr1(pB.y);
-      double pr1 = dpp_shl1(pB.x);
-      if (lane == 0) pl0 = eL;
-      if (lane == 63) pr1 = eR;
-      const int* rc = k.rowcls + (i + 1) * 4;
-      double rn0 = 0.0, rn1 = 0.0, wn0 = 0.0, wn1 = 0.0;
-      if (cl.own0) {
-        const CS c = cset<EXACT>(k, rc, i, c0, t0);
-        const double Ap = stencil<EXACT>(k, c, pm0, pB.x, pN.x, pl0, pB.y);
-        wn0 = wC.x + alpha * pB.x;
-        rn0 = rC.x - alpha * Ap;
-        szr += zval<EXACT>(c, rn0) * rn0;
+        const int rl = i - s0;
+        const RowCls ci = rcl_read(sd.rcv, rl);
+        const double eL = readlane(sd.hL, rl), eR = readlane(sd.hR, rl);
+        double pl0 = dpp_shr1(pB.y);
+        double pr1 = dpp_shl1(pB.x);
+        if (lane == 0) pl0 = eL;
+        if (lane == 63) pr1 = eR;
+        CS x0, x1;
+        if (!has_gen(ci, j0, jhi)) {
+          x0 = cset_fast<EXACT>(k, ci, c0);
+          x1 = cset_fast<EXACT>(k, ci, c1);
+        } else {
+          const int* rcp = k.rowcls + (i + 1) * 4;
+          x0 = cset<EXACT>(k, rcp, i, c0, tv_at(k, ca));
+          x1 = cset<EXACT>(k, rcp, i, c1, tv_at(k, ca + 1));
+        }
+        const double Ap0 = stencil<EXACT>(k, x0, pm0, pB.x, pN.x, pl0, pB.y);
+        const double Ap1 = stencil<EXACT>(k, x1, pm1, pB.y, pN.y, pB.x, pr1);
+        const double wn0 = wC.x + alpha * pB.x, wn1 = wC.y + alpha * pB.y;
+        const double rn0 = rC.x - alpha * Ap0, rn1 = rC.y - alpha * Ap1;
+        if (own0) szr += zval<EXACT>(x0, rn0) * rn0;
+        if (own1) szr += zval<EXACT>(x1, rn1) * rn1;
+        double* rd = r + i * pitch + c0;
+        double* wd = w + i * pitch + c0;
+        if (own1) {
+          *reinterpret_cast<double2*>(rd) = make_double2(rn0, rn1);
+          *reinterpret_cast<double2*>(wd) = make_double2(wn0, wn1);
+        } else if (own0) {
+          rd[0] = rn0;
+          wd[0] = wn0;
+        }
+        if (c0 == 1 && k.has[DOWN]) k.send_dn[i - 1] = rn0;
+        if (k.has[UP]) {
+          if (c0 == ny) k.send_up[i - 1] = rn0;
+          if (c1 == ny) k.send_up[i - 1] = rn1;
+        }
+        pm0 = pB.x;
+        pm1 = pB.y;
+        pB = pN;
+        pN = pNN;
+        rC = rNx;
+        wC = wNx;
       }
-      if (cl.own1) {
-        const CS c = cset<EXACT>(k, rc, i, c1, t1);
-        const double Ap = stencil<EXACT>(k, c, pm1, pB.y, pN.y, pB.x, pr1);
-        wn1 = wC.y + alpha * pB.y;
-        rn1 = rC.y - alpha * Ap;
-        szr += zval<EXACT>(c, rn1) * rn1;
-      }
-      double* rd = r + i * pitch + c0;
-      double* wd = w + i * pitch + c0;
-      if (cl.own1) {
-        *reinterpret_cast<double2*>(rd) = make_double2(rn0, rn1);
-        *reinterpret_cast<double2*>(wd) = make_double2(wn0, wn1);
-      } else if (cl.own0) {
-        rd[0] = rn0;
-        wd[0] = wn0;
-      }
-      if (c0 == 1 && k.has[DOWN]) k.send_dn[i - 1] = rn0;
-      if (k.has[UP]) {
-        if (c0 == k.ny) k.send_up[i - 1] = rn0;
-        if (c1 == k.ny) k.send_up[i - 1] = rn1;
-      }
-      pm0 = pB.x;
-      pm1 = pB.y;
-      pB = pN;
-      pN = pNN;
-      rC = rNx;
-      wC = wNx;
     }
   }
 

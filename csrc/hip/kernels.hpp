@@ -65,6 +65,7 @@ struct KParams {
   int nstrips;                   // 128-column wave strips across ny (+ halo column)
   int nitems;                    // nstrips × ceil(nx / ti)
   int nblocks;                   // persistent grid size of the marching kernels
+  int order;                     // item order: 0 chunk-major (compact active window), 1 strip-major
   int check_tol;                 // 0 → never stop on ‖Δw‖ (fixed-iteration runs)
   double D_in, D_out;            // exact-arithmetic diagonal in the interior / exterior class
   double dinv_in, dinv_out;      // fast-arithmetic 1/D in the interior / exterior class
@@ -74,7 +75,7 @@ struct KParams {
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
 constexpr int kWPB = 4;          // waves per block
 constexpr int kSW = 128;         // columns per wave strip (2 per lane, 16-B accesses)
-constexpr int kTImax = 64;       // max rows per work item (halo rows live in one lane each)
+constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live one per lane)
 
 void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
                  hipStream_t s);
