@@ -210,6 +210,17 @@ PYBIND11_MODULE(_native, m) {
       py::arg("prob"), py::arg("block"), py::arg("reduce_fn"), py::arg("exchange_fn"), py::arg("barrier_fn"),
       py::arg("opt") = SolveOptions(), py::arg("return_w") = false);
 
+  m.def("host_coefficients", [](const Problem& P, const Block& blk) {
+    std::vector<double> a, b;
+    std::vector<int> c;
+    host_coefficients(P, blk, a, b, c);
+    const int64_t R = blk.nx + 2, C = blk.ny + 2;
+    auto* heap = new std::vector<int>(std::move(c));
+    py::capsule owner(heap, [](void* p) { delete static_cast<std::vector<int>*>(p); });
+    py::array_t<int> ca({R, C}, {C * int64_t(sizeof(int)), int64_t(sizeof(int))}, heap->data(), owner);
+    return py::make_tuple(to_array(std::move(a), R, C), to_array(std::move(b), R, C), ca);
+  });
+
   // ---- device (HIP / RCCL) ----------------------------------------------
   m.def("device_count", &device_count);
   m.def("set_device", &set_device);

@@ -113,4 +113,63 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx,
   return out;
 }
 
+std::vector<double> chord_tables(const Problem& P, const Block& blk) {
+  const double h1 = P.h1(), h2 = P.h2();
+  std::vector<double> t((blk.nx + 4) * 4 + (blk.ny + 4) * 4, 0.0);
+  double* col = t.data();
+  double* row = t.data() + (blk.nx + 4) * 4;
+  for (int64_t li = -1; li <= blk.nx + 2; ++li) {
+    const int64_t gi = blk.i0 - 1 + li;
+    const double x = P.A1 + gi * h1;  // x_i exactly as the reference forms it
+    double* c = col + (li + 1) * 4;
+    c[0] = chord_half_vertical(x - 0.5 * h1, P.cx, P.cy, P.sx);
+    c[1] = x - 0.5 * h1;
+    c[2] = x + 0.5 * h1;
+    c[3] = x;
+  }
+  for (int64_t lj = -1; lj <= blk.ny + 2; ++lj) {
+    const int64_t gj = blk.j0 - 1 + lj;
+    const double y = P.A2 + gj * h2;
+    double* r = row + (lj + 1) * 4;
+    r[0] = y - 0.5 * h2;
+    r[1] = y + 0.5 * h2;
+    r[2] = chord_half_horizontal(y - 0.5 * h2, P.cx, P.cy, P.sy);
+    r[3] = y;
+  }
+  return t;
+}
+
+void host_coefficients(const Problem& P, const Block& blk, std::vector<double>& a, std::vector<double>& b,
+                       std::vector<int>& cls) {
+  // Host mirror of the kernels' cset(): class lookup, then exact face
+  // coefficients only in the boundary band (tests compare with fic_reg).
+  const std::vector<double> t = chord_tables(P, blk);
+  const double* col = t.data();
+  const double* row = t.data() + (blk.nx + 4) * 4;
+  const std::vector<int> rc = row_classes(col, row, blk.nx, blk.ny);
+  const double h1 = P.h1(), h2 = P.h2(), eps = P.eps(), inv_eps = 1.0 / eps;
+  const int64_t R = blk.nx + 2, C = blk.ny + 2;
+  a.assign(size_t(R * C), 0.0);
+  b.assign(size_t(R * C), 0.0);
+  cls.assign(size_t(R * C), 0);
+  for (int64_t q = 0; q < R; ++q)
+    for (int64_t lj = 0; lj < C; ++lj) {
+      const int* c = rc.data() + (q + 1) * 4;
+      const size_t at = size_t(q * C + lj);
+      if (lj >= c[0] && lj <= c[1]) {
+        a[at] = b[at] = 1.0;
+        cls[at] = 0;
+      } else if (lj < c[2] || lj > c[3]) {
+        a[at] = b[at] = inv_eps;
+        cls[at] = 1;
+      } else {
+        const double* rv = row + (lj + 1) * 4;
+        const double* cv = col + (q + 1) * 4;
+        a[at] = face_coef(chord_len(cv[0], rv[0], rv[1]), h2, eps);
+        b[at] = face_coef(chord_len(rv[2], cv[1], cv[2]), h1, eps);
+        cls[at] = 2;
+      }
+    }
+}
+
 }  // namespace pe

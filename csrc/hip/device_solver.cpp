@@ -153,30 +153,10 @@ DeviceSolver::~DeviceSolver() {
 KParams& DeviceSolver::params() { return *kp_; }
 
 void DeviceSolver::build_tables() {
-  const Problem& P = prob_;
-  const double h1 = P.h1(), h2 = P.h2();
-  std::vector<double> t((blk_.nx + 4) * 4 + (blk_.ny + 4) * 4, 0.0);
-  double* col = t.data();
-  double* row = t.data() + (blk_.nx + 4) * 4;
-  for (int64_t li = -1; li <= blk_.nx + 2; ++li) {
-    const int64_t gi = blk_.i0 - 1 + li;
-    const double x = P.A1 + gi * h1;
-    double* c = col + (li + 1) * 4;
-    c[0] = chord_half_vertical(x - 0.5 * h1, P.cx, P.cy, P.sx);
-    c[1] = x - 0.5 * h1;
-    c[2] = x + 0.5 * h1;
-    c[3] = x;
-  }
-  for (int64_t lj = -1; lj <= blk_.ny + 2; ++lj) {
-    const int64_t gj = blk_.j0 - 1 + lj;
-    const double y = P.A2 + gj * h2;
-    double* r = row + (lj + 1) * 4;
-    r[0] = y - 0.5 * h2;
-    r[1] = y + 0.5 * h2;
-    r[2] = chord_half_horizontal(y - 0.5 * h2, P.cx, P.cy, P.sy);
-    r[3] = y;
-  }
+  const std::vector<double> t = chord_tables(prob_, blk_);
   PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
+  const double* col = t.data();
+  const double* row = t.data() + (blk_.nx + 4) * 4;
   const std::vector<int> rc = row_classes(col, row, blk_.nx, blk_.ny);
   PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
 }

@@ -138,6 +138,14 @@ class DeviceSolver {
 // and exactly 1/eps for lj ∉ [out_lo, out_hi].  Conservative: anything else is
 // evaluated exactly.
 std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx, int64_t ny);
+// Chord tables of a block: (nx+4)×4 column entries {halfA, sB, eB, x} then
+// (ny+4)×4 row entries {sA, eA, halfB, y}, indexed by local index + 1.
+std::vector<double> chord_tables(const Problem& P, const Block& blk);
+// Host mirror of the kernels' coefficient path for local (li, lj) ∈
+// [0, nx+1] × [0, ny+1]: a(li, lj), b(li, lj) and the class (0 interior,
+// 1 exterior, 2 boundary band).  Row-major (nx+2) × (ny+2).
+void host_coefficients(const Problem& P, const Block& blk, std::vector<double>& a, std::vector<double>& b,
+                       std::vector<int>& cls);
 
 // P virtual ranks on ONE device (LocalComm).  Every rank runs the
 // same kernels and the same halo plan as under RCCL; the transport is

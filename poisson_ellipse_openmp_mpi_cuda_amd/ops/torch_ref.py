@@ -1,0 +1,173 @@
+"""Independent PyTorch fp64 oracle of the fictitious-domain operator and PCG.
+
+A vectorised re-statement of the reference numerics (fic_reg_local,
+mat_A_local, mat_D, dot_local, solve_mpi in
+stage2-mpi/poisson_mpi_decomp.cpp:124-460) on whole-grid tensors, used by the
+tests as an oracle for the native CPU backends and the gfx950 kernels.  It
+runs on any torch device ("cpu" here, "cuda" = HIP on the GPU box).
+
+Arrays use the reference's global indexing: shape (M+1, N+1), index [i, j]
+for node (x_i, y_j); interior unknowns are [1:M, 1:N]; the box boundary is
+held at 0 (Dirichlet).
+"""
+
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ..models.ellipse import EllipseProblem
+
+
+def _div(a: torch.Tensor, s: float) -> torch.Tensor:
+    """a / s, correctly rounded.  (PyTorch's CPU `tensor / python_scalar`
+    multiplies by the reciprocal, which differs from IEEE division in the last
+    bit — enough to break bitwise parity with the reference formulas.)"""
+    return a / torch.full_like(a, s)
+
+
+def _grid(prob: EllipseProblem, device, dtype=torch.float64):
+    h1, h2 = prob.h1, prob.h2
+    i = torch.arange(0, prob.M + 1, device=device, dtype=dtype)
+    j = torch.arange(0, prob.N + 1, device=device, dtype=dtype)
+    x = prob.A1 + i * h1
+    y = prob.A2 + j * h2
+    return x, y
+
+
+def _face_coef_np(l, h, eps):
+    import numpy as np
+
+    blend = (l / h) + (1.0 - l / h) / eps
+    out = np.where(l < 1e-9, 1.0 / eps, blend)
+    return np.where(np.abs(l - h) < 1e-9, 1.0, out)
+
+
+def assemble(prob: EllipseProblem, device="cpu"):
+    """Coefficients a, b (shape (M+1, N+1); row/col 0 unused) and RHS B.
+
+    Built with numpy (hardware IEEE sqrt / division: bit-identical to the
+    reference's C++ fic_reg) and moved to `device`; PyTorch's CPU sqrt and
+    scalar division are not always correctly rounded.
+    """
+    import numpy as np
+
+    h1, h2, eps = prob.h1, prob.h2, prob.eps
+    sx, sy = math.sqrt(prob.cx), math.sqrt(prob.cy)
+    x = prob.A1 + np.arange(0, prob.M + 1, dtype=np.float64) * h1
+    y = prob.A2 + np.arange(0, prob.N + 1, dtype=np.float64) * h2
+    X = x[:, None] + np.zeros((1, y.size))
+    Y = y[None, :] + np.zeros((x.size, 1))
+    with np.errstate(invalid="ignore"):
+        # vertical face at x_i - h1/2 over [y_j - h2/2, y_j + h2/2]
+        c = X - 0.5 * h1
+        half = np.sqrt(np.maximum(0.0, (1.0 - prob.cx * c * c) / prob.cy))
+        la = np.maximum(0.0, np.minimum(Y + 0.5 * h2, half) - np.maximum(Y - 0.5 * h2, -half))
+        la = np.where(np.abs(sx * c) >= 1.0, 0.0, la)
+        # horizontal face at y_j - h2/2 over [x_i - h1/2, x_i + h1/2]
+        c2 = Y - 0.5 * h2
+        half2 = np.sqrt(np.maximum(0.0, (1.0 - prob.cy * c2 * c2) / prob.cx))
+        lb = np.maximum(0.0, np.minimum(X + 0.5 * h1, half2) - np.maximum(X - 0.5 * h1, -half2))
+        lb = np.where(np.abs(sy * c2) >= 1.0, 0.0, lb)
+    a = _face_coef_np(la, h2, eps)
+    b = _face_coef_np(lb, h1, eps)
+    inside = (prob.cx * X * X + prob.cy * Y * Y) < 1.0
+    B = np.where(inside, prob.F, 0.0)
+    B[0, :] = B[-1, :] = 0.0
+    B[:, 0] = B[:, -1] = 0.0
+    t = lambda v: torch.from_numpy(np.ascontiguousarray(v)).to(device)  # noqa: E731
+    return t(a), t(b), t(B)
+
+
+def apply_A(p, a, b, h1, h2):
+    """(A p) on interior nodes; boundary rows/cols of the result are 0."""
+    out = torch.zeros_like(p)
+    pc = p[1:-1, 1:-1]
+    Ax = (-1.0 / h1) * (_div(a[2:, 1:-1] * (p[2:, 1:-1] - pc), h1) - _div(a[1:-1, 1:-1] * (pc - p[:-2, 1:-1]), h1))
+    Ay = (-1.0 / h2) * (_div(b[1:-1, 2:] * (p[1:-1, 2:] - pc), h2) - _div(b[1:-1, 1:-1] * (pc - p[1:-1, :-2]), h2))
+    out[1:-1, 1:-1] = Ax + Ay
+    return out
+
+
+def diag(a, b, h1, h2):
+    """Jacobi diagonal D on interior nodes (0 elsewhere)."""
+    D = torch.zeros_like(a)
+    D[1:-1, 1:-1] = _div(a[2:, 1:-1] + a[1:-1, 1:-1], h1 * h1) + _div(b[1:-1, 2:] + b[1:-1, 1:-1], h2 * h2)
+    return D
+
+
+def apply_Dinv(r, D):
+    z = torch.zeros_like(r)
+    m = D != 0
+    z[m] = r[m] / D[m]
+    return z
+
+
+def dot(u, v, h1, h2):
+    return float((u[1:-1, 1:-1] * v[1:-1, 1:-1]).sum()) * h1 * h2
+
+
+@dataclass
+class TorchPCGResult:
+    iters: int
+    converged: bool
+    w: torch.Tensor
+    l2_err: float
+    max_err: float
+    history: list
+
+
+def pcg(prob: EllipseProblem, device="cpu", w0: Optional[torch.Tensor] = None, max_iter: Optional[int] = None,
+        keep_history: bool = False) -> TorchPCGResult:
+    """Reference-algorithm Jacobi PCG (stage2 solve_mpi order of operations)."""
+    a, b, B = assemble(prob, device)
+    h1, h2 = prob.h1, prob.h2
+    D = diag(a, b, h1, h2)
+    w = torch.zeros_like(B) if w0 is None else w0.clone()
+    r = B - apply_A(w, a, b, h1, h2)
+    r[0, :] = r[-1, :] = 0
+    r[:, 0] = r[:, -1] = 0
+    z = apply_Dinv(r, D)
+    p = z.clone()
+    zr_old = dot(z, r, h1, h2)
+    cap = prob.iter_cap if max_iter is None else max_iter
+    hist = []
+    converged = False
+    k = 0
+    for k in range(1, cap + 1):
+        Ap = apply_A(p, a, b, h1, h2)
+        den = dot(Ap, p, h1, h2)
+        if abs(den) < 1e-15:
+            break
+        alpha = zr_old / den
+        dw = alpha * p
+        w = w + dw
+        r = r - alpha * Ap
+        z = apply_Dinv(r, D)
+        zr_new = dot(z, r, h1, h2)
+        d2 = float((dw[1:-1, 1:-1] ** 2).sum())
+        diff = math.sqrt(d2 * h1 * h2) if prob.norm == "weighted" else math.sqrt(d2)
+        if keep_history:
+            hist.append(diff)
+        if diff < prob.tol:
+            converged = True
+            break
+        beta = zr_new / zr_old
+        zr_old = zr_new
+        p = z + beta * p
+    l2, mx = error_vs_analytic(prob, w)
+    return TorchPCGResult(k, converged, w, l2, mx, hist)
+
+
+def error_vs_analytic(prob: EllipseProblem, w: torch.Tensor):
+    """(L2 error in D, h-weighted; max error in D) against u = F(1-cx x²-cy y²)/(2cx+2cy)."""
+    x, y = _grid(prob, w.device)
+    X = x[:, None]
+    Y = y[None, :]
+    inside = (prob.cx * X * X + prob.cy * Y * Y) < 1.0
+    u = prob.F / (2.0 * prob.cx + 2.0 * prob.cy) * (1.0 - prob.cx * X * X - prob.cy * Y * Y)
+    e = torch.where(inside, w - u, torch.zeros_like(w))[1:-1, 1:-1]
+    return math.sqrt(float((e * e).sum()) * prob.h1 * prob.h2), float(e.abs().max())

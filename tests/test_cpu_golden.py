@@ -1,0 +1,65 @@
+"""CPU backends reproduce the reference's published iteration counts exactly
+(Этап1.pdf p.4, Этап2.pdf p.5, Этап3.pdf p.8, Этап_4_1213.pdf p.11) and the
+survey's replica values (40×40 → 50 weighted / 61 stage0
+unweighted; L2 errors)."""
+
+import numpy as np
+import pytest
+
+from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem, solve
+from poisson_ellipse_openmp_mpi_cuda_amd.models.ellipse import GOLDEN_ITERS, GOLDEN_L2
+
+
+@pytest.mark.parametrize("M,N,norm", [(40, 40, "weighted"), (40, 40, "unweighted"), (10, 10, "unweighted"),
+                                      (20, 20, "unweighted"), (400, 600, "weighted")])
+def test_serial_golden(M, N, norm):
+    rep = solve(EllipseProblem(M, N, norm=norm), backend="serial")
+    assert rep.converged
+    assert rep.iters == GOLDEN_ITERS[(M, N, norm)]
+    if (M, N) in GOLDEN_L2 and norm == "weighted":
+        assert rep.l2_err == pytest.approx(GOLDEN_L2[(M, N)], rel=5e-3)
+
+
+def test_omp_800x1200_golden():
+    rep = solve(EllipseProblem(800, 1200), backend="omp", threads=8)
+    assert rep.iters == 989 and rep.converged
+    assert rep.l2_err == pytest.approx(GOLDEN_L2[(800, 1200)], rel=5e-3)
+    assert rep.max_outside < 1e-6  # fictitious domain: w ≈ 0 outside D
+
+
+def test_weighted_10x10_is_15():
+    # the shipped weighted-norm code gives 15 (stage0's unweighted rule: 17)
+    assert solve(EllipseProblem(10, 10), backend="serial").iters == 15
+
+
+@pytest.mark.parametrize("ranks,threads", [(2, 1), (3, 1), (4, 2), (8, 1)])
+def test_thread_ranks_match_serial(ranks, threads):
+    prob = EllipseProblem(120, 90)
+    ref = solve(prob, backend="serial", return_w=True)
+    rep = solve(prob, backend="ranks", ranks=ranks, threads=threads, return_w=True)
+    assert rep.iters == ref.iters
+    assert rep.Px * rep.Py == ranks
+    np.testing.assert_allclose(rep.w, ref.w, rtol=0, atol=1e-12)
+
+
+def test_omp_threads_deterministic():
+    prob = EllipseProblem(100, 150)
+    a = solve(prob, backend="omp", threads=4, return_w=True, keep_history=True)
+    b = solve(prob, backend="omp", threads=4, return_w=True, keep_history=True)
+    assert a.iters == b.iters
+    assert np.array_equal(a.w, b.w)
+
+
+def test_random_init_converges_to_same_solution():
+    prob = EllipseProblem(60, 60)
+    z = solve(prob, backend="serial", return_w=True)
+    r = solve(prob, backend="serial", init="random", seed=7, return_w=True)
+    assert r.converged and r.iters != z.iters
+    assert np.max(np.abs(r.w - z.w)) < 1e-4
+
+
+def test_general_ellipse_family_analytic_error():
+    # circle x²+y²<1 in [-1,1]²: u = (1-x²-y²)/4
+    prob = EllipseProblem(128, 128, A2=-1.0, B2=1.0, cy=1.0)
+    rep = solve(prob, backend="omp", threads=4)
+    assert rep.converged and rep.l2_err < 1e-2

@@ -1,0 +1,72 @@
+"""Decomposition: reference-compatible process grid, partition properties,
+neighbour symmetry (reference: stage2-mpi/poisson_mpi_decomp.cpp:60-111,
+:246-252)."""
+
+import math
+
+import pytest
+
+from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+
+def ref_grid(P):
+    Px = int(math.sqrt(P))
+    while Px > 1 and P % Px:
+        Px -= 1
+    return Px, P // Px
+
+
+@pytest.mark.parametrize("P", range(1, 33))
+def test_reference_grid_matches_formula(nat, P):
+    pg = nat.choose_process_grid_reference(P)
+    assert (pg.Px, pg.Py) == ref_grid(P)
+    assert D.process_grid(P, 400, 600, "reference") == ref_grid(P)
+
+
+def test_aspect_grid_baseline_configs():
+    # BASELINE.json: 2 GPUs "2x1" at 4096², 8 GPUs "4x2" at 8192²
+    assert D.process_grid(2, 4096, 4096) == (2, 1)
+    assert D.process_grid(8, 8192, 8192) == (4, 2)
+    assert D.process_grid(1, 8192, 8192) == (1, 1)
+    assert D.process_grid(4, 8192, 8192) in ((2, 2), (4, 1))
+
+
+@pytest.mark.parametrize("M,N,P,mode", [(40, 40, 4, "reference"), (400, 600, 6, "aspect"), (123, 77, 8, "aspect"),
+                                        (37, 500, 5, "reference"), (1000, 9, 7, "aspect")])
+def test_partition_covers_disjoint_balanced(M, N, P, mode):
+    blks = D.blocks(M, N, P, mode)
+    seen = [[0] * (N - 1) for _ in range(M - 1)]
+    nxs, nys = {}, {}
+    for b in blks:
+        assert b.nx >= 1 and b.ny >= 1
+        assert b.pitch >= b.ny + 2 and b.pitch % 8 == 0
+        assert (b.base + 1 * b.pitch + 1) % 8 == 0  # owned rows 64-B aligned
+        for i in range(b.i0, b.i1 + 1):
+            for j in range(b.j0, b.j1 + 1):
+                seen[i - 1][j - 1] += 1
+        nxs.setdefault(b.px, b.nx)
+        nys.setdefault(b.py, b.ny)
+        assert nxs[b.px] == b.nx and nys[b.py] == b.ny
+    assert all(v == 1 for row in seen for v in row)
+    assert max(nxs.values()) - min(nxs.values()) <= 1
+    assert max(nys.values()) - min(nys.values()) <= 1
+    # remainder goes to the lowest coordinates (reference :84-110)
+    assert sorted(nxs.items(), key=lambda t: t[0]) == sorted(nxs.items(), key=lambda t: -t[1])
+
+
+@pytest.mark.parametrize("P", [1, 2, 3, 4, 6, 8, 12])
+def test_neighbour_symmetry(P):
+    blks = D.blocks(300, 200, P, "aspect")
+    opp = {0: 1, 1: 0, 2: 3, 3: 2}
+    for b in blks:
+        for d, n in enumerate(b.nbr):
+            if n < 0:
+                continue
+            nb = blks[n]
+            assert nb.nbr[opp[d]] == b.rank
+            if d < 2:  # x-neighbours share the j range (contiguous rows exchanged)
+                assert (nb.j0, nb.j1) == (b.j0, b.j1)
+            else:
+                assert (nb.i0, nb.i1) == (b.i0, b.i1)
+        assert (b.nbr[0] < 0) == (b.px == 0) and (b.nbr[1] < 0) == (b.px == b.Px - 1)
+        assert (b.nbr[2] < 0) == (b.py == 0) and (b.nbr[3] < 0) == (b.py == b.Py - 1)
