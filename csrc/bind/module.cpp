@@ -242,6 +242,33 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("uid"), py::arg("rank"), py::arg("size"));
   m.def(
+      "make_host_staged_comm",
+      [](int rank, int size, py::function reduce_fn, py::function exchange_fn, py::function barrier_fn) {
+        auto reduce = [reduce_fn](double* buf, int n, bool is_max) {
+          py::gil_scoped_acquire g;
+          py::array_t<double> a({n}, {int64_t(sizeof(double))}, buf, py::none());
+          reduce_fn(a, is_max);
+        };
+        auto exch = [exchange_fn](const std::vector<Exchange>& ex) {
+          py::gil_scoped_acquire g;
+          py::list items;
+          for (const auto& e : ex) {
+            py::array_t<double> s({e.count}, {int64_t(sizeof(double))}, const_cast<double*>(e.send), py::none());
+            py::array_t<double> r({e.count}, {int64_t(sizeof(double))}, e.recv, py::none());
+            items.append(py::make_tuple(e.dir, e.peer, s, r));
+          }
+          exchange_fn(items);
+        };
+        auto bar = [barrier_fn]() {
+          py::gil_scoped_acquire g;
+          barrier_fn();
+        };
+        auto h = std::make_unique<CommHandle>();
+        h->comm = make_callback_device_comm(rank, size, reduce, exch, bar);
+        return h;
+      },
+      py::arg("rank"), py::arg("size"), py::arg("reduce_fn"), py::arg("exchange_fn"), py::arg("barrier_fn"));
+  m.def(
       "make_rccl_comm_from_handle",
       [](uintptr_t handle) {
         auto h = std::make_unique<CommHandle>();

@@ -89,7 +89,59 @@ class RcclComm final : public DeviceComm {
   double* scratch_ = nullptr;
 };
 
+class HostStagedComm final : public DeviceComm {
+ public:
+  HostStagedComm(int rank, int size, CallbackHostComm::ReduceFn r, CallbackHostComm::ExchangeFn e,
+                 CallbackHostComm::BarrierFn b)
+      : host_(rank, size, std::move(r), std::move(e), std::move(b)) {}
+  int rank() const override { return host_.rank(); }
+  int size() const override { return host_.size(); }
+  void allreduce_sum(double* d, int n, hipStream_t s) override { reduce(d, n, s, false); }
+  void allreduce_max(double* d, int n, hipStream_t s) override { reduce(d, n, s, true); }
+  void exchange(const std::vector<Exchange>& ex, hipStream_t s) override {
+    if (ex.empty()) return;
+    PE_HIP_CHECK(hipStreamSynchronize(s));
+    std::vector<std::vector<double>> snd(ex.size()), rcv(ex.size());
+    std::vector<Exchange> hx;
+    for (size_t k = 0; k < ex.size(); ++k) {
+      snd[k].resize(size_t(ex[k].count));
+      rcv[k].resize(size_t(ex[k].count));
+      PE_HIP_CHECK(hipMemcpy(snd[k].data(), ex[k].send, sizeof(double) * ex[k].count, hipMemcpyDeviceToHost));
+      hx.push_back(Exchange{ex[k].dir, ex[k].peer, snd[k].data(), rcv[k].data(), ex[k].count});
+    }
+    host_.exchange(hx);
+    for (size_t k = 0; k < ex.size(); ++k)
+      PE_HIP_CHECK(hipMemcpy(ex[k].recv, rcv[k].data(), sizeof(double) * ex[k].count, hipMemcpyHostToDevice));
+  }
+  void host_max(double* h, int n, hipStream_t s) override {
+    PE_HIP_CHECK(hipStreamSynchronize(s));
+    host_.allreduce_max(h, n);
+  }
+  void barrier(hipStream_t s) override {
+    PE_HIP_CHECK(hipStreamSynchronize(s));
+    host_.barrier();
+  }
+  std::string name() const override { return "host-staged"; }
+
+ private:
+  void reduce(double* d, int n, hipStream_t s, bool is_max) {
+    std::vector<double> h(static_cast<size_t>(n));
+    PE_HIP_CHECK(hipStreamSynchronize(s));
+    PE_HIP_CHECK(hipMemcpy(h.data(), d, sizeof(double) * n, hipMemcpyDeviceToHost));
+    if (is_max) host_.allreduce_max(h.data(), n);
+    else host_.allreduce_sum(h.data(), n);
+    PE_HIP_CHECK(hipMemcpy(d, h.data(), sizeof(double) * n, hipMemcpyHostToDevice));
+  }
+  CallbackHostComm host_;
+};
+
 }  // namespace
+
+std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
+                                                      CallbackHostComm::ExchangeFn exch,
+                                                      CallbackHostComm::BarrierFn barrier) {
+  return std::make_unique<HostStagedComm>(rank, size, std::move(reduce), std::move(exch), std::move(barrier));
+}
 
 std::string rccl_unique_id() {
   ncclUniqueId id;

@@ -64,6 +64,15 @@ std::unique_ptr<DeviceComm> make_rccl_comm(const std::string& uid, int rank, int
 // Wrap an existing ncclComm_t (e.g. one owned by another runtime); not owned.
 std::unique_ptr<DeviceComm> make_rccl_comm_from_handle(void* nccl_comm);
 
+// Host-staged transport over caller callbacks (e.g. torch.distributed gloo):
+// device → host copy, host collective, host → device copy — the reference's
+// stage-4 pattern (poisson_mpi_cuda2.cu:331-500).  A test/fallback transport
+// for several ranks sharing one GPU (RCCL refuses duplicate devices); the
+// production transport is RCCL.
+std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
+                                                      CallbackHostComm::ExchangeFn exch,
+                                                      CallbackHostComm::BarrierFn barrier);
+
 namespace dev {
 struct DevState;
 struct KParams;

@@ -30,6 +30,9 @@ import torch.distributed as dist
 from .._loader import native
 
 
+_GLOO = None
+
+
 @dataclass
 class DistContext:
     rank: int
@@ -77,11 +80,21 @@ def _store():
 
 
 def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
-    """Native RCCL communicator over all ranks; unique id via the torch store."""
+    """Native device communicator over all ranks.
+
+    Default: RCCL over xGMI, unique id via the torch store.  PE_COMM=host
+    selects the host-staged gloo transport (several ranks on one GPU — RCCL
+    refuses duplicate devices — for testing the multi-process path on a
+    single-GPU box)."""
     nat = native()
     nat.set_device(ctx.local_rank % max(1, nat.device_count()))
     if ctx.world == 1:
         return None
+    if os.environ.get("PE_COMM", "rccl") == "host":
+        global _GLOO
+        if _GLOO is None:
+            _GLOO = dist.new_group(backend="gloo")
+        return nat.make_host_staged_comm(ctx.rank, ctx.world, *gloo_callbacks(_GLOO))
     store = _store()
     key = f"{tag}/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
     if ctx.rank == 0:

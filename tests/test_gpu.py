@@ -168,3 +168,29 @@ def test_graft_smoke(gpu):
     import __graft_entry__ as g
 
     g.smoke()
+
+
+def test_two_process_device_path_host_staged(gpu):
+    """torchrun-style 2-process job on the one GPU: torch.distributed bootstrap,
+    per-rank blocks, halo plan, timer reduction and gather — with the
+    host-staged transport (RCCL refuses two ranks on one device)."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+           "--quiet", "400", "600"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["iters"] == 546 and d["ranks"] == 2 and d["Px"] * d["Py"] == 2
+    assert d["l2_err"] == pytest.approx(3.06e-4, rel=5e-3)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "30", "--warmup", "3", "--grid", "512", "512"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
