@@ -51,6 +51,7 @@ def main() -> int:
     ap.add_argument("--decomp", default="aspect", choices=("aspect", "reference"))
     ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solve")
     ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused"))
     a = ap.parse_args()
     M, N = (a.grid[0], a.grid[-1])
 
@@ -80,6 +81,7 @@ def main() -> int:
     opt = nat.SolveOptions()
     opt.check_tol = False  # fixed work per step in the timed region
     opt.variant = a.variant
+    opt.algo = {"auto": 0, "classic": 1, "fused": 2}[a.algo]
     solver = nat.DeviceSolver(P, blk, comm, opt)
 
     def barrier():
@@ -121,6 +123,7 @@ def main() -> int:
     if not a.no_solve:
         sopt = nat.SolveOptions()
         sopt.variant = a.variant
+        sopt.algo = opt.algo
         full = nat.DeviceSolver(P, blk, comm, sopt)
         barrier()
         res = full.solve()
@@ -153,6 +156,7 @@ def main() -> int:
             "seq_len": None,
             "parallelism": f"2d-decomp {blk.Px}x{blk.Py} (RCCL)" if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
+            "algo": "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else "classic (2 kernels, 2 allreduces / iter)",
         },
         "valid": valid,
     }

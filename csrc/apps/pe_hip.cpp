@@ -2,7 +2,7 @@
 // MI355X: one process per GPU, RCCL over xGMI, device-resident PCG.
 //
 //   pe_hip [--tol 1e-6] [--max-iter K] [--decomp aspect|reference]
-//          [--init zero|random] [--seed S] [--variant 0|1] [--chunk K]
+//          [--init zero|random] [--seed S] [--variant 0|1] [--algo auto|classic|fused] [--chunk K]
 //          [--no-graph] [--timing] [--vranks P] [--json] [M N]
 //
 // Multi-GPU: `pe_launch -n 8 bin/pe_hip 8192 8192` (or torchrun-style env
@@ -72,6 +72,10 @@ int main(int argc, char** argv) {
   opt.init = args.get("init", "zero") == "random" ? Init::Random : Init::Zero;
   opt.seed = uint64_t(args.geti("seed", 1234));
   opt.variant = int(args.geti("variant", 0));
+  {
+    const std::string a = args.get("algo", "auto");
+    opt.algo = a == "classic" ? 1 : a == "fused" ? 2 : 0;
+  }
   opt.chunk = int(args.geti("chunk", 0));
   opt.use_graph = !args.flag("no-graph");
   opt.timing = args.flag("timing");

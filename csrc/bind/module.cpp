@@ -50,6 +50,12 @@ py::dict state_dict(const dev::DevState& s) {
   d["iter"] = s.iter;
   d["done"] = s.done;
   d["status"] = s.status;
+  d["started"] = s.started;
+  d["gprev"] = s.gprev;
+  d["fs"] = py::make_tuple(py::make_tuple(s.fs[0][0], s.fs[0][1], s.fs[0][2], s.fs[0][3], s.fs[0][4], s.fs[0][5],
+                                          s.fs[0][6]),
+                           py::make_tuple(s.fs[1][0], s.fs[1][1], s.fs[1][2], s.fs[1][3], s.fs[1][4], s.fs[1][5],
+                                          s.fs[1][6]));
   return d;
 }
 
@@ -134,7 +140,8 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("use_graph", &SolveOptions::use_graph)
       .def_readwrite("timing", &SolveOptions::timing)
       .def_readwrite("check_tol", &SolveOptions::check_tol)
-      .def_readwrite("variant", &SolveOptions::variant);
+      .def_readwrite("variant", &SolveOptions::variant)
+      .def_readwrite("algo", &SolveOptions::algo);
 
   py::class_<SolveResult>(m, "SolveResult")
       .def_readonly("iters", &SolveResult::iters)
@@ -324,12 +331,12 @@ PYBIND11_MODULE(_native, m) {
            })
       .def("field",
            [](DeviceSolver& s, int which) {
-             const Block& b = s.block();
-             std::vector<double> v(size_t(b.rows * b.pitch));
+             std::vector<double> v(size_t(s.field_rows() * s.field_cols()));
              s.copy_field(which, v.data());
-             return to_array(std::move(v), b.rows, b.pitch);
+             return to_array(std::move(v), s.field_rows(), s.field_cols());
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
+      .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("blocks", [](DeviceSolver& s) { return dev::grid_blocks(s.params()); })
       .def_property_readonly("block", &DeviceSolver::block);
@@ -355,6 +362,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("device_apply_A", [](const Problem& P, const Block& blk, py::array_t<double, py::array::c_style> p) {
     if (p.size() != blk.rows * blk.pitch) throw std::invalid_argument("p must be rows x pitch");
     SolveOptions opt;
+    opt.algo = 1;  // classic layout: p is rows × pitch of the block
     DeviceSolver s(P, blk, nullptr, opt);
     const size_t bytes = sizeof(double) * blk.rows * blk.pitch;
     double *dp = nullptr, *dA = nullptr;
@@ -372,6 +380,7 @@ PYBIND11_MODULE(_native, m) {
   });
   m.def("device_coefficients", [](const Problem& P, const Block& blk) {
     SolveOptions opt;
+    opt.algo = 1;
     DeviceSolver s(P, blk, nullptr, opt);
     const size_t n = size_t(blk.rows * blk.pitch), bytes = sizeof(double) * n;
     double* d = nullptr;

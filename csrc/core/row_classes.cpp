@@ -56,8 +56,8 @@ int64_t last_true(int64_t lo, int64_t hi, P pred) {
 
 }  // namespace
 
-std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx, int64_t ny) {
-  const int64_t L = -1, H = ny + 2;  // row-table index range
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi) {
+  const int64_t L = -1, H = cols_hi;  // row-table index range
   auto sA = [&](int64_t j) { return rowT[(j + 1) * 4 + 0]; };
   auto eA = [&](int64_t j) { return rowT[(j + 1) * 4 + 1]; };
   auto hB = [&](int64_t j) { return rowT[(j + 1) * 4 + 2]; };
@@ -93,8 +93,8 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx,
     return b_level(std::max(-eB, sB), true);
   };
 
-  std::vector<int> out(size_t(nx + 4) * 4, 0);
-  for (int64_t q = -1; q <= nx + 1; ++q) {
+  std::vector<int> out(size_t(rows_hi + 2) * 4, 0);
+  for (int64_t q = -1; q <= rows_hi - 1; ++q) {
     const Iv bi = b_in(q);
     const Iv in = meet(meet(a_in(q), a_in(q + 1)), meet(bi, shift(bi, -1)));
     const Iv bn = b_notout(q);
@@ -113,12 +113,12 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx,
   return out;
 }
 
-std::vector<double> chord_tables(const Problem& P, const Block& blk) {
+std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi) {
   const double h1 = P.h1(), h2 = P.h2();
-  std::vector<double> t((blk.nx + 4) * 4 + (blk.ny + 4) * 4, 0.0);
+  std::vector<double> t((rows_hi + 2) * 4 + (cols_hi + 2) * 4, 0.0);
   double* col = t.data();
-  double* row = t.data() + (blk.nx + 4) * 4;
-  for (int64_t li = -1; li <= blk.nx + 2; ++li) {
+  double* row = t.data() + (rows_hi + 2) * 4;
+  for (int64_t li = -1; li <= rows_hi; ++li) {
     const int64_t gi = blk.i0 - 1 + li;
     const double x = P.A1 + gi * h1;  // x_i exactly as the reference forms it
     double* c = col + (li + 1) * 4;
@@ -127,7 +127,7 @@ std::vector<double> chord_tables(const Problem& P, const Block& blk) {
     c[2] = x + 0.5 * h1;
     c[3] = x;
   }
-  for (int64_t lj = -1; lj <= blk.ny + 2; ++lj) {
+  for (int64_t lj = -1; lj <= cols_hi; ++lj) {
     const int64_t gj = blk.j0 - 1 + lj;
     const double y = P.A2 + gj * h2;
     double* r = row + (lj + 1) * 4;
@@ -143,10 +143,10 @@ void host_coefficients(const Problem& P, const Block& blk, std::vector<double>& 
                        std::vector<int>& cls) {
   // Host mirror of the kernels' cset(): class lookup, then exact face
   // coefficients only in the boundary band (tests compare with fic_reg).
-  const std::vector<double> t = chord_tables(P, blk);
+  const std::vector<double> t = chord_tables(P, blk, blk.nx + 2, blk.ny + 2);
   const double* col = t.data();
   const double* row = t.data() + (blk.nx + 4) * 4;
-  const std::vector<int> rc = row_classes(col, row, blk.nx, blk.ny);
+  const std::vector<int> rc = row_classes(col, row, blk.nx + 2, blk.ny + 2);
   const double h1 = P.h1(), h2 = P.h2(), eps = P.eps(), inv_eps = 1.0 / eps;
   const int64_t R = blk.nx + 2, C = blk.ny + 2;
   a.assign(size_t(R * C), 0.0);

@@ -33,19 +33,72 @@ using clk = std::chrono::steady_clock;
 double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 }  // namespace
 
+// Can the single-sweep kernel run this block?  It needs the fast arithmetic
+// variant and neighbours at least two nodes deep in every split direction
+// (its halo is two rows / columns deep).
+static bool fused_possible(const Problem& P, const Block& b) {
+  const int64_t min_rows = (P.M - 1) / b.Px, min_cols = (P.N - 1) / b.Py;
+  return (b.Px == 1 || min_rows >= 2) && (b.Py == 1 || min_cols >= 2);
+}
+
 DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* comm, const SolveOptions& opt)
     : prob_(prob), blk_(blk), comm_(comm), opt_(opt), kp_(std::make_unique<KParams>()) {
   if (!comm_) {
     self_ = std::make_unique<SelfDeviceComm>();
     comm_ = self_.get();
   }
+  const bool can_fuse = opt_.variant == 0 && fused_possible(prob_, blk_);
+  if (opt_.algo == 2 && !can_fuse)
+    throw std::invalid_argument("single-sweep algorithm needs variant 0 and >= 2 rows/columns per split block");
+  fused_ = opt_.algo == 2 || (opt_.algo == 0 && can_fuse);
+
   PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
-  const int64_t A = blk_.alloc;
-  PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * A * 4));
-  const int64_t ntab = (blk_.nx + 4) * 4 + (blk_.ny + 4) * 4;
+  KParams& k = *kp_;
+  std::memset(&k, 0, sizeof(KParams));
+  const int64_t nx = blk_.nx, ny = blk_.ny;
+  int ti = fused_ ? 16 : 8;  // 8192² sweeps: classic 8 rows, single-sweep 16 (4 halo rows per item)
+  if (const char* e = std::getenv("PE_TI")) ti = std::max(1, std::atoi(e));
+  if (fused_) ti = std::min(ti, dev::kFTImax);
+
+  int64_t strips = 0, rows_hi = nx + 2, cols_hi = ny + 2;
+  if (fused_) {
+    // Planes: columns -1 .. 124·nstrips+2 (strip loads never leave the row),
+    // rows -1 .. nx+4 (two prefetch rows past the halo).  x[b] interleaves the
+    // r and p planes by row.
+    strips = (ny + dev::kFSW - 1) / dev::kFSW;
+    plane_ = ((dev::kFSW * strips + 4 + 7) / 8) * 8;
+    const int64_t rows = nx + 6;
+    xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
+    wsize_ = ((rows * plane_ + 64 + 31) / 32) * 32;
+    PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * (2 * xsize_ + wsize_)));
+    k.pitch = 2 * plane_;
+    k.wpitch = plane_;
+    k.poff = plane_;
+    k.x[0] = fields_ + k.pitch + 1;  // local (0, 0): row -1, column -1 at element 0
+    k.x[1] = fields_ + xsize_ + k.pitch + 1;
+    k.w = fields_ + 2 * xsize_ + plane_ + 1;
+    k.r = k.x[0];
+    k.p[0] = k.x[0] + plane_;
+    k.p[1] = k.x[1] + plane_;
+    hsize_ = std::max<int64_t>(1, nx) * 4;
+    rows_hi = nx + 3;
+    cols_hi = dev::kFSW * strips + 3;
+  } else {
+    strips = (ny + dev::kSW - 1) / dev::kSW;
+    const int64_t A = blk_.alloc;
+    PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * A * 4));
+    k.pitch = blk_.pitch;
+    k.wpitch = blk_.pitch;
+    k.r = fields_ + blk_.base;
+    k.w = fields_ + A + blk_.base;
+    k.p[0] = fields_ + 2 * A + blk_.base;
+    k.p[1] = fields_ + 3 * A + blk_.base;
+    hsize_ = std::max<int64_t>(1, nx);
+  }
+  const int64_t ntab = (rows_hi + 2) * 4 + (cols_hi + 2) * 4;
   PE_HIP_CHECK(hipMalloc(&tables_, sizeof(double) * ntab));
-  PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * (blk_.nx + 4) * 4));
-  PE_HIP_CHECK(hipMalloc(&halo_, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4));
+  PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * (rows_hi + 2) * 4));
+  PE_HIP_CHECK(hipMalloc(&halo_, sizeof(double) * hsize_ * 4));
   PE_HIP_CHECK(hipMalloc(&st_, sizeof(DevState)));
   PE_HIP_CHECK(hipHostMalloc(&hst_, sizeof(DevState) * 2, hipHostMallocDefault));
   std::memset(hst_, 0, sizeof(DevState) * 2);
@@ -54,11 +107,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   PE_HIP_CHECK(hipEventCreate(&t0_));
   PE_HIP_CHECK(hipEventCreate(&t1_));
 
-  KParams& k = *kp_;
-  std::memset(&k, 0, sizeof(KParams));
-  k.nx = blk_.nx;
-  k.ny = blk_.ny;
-  k.pitch = blk_.pitch;
+  k.fused = fused_ ? 1 : 0;
+  k.nx = nx;
+  k.ny = ny;
   k.M = prob_.M;
   k.N = prob_.N;
   k.gi0 = blk_.i0 - 1;
@@ -83,30 +134,22 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   for (int d = 0; d < 4; ++d) k.has[d] = blk_.has(d) ? 1 : 0;
   k.colT = tables_;
   k.rowcls = rowcls_;
-  k.rowT = tables_ + (blk_.nx + 4) * 4;
-  k.r = fields_ + blk_.base;
-  k.w = fields_ + A + blk_.base;
-  k.p[0] = fields_ + 2 * A + blk_.base;
-  k.p[1] = fields_ + 3 * A + blk_.base;
-  const int64_t hx = std::max<int64_t>(1, blk_.nx);
+  k.rowT = tables_ + (rows_hi + 2) * 4;
   k.send_dn = halo_;
-  k.send_up = halo_ + hx;
-  k.recv_dn = halo_ + 2 * hx;
-  k.recv_up = halo_ + 3 * hx;
+  k.send_up = halo_ + hsize_;
+  k.recv_dn = halo_ + 2 * hsize_;
+  k.recv_up = halo_ + 3 * hsize_;
   k.st = st_;
   k.check_tol = opt_.check_tol ? 1 : 0;
-  // Work decomposition: 128-column wave strips × `ti`-row chunks, dealt
-  // round-robin (chunk-major) to a persistent grid of ~16 waves per CU, so
-  // the waves running at any moment cover a compact window of rows
-  // (measured: long per-wave row ranges spread over the whole array run
-  // 25 % slower than 8-16-row items despite their halo-row re-reads, which
-  // then hit L2/MALL).
-  const int64_t strips = (blk_.ny + dev::kSW - 1) / dev::kSW;
-  int ti = 8;  // sweep at 8192² (order × ti × waves): 8 rows, chunk-major, 4096 waves best
-  if (const char* e = std::getenv("PE_TI")) ti = std::max(1, std::atoi(e));
+  // Work decomposition: wave strips (128 columns classic, 124 output
+  // columns single-sweep) × `ti`-row chunks, dealt round-robin (chunk-major)
+  // to a persistent grid of ~16 waves per CU, so the waves running at any
+  // moment cover a compact window of rows (measured: long per-wave row
+  // ranges spread over the whole array run 25 % slower than 8-16-row items
+  // despite their halo-row re-reads, which then hit L2/MALL).
   k.ti = ti;
   k.nstrips = int(strips);
-  k.nitems = int(strips * ((blk_.nx + ti - 1) / ti));
+  k.nitems = int(strips * ((nx + ti - 1) / ti));
   k.order = 0;
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
   int wave_cap = 256 * 16;
@@ -114,7 +157,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   const int per = (k.nitems + wave_cap - 1) / wave_cap;
   const int waves = (k.nitems + per - 1) / per;
   k.nblocks = std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
-  const int64_t npart = std::max<int64_t>(3 * int64_t(k.nblocks), 3 * 4096);
+  const int64_t npart = 8 * std::max<int64_t>(int64_t(k.nblocks), 4096);
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * npart));
   k.partial = partial_;
   k.ih1sq = 1.0 / k.h1sq;
@@ -123,11 +166,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.D_out = (k.inv_eps + k.inv_eps) / k.h1sq + (k.inv_eps + k.inv_eps) / k.h2sq;
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
-  build_tables();
+  build_tables(rows_hi, cols_hi);
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
-  const double pts = double(blk_.nx) * double(blk_.ny);
-  const double t_iter = pts * 64.0 / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
+  const double pts = double(nx) * double(ny);
+  const double t_iter = pts * (fused_ ? 48.0 : 64.0) / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
   int c = int(0.5e-3 / t_iter);
   c = std::max(8, std::min(128, c));
   c += c & 1;
@@ -152,12 +195,12 @@ DeviceSolver::~DeviceSolver() {
 
 KParams& DeviceSolver::params() { return *kp_; }
 
-void DeviceSolver::build_tables() {
-  const std::vector<double> t = chord_tables(prob_, blk_);
+void DeviceSolver::build_tables(int64_t rows_hi, int64_t cols_hi) {
+  const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi);
   PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
   const double* col = t.data();
-  const double* row = t.data() + (blk_.nx + 4) * 4;
-  const std::vector<int> rc = row_classes(col, row, blk_.nx, blk_.ny);
+  const double* row = t.data() + (rows_hi + 2) * 4;
+  const std::vector<int> rc = row_classes(col, row, rows_hi, cols_hi);
   PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
 }
 
@@ -174,14 +217,42 @@ std::vector<Exchange> DeviceSolver::halo_plan() const {
   return ex;
 }
 
+std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
+  if (!fused_) return {HaloPhase{halo_plan(), false}};
+  const KParams& k = *kp_;
+  std::vector<HaloPhase> ph(2);
+  // Phase 0: y strips (4 values per owned row: r and p of two columns).
+  const int64_t c = 4 * blk_.nx;
+  if (blk_.has(DOWN)) ph[0].ex.push_back(Exchange{DOWN, blk_.nbr[DOWN], k.send_dn, const_cast<double*>(k.recv_dn), c});
+  if (blk_.has(UP)) ph[0].ex.push_back(Exchange{UP, blk_.nbr[UP], k.send_up, const_cast<double*>(k.recv_up), c});
+  ph[0].unpack = blk_.has(DOWN) || blk_.has(UP);
+  // Phase 1: two full interleaved (r, p) rows per side, halo columns included
+  // (so the corners arrive from the diagonal rank through the x neighbour).
+  double* x = k.x[buf];
+  const int64_t n = 2 * k.pitch;
+  if (blk_.has(LEFT)) ph[1].ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], x + 1 * k.pitch - 1, x - 1 * k.pitch - 1, n});
+  if (blk_.has(RIGHT))
+    ph[1].ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], x + (blk_.nx - 1) * k.pitch - 1,
+                                x + (blk_.nx + 1) * k.pitch - 1, n});
+  return ph;
+}
+
+void DeviceSolver::enqueue_exchange(int buf) {
+  for (const HaloPhase& ph : halo_phases(buf)) {
+    comm_->exchange(ph.ex, stream_);
+    if (ph.unpack) dev::launch_unpack(*kp_, buf, stream_);
+  }
+}
+
 double* DeviceSolver::red_F_dev() { return st_->red_F; }
 double* DeviceSolver::red_G_dev() { return st_->red_G; }
+double* DeviceSolver::fs_dev(int par) { return st_->fs[par]; }
 double* DeviceSolver::err_dev() { return st_->err; }
 
 void DeviceSolver::enqueue_init() {
-  const int64_t A = blk_.alloc;
-  PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * A * 4, stream_));
-  PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * std::max<int64_t>(1, blk_.nx) * 4, stream_));
+  const int64_t n = fused_ ? 2 * xsize_ + wsize_ : 4 * blk_.alloc;
+  PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * n, stream_));
+  PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * hsize_ * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
   dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
   PE_HIP_CHECK(hipGetLastError());
@@ -189,9 +260,18 @@ void DeviceSolver::enqueue_init() {
 
 void DeviceSolver::enqueue_F(int par) { dev::launch_F(*kp_, par, opt_.variant, stream_); }
 void DeviceSolver::enqueue_G(int par) { dev::launch_G(*kp_, par, opt_.variant, stream_); }
+void DeviceSolver::enqueue_S(int par) { dev::launch_S(*kp_, par, stream_); }
+void DeviceSolver::enqueue_pack(int buf) { dev::launch_pack(*kp_, buf, stream_); }
+void DeviceSolver::enqueue_unpack(int buf) { dev::launch_unpack(*kp_, buf, stream_); }
 void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 
 void DeviceSolver::enqueue_iteration(int par) {
+  if (fused_) {
+    dev::launch_S(*kp_, par, stream_);
+    enqueue_exchange(par);
+    comm_->allreduce_sum(st_->fs[par], 7, stream_);
+    return;
+  }
   dev::launch_F(*kp_, par, opt_.variant, stream_);
   comm_->allreduce_sum(st_->red_F, 2, stream_);
   dev::launch_G(*kp_, par, opt_.variant, stream_);
@@ -234,6 +314,16 @@ void DeviceSolver::synchronize() { PE_HIP_CHECK(hipStreamSynchronize(stream_)); 
 
 void DeviceSolver::reset() {
   enqueue_init();
+  if (fused_) {
+    // r⁰ (and p = 0) in x[0] → halos → sweep S_0 (z₀, A z₀ and their sums,
+    // no iteration counted) into x[1]; iteration 1 then reads x[1] (par 0).
+    dev::launch_pack(*kp_, 0, stream_);
+    enqueue_exchange(0);
+    dev::launch_S(*kp_, 1, stream_);
+    enqueue_exchange(1);
+    comm_->allreduce_sum(st_->fs[1], 7, stream_);
+    return;
+  }
   comm_->exchange(halo_plan(), stream_);
   comm_->allreduce_sum(st_->red_G, 1, stream_);
 }
@@ -281,7 +371,23 @@ SolveResult DeviceSolver::solve() {
     int64_t k = 0;
     DevState hs;
     for (;;) {
-      for (int it = 0; it < chunk_; ++it, ++k) {
+      for (int it = 0; it < chunk_ && fused_; ++it, ++k) {
+        const int par = int(k & 1);
+        PE_HIP_CHECK(hipEventRecord(ev[0], stream_));
+        dev::launch_S(*kp_, par, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[1], stream_));
+        enqueue_exchange(par);
+        PE_HIP_CHECK(hipEventRecord(ev[2], stream_));
+        comm_->allreduce_sum(st_->fs[par], 7, stream_);
+        PE_HIP_CHECK(hipEventRecord(ev[3], stream_));
+        PE_HIP_CHECK(hipEventSynchronize(ev[3]));
+        float t[3];
+        for (int q = 0; q < 3; ++q) PE_HIP_CHECK(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
+        res.t.gpu += t[0] * 1e-3;
+        res.t.halo += t[1] * 1e-3;
+        res.t.reduce += t[2] * 1e-3;
+      }
+      for (int it = 0; it < chunk_ && !fused_; ++it, ++k) {
         const int par = int(k & 1);
         PE_HIP_CHECK(hipEventRecord(ev[0], stream_));
         dev::launch_F(*kp_, par, opt_.variant, stream_);
@@ -367,18 +473,30 @@ SolveResult DeviceSolver::solve() {
 void DeviceSolver::copy_w(double* host, bool owned_only) {
   const KParams& k = *kp_;
   if (owned_only) {
-    PE_HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * blk_.ny, k.w + k.pitch + 1, sizeof(double) * k.pitch,
+    PE_HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * blk_.ny, k.w + k.wpitch + 1, sizeof(double) * k.wpitch,
                                   sizeof(double) * blk_.ny, blk_.nx, hipMemcpyDeviceToHost, stream_));
   } else {
-    PE_HIP_CHECK(hipMemcpyAsync(host, k.w, sizeof(double) * blk_.rows * k.pitch, hipMemcpyDeviceToHost, stream_));
+    PE_HIP_CHECK(hipMemcpyAsync(host, k.w, sizeof(double) * blk_.rows * k.wpitch, hipMemcpyDeviceToHost, stream_));
   }
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
+int64_t DeviceSolver::field_rows() const { return fused_ ? blk_.nx + 4 : blk_.rows; }
+int64_t DeviceSolver::field_cols() const { return fused_ ? plane_ : blk_.pitch; }
+
 void DeviceSolver::copy_field(int which, double* host) {
   const KParams& k = *kp_;
-  const double* src = which == 0 ? k.r : which == 1 ? k.w : which == 2 ? k.p[0] : k.p[1];
-  PE_HIP_CHECK(hipMemcpyAsync(host, src, sizeof(double) * blk_.rows * k.pitch, hipMemcpyDeviceToHost, stream_));
+  if (fused_) {
+    // rows -1..nx+2 of one plane, columns -1.. (plane width)
+    const double* base = which == 0 ? k.x[0] : which == 1 ? k.w : which == 2 ? k.x[0] + k.poff
+                         : which == 3 ? k.x[1] + k.poff : k.x[1];
+    const int64_t stride = which == 1 ? k.wpitch : k.pitch;
+    PE_HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * plane_, base - stride - 1, sizeof(double) * stride,
+                                  sizeof(double) * plane_, blk_.nx + 4, hipMemcpyDeviceToHost, stream_));
+  } else {
+    const double* src = which == 0 ? k.r : which == 1 ? k.w : which == 2 ? k.p[0] : k.p[1];
+    PE_HIP_CHECK(hipMemcpyAsync(host, src, sizeof(double) * blk_.rows * k.pitch, hipMemcpyDeviceToHost, stream_));
+  }
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
@@ -395,21 +513,22 @@ SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, con
     blks.push_back(decompose(P.M, P.N, pg, r));
     s.push_back(std::make_unique<DeviceSolver>(P, blks.back(), nullptr, opt));
   }
-  std::vector<std::vector<Exchange>> plan(ranks);
-  for (int r = 0; r < ranks; ++r) plan[r] = s[r]->halo_plan();
+  const bool fused = s[0]->fused();
   std::vector<hipEvent_t> ev(ranks);
   for (auto& e : ev) PE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  // Device pointer tables for the cross-rank reduction kernel.
-  std::vector<double*> hp(3 * ranks);
+  // Device pointer tables for the cross-rank reduction kernel:
+  // [red_F | red_G | err | fs0 | fs1] × ranks.
+  std::vector<double*> hp(5 * ranks);
   for (int r = 0; r < ranks; ++r) {
     hp[r] = s[r]->red_F_dev();
     hp[ranks + r] = s[r]->red_G_dev();
     hp[2 * ranks + r] = s[r]->err_dev();
+    hp[3 * ranks + r] = s[r]->fs_dev(0);
+    hp[4 * ranks + r] = s[r]->fs_dev(1);
   }
   double** dp = nullptr;
-  PE_HIP_CHECK(hipMalloc(&dp, sizeof(double*) * 3 * ranks));
-  PE_HIP_CHECK(hipMemcpy(dp, hp.data(), sizeof(double*) * 3 * ranks, hipMemcpyHostToDevice));
-  double* err1[64];
+  PE_HIP_CHECK(hipMalloc(&dp, sizeof(double*) * 5 * ranks));
+  PE_HIP_CHECK(hipMemcpy(dp, hp.data(), sizeof(double*) * 5 * ranks, hipMemcpyHostToDevice));
   hipStream_t s0 = s[0]->stream();
 
   auto join_all = [&]() {
@@ -425,25 +544,39 @@ SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, con
     dev::launch_group_reduce(table, ranks, n, is_max, s0);
     fork_all();
   };
-  auto exchange = [&]() {
-    for (int r = 0; r < ranks; ++r) PE_HIP_CHECK(hipEventRecord(ev[r], s[r]->stream()));
-    for (int r = 0; r < ranks; ++r)
-      for (const auto& e : plan[r]) {
-        const auto& peer = plan[e.peer];
-        const Exchange* src = nullptr;
-        for (const auto& pe : peer)
-          if (pe.dir == opposite(e.dir)) src = &pe;
-        if (!src || src->count != e.count) throw std::runtime_error("group halo plan mismatch");
-        PE_HIP_CHECK(hipStreamWaitEvent(s[r]->stream(), ev[e.peer], 0));
-        PE_HIP_CHECK(hipMemcpyAsync(e.recv, src->send, sizeof(double) * e.count, hipMemcpyDeviceToDevice,
-                                    s[r]->stream()));
-      }
+  // Same halo phases as under RCCL; the transport is a D2D copy from the
+  // peer's send region once the peer's stream has produced it.
+  auto exchange = [&](int buf) {
+    std::vector<std::vector<DeviceSolver::HaloPhase>> plan(ranks);
+    for (int r = 0; r < ranks; ++r) plan[r] = s[r]->halo_phases(buf);
+    for (size_t ph = 0; ph < plan[0].size(); ++ph) {
+      for (int r = 0; r < ranks; ++r) PE_HIP_CHECK(hipEventRecord(ev[r], s[r]->stream()));
+      for (int r = 0; r < ranks; ++r)
+        for (const auto& e : plan[r][ph].ex) {
+          const Exchange* src = nullptr;
+          for (const auto& pe : plan[e.peer][ph].ex)
+            if (pe.dir == opposite(e.dir)) src = &pe;
+          if (!src || src->count != e.count) throw std::runtime_error("group halo plan mismatch");
+          PE_HIP_CHECK(hipStreamWaitEvent(s[r]->stream(), ev[e.peer], 0));
+          PE_HIP_CHECK(hipMemcpyAsync(e.recv, src->send, sizeof(double) * e.count, hipMemcpyDeviceToDevice,
+                                      s[r]->stream()));
+        }
+      for (int r = 0; r < ranks; ++r)
+        if (plan[r][ph].unpack) s[r]->enqueue_unpack(buf);
+    }
   };
-  (void)err1;
 
   for (int r = 0; r < ranks; ++r) s[r]->enqueue_init();
-  exchange();
-  reduce(dp + ranks, 1, 0);
+  if (fused) {
+    for (int r = 0; r < ranks; ++r) s[r]->enqueue_pack(0);
+    exchange(0);
+    for (int r = 0; r < ranks; ++r) s[r]->enqueue_S(1);
+    exchange(1);
+    reduce(dp + 4 * ranks, 7, 0);
+  } else {
+    exchange(0);
+    reduce(dp + ranks, 1, 0);
+  }
   PE_HIP_CHECK(hipStreamSynchronize(s0));
   SolveResult res;
   res.t.setup = secs(t_start, clk::now());
@@ -455,10 +588,16 @@ SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, con
   for (;;) {
     for (int it = 0; it < chunk; ++it, ++k) {
       const int par = int(k & 1);
+      if (fused) {
+        for (int r = 0; r < ranks; ++r) s[r]->enqueue_S(par);
+        exchange(par);
+        reduce(dp + (3 + par) * ranks, 7, 0);
+        continue;
+      }
       for (int r = 0; r < ranks; ++r) s[r]->enqueue_F(par);
       reduce(dp, 2, 0);
       for (int r = 0; r < ranks; ++r) s[r]->enqueue_G(par);
-      exchange();
+      exchange(0);
       reduce(dp + ranks, 1, 0);
     }
     s[0]->read_state(&hs);

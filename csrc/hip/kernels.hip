@@ -29,237 +29,12 @@
 // the 1-D chord tables.  Dot products end in a deterministic last-workgroup
 // reduction (agent-scope release/acquire ticket; partials summed in block
 // order), so results are bitwise reproducible run to run.
-#include <hip/hip_runtime.h>
-
-#include "kernels.hpp"
-#include "pe/decomp.hpp"
-#include "pe/problem.hpp"
+#include "kcommon.hpp"
 
 namespace pe {
 namespace dev {
 
 namespace {
-
-constexpr int TJ = kTJ;
-constexpr int SW = kSW;
-
-// Read-only table access through the constant address space: uniform
-// addresses lower to s_load (lgkmcnt), so a table read inside the marching
-// loop never waits on the vector-memory prefetch queue (vmcnt).
-template <class T>
-__device__ __forceinline__ T cload(const T* p) {
-  return *(const __attribute__((address_space(4))) T*)((uintptr_t)p);
-}
-
-__device__ __forceinline__ double fcoef(double l, double h, double eps, double inv_eps) {
-  if (fabs(l - h) < 1e-9) return 1.0;
-  if (l < 1e-9) return inv_eps;
-  return (l / h) + (1.0 - l / h) / eps;
-}
-
-// Per-column chord-table values of one node column lj: the vertical-face
-// y-range (sA, eA) and the horizontal-face half-widths of columns lj, lj+1.
-// Kept in registers by the marching kernels (no table loads in the loop).
-struct TV {
-  double sA, eA, hB, hB1;
-};
-__device__ __forceinline__ TV tv_at(const KParams& k, int64_t lj) {
-  const double* t = k.rowT + (lj + 1) * 4;
-  return TV{t[0], t[1], t[2], t[6]};
-}
-
-// a_{q, lj}: vertical face left of node q.  colT is indexed by the
-// wave-uniform row q → scalar loads, which do not drain vector-memory prefetch.
-__device__ __forceinline__ double coefA(const KParams& k, int64_t q, const TV& t) {
-  const double half = cload(k.colT + (q + 1) * 4 + 0);
-  return fcoef(chord_len(half, t.sA, t.eA), k.h2, k.eps, k.inv_eps);
-}
-// b_{q, ·}: horizontal face below the node, chord half-width `half`.
-__device__ __forceinline__ double coefB(const KParams& k, int64_t q, double half) {
-  const double sB = cload(k.colT + (q + 1) * 4 + 1);
-  const double eB = cload(k.colT + (q + 1) * 4 + 2);
-  return fcoef(chord_len(half, sB, eB), k.h1, k.eps, k.inv_eps);
-}
-
-// Coefficients of node (q, lj): a(q), a(q+1), b(q, lj), b(q, lj+1), and the
-// Jacobi diagonal (EXACT: D, used as r / D; fast: 1/D, used as r * dinv).
-struct CS {
-  double a0, a1, b0, b1, d;
-};
-
-template <bool EXACT>
-__device__ __forceinline__ CS cset(const KParams& k, const int* rc, int64_t q, int64_t lj, const TV& t) {
-  CS c;
-  const int in_lo = cload(rc), in_hi = cload(rc + 1), out_lo = cload(rc + 2), out_hi = cload(rc + 3);
-  if (lj >= in_lo && lj <= in_hi) {  // interior: every face fully inside D
-    c.a0 = c.a1 = c.b0 = c.b1 = 1.0;
-    c.d = EXACT ? k.D_in : k.dinv_in;
-  } else if (lj < out_lo || lj > out_hi) {  // exterior: every face fully outside D
-    c.a0 = c.a1 = c.b0 = c.b1 = k.inv_eps;
-    c.d = EXACT ? k.D_out : k.dinv_out;
-  } else {  // boundary band: evaluate the face lengths
-    c.a0 = coefA(k, q, t);
-    c.a1 = coefA(k, q + 1, t);
-    c.b0 = coefB(k, q, t.hB);
-    c.b1 = coefB(k, q, t.hB1);
-    // D = (a_{i+1} + a_i)/h1² + (b_{j+1} + b_j)/h2²  (reference mat_D, same order)
-    if constexpr (EXACT) c.d = (c.a1 + c.a0) / k.h1sq + (c.b1 + c.b0) / k.h2sq;
-    else c.d = 1.0 / ((c.a1 + c.a0) * k.ih1sq + (c.b1 + c.b0) * k.ih2sq);
-  }
-  return c;
-}
-template <bool EXACT>
-__device__ __forceinline__ CS cset_mem(const KParams& k, int64_t q, int64_t lj) {
-  return cset<EXACT>(k, k.rowcls + (q + 1) * 4, q, lj, tv_at(k, lj));
-}
-
-template <bool EXACT>
-__device__ __forceinline__ double zval(const CS& c, double r) {
-  if constexpr (EXACT) return (c.d != 0.0) ? r / c.d : 0.0;
-  else return r * c.d;
-}
-
-template <bool EXACT>
-__device__ __forceinline__ double stencil(const KParams& k, const CS& c, double pm, double p0, double pn, double pl,
-                                          double pr) {
-  if constexpr (EXACT) {
-    // Reference apply_A (poisson_mpi_cuda2.cu:526-535), same expression tree.
-    const double Ax = k.nih1 * (c.a1 * (pn - p0) / k.h1 - c.a0 * (p0 - pm) / k.h1);
-    const double Ay = k.nih2 * (c.b1 * (pr - p0) / k.h2 - c.b0 * (p0 - pl) / k.h2);
-    return Ax + Ay;
-  } else {
-    return (c.a0 * (p0 - pm) - c.a1 * (pn - p0)) * k.ih1sq + (c.b0 * (p0 - pl) - c.b1 * (pr - p0)) * k.ih2sq;
-  }
-}
-
-__device__ __forceinline__ bool row_valid(const KParams& k, int64_t q) {
-  return (q >= 1 && q <= k.nx) || (q == 0 && k.has[LEFT]) || (q == k.nx + 1 && k.has[RIGHT]);
-}
-// Is local node (q, lj) a value this rank computes (owned, or a halo node
-// whose neighbour exists)?  Global-boundary halos and halo corners are not.
-__device__ __forceinline__ bool valid_node(const KParams& k, int64_t q, int64_t lj) {
-  const bool rin = q >= 1 && q <= k.nx;
-  const bool cin = lj >= 1 && lj <= k.ny;
-  const bool ch = (lj == 0 && k.has[DOWN]) || (lj == k.ny + 1 && k.has[UP]);
-  return (rin && (cin || ch)) || (row_valid(k, q) && !rin && cin);
-}
-
-__device__ __forceinline__ double load_r(const KParams& k, int64_t q, int64_t lj) {
-  if (lj == 0) return k.recv_dn[q - 1];
-  if (lj == k.ny + 1) return k.recv_up[q - 1];
-  return k.r[q * k.pitch + lj];
-}
-
-// ---- wave-level helpers -------------------------------------------------
-__device__ __forceinline__ double dpp_shr1(double v) {  // lane l ← lane l-1 (lane 0 ← 0)
-  const long long x = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(x), 0x138, 0xF, 0xF, true);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), 0x138, 0xF, 0xF, true);
-  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
-__device__ __forceinline__ double dpp_shl1(double v) {  // lane l ← lane l+1 (lane 63 ← 0)
-  const long long x = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(x), 0x130, 0xF, 0xF, true);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), 0x130, 0xF, 0xF, true);
-  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
-__device__ __forceinline__ double readlane(double v, int l) {
-  const long long x = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_readlane(int(x), l);
-  const int hi = __builtin_amdgcn_readlane(int(x >> 32), l);
-  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
-
-// Deterministic block reduction of N sums (or maxima) → thread 0.
-template <int N, bool MAX>
-__device__ __forceinline__ void block_reduce(double (&v)[N], double* sm) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1)
-#pragma unroll
-    for (int n = 0; n < N; ++n) {
-      const double t = __shfl_xor(v[n], o, 64);
-      v[n] = MAX ? fmax(v[n], t) : v[n] + t;
-    }
-  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-  if (lane == 0)
-#pragma unroll
-    for (int n = 0; n < N; ++n) sm[n * 4 + wid] = v[n];
-  __syncthreads();
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int n = 0; n < N; ++n)
-      v[n] = MAX ? fmax(fmax(sm[n * 4], sm[n * 4 + 1]), fmax(sm[n * 4 + 2], sm[n * 4 + 3]))
-                 : ((sm[n * 4] + sm[n * 4 + 1]) + sm[n * 4 + 2]) + sm[n * 4 + 3];
-}
-
-// Publish this block's partials and take a ticket; true in the block that
-// arrives last (all partials visible to it).  Protocol: producer store →
-// vmcnt(0) → agent release → vmcnt(0) → relaxed agent fetch_add; the last
-// arriver does an agent acquire before reading (cdna_hip_programming §6 G16).
-__device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, int* sflag) {
-  if (threadIdx.x == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int last = (t == nblocks - 1);
-    if (last) {
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    *sflag = last;
-  }
-  __syncthreads();
-  return *sflag != 0;
-}
-
-// Sum N-tuples of partials [nblocks][N] in block order (deterministic).
-template <int N>
-__device__ __forceinline__ void reduce_partials(const double* partial, unsigned nblocks, double (&v)[N], double* sm) {
-#pragma unroll
-  for (int n = 0; n < N; ++n) v[n] = 0.0;
-  for (unsigned m = threadIdx.x; m < nblocks; m += TJ)
-#pragma unroll
-    for (int n = 0; n < N; ++n) v[n] += partial[size_t(m) * N + n];
-  block_reduce<N, false>(v, sm);
-}
-
-// One p_k value at a single node (strip-edge columns, prologue only).
-template <bool EXACT>
-__device__ __forceinline__ double p_point(const KParams& k, int64_t q, int64_t lj, double beta, const double* pold) {
-  return zval<EXACT>(cset_mem<EXACT>(k, q, lj), load_r(k, q, lj)) + beta * pold[q * k.pitch + lj];
-}
-
-// Unconditional 16-byte load (address already clamped in range): a
-// predicated load would make hipcc branch around it and drain vmcnt(0),
-// which serialises the row prefetch (measured in the .s).
-__device__ __forceinline__ double2 ld2(const double* p) { return *reinterpret_cast<const double2*>(p); }
-
-// Row class (interior interval / exterior hull) of one row, in SGPRs.
-struct RowCls {
-  int in_lo, in_hi, out_lo, out_hi;
-};
-__device__ __forceinline__ RowCls rcl_read(const int4& v, int l) {
-  return RowCls{__builtin_amdgcn_readlane(v.x, l), __builtin_amdgcn_readlane(v.y, l),
-                __builtin_amdgcn_readlane(v.z, l), __builtin_amdgcn_readlane(v.w, l)};
-}
-// Does columns [jlo, jhi] of this row contain a boundary-band node?  (scalar)
-__device__ __forceinline__ bool has_gen(const RowCls& c, int64_t jlo, int64_t jhi) {
-  const int64_t lo = max(jlo, int64_t(c.out_lo)), hi = min(jhi, int64_t(c.out_hi));
-  if (lo > hi) return false;
-  if (c.in_lo > c.in_hi) return true;
-  return lo < c.in_lo || hi > c.in_hi;
-}
-// Coefficients of a node in a row without boundary-band nodes in this strip.
-template <bool EXACT>
-__device__ __forceinline__ CS cset_fast(const KParams& k, const RowCls& c, int64_t lj) {
-  const bool in = lj >= c.in_lo && lj <= c.in_hi;
-  const double f = in ? 1.0 : k.inv_eps;
-  CS cs;
-  cs.a0 = cs.a1 = cs.b0 = cs.b1 = f;
-  cs.d = EXACT ? (in ? k.D_in : k.D_out) : (in ? k.dinv_in : k.dinv_out);
-  return cs;
-}
 
 constexpr int SEG = 60;  // rows per segment: rows seg-1 .. seg+SEG live one per lane
 
@@ -631,11 +406,13 @@ __global__ __launch_bounds__(TJ) void kInit(KParams k, int init_random, unsigned
                                        random_w0(gi, gj - 1, k.M, k.N, seed, amp),
                                        random_w0(gi, gj + 1, k.M, k.N, seed, amp));
       rr = rr - Aw;
-      k.w[at] = w0;
+      k.w[li * k.wpitch + lj] = w0;
     }
     k.r[at] = rr;
-    if (lj == 1 && k.has[DOWN]) k.send_dn[li - 1] = rr;
-    if (lj == k.ny && k.has[UP]) k.send_up[li - 1] = rr;
+    if (!k.fused) {  // fused layout: launch_pack gathers the y strips
+      if (lj == 1 && k.has[DOWN]) k.send_dn[li - 1] = rr;
+      if (lj == k.ny && k.has[UP]) k.send_up[li - 1] = rr;
+    }
     szr += zval<EXACT>(c, rr) * rr;
   }
   double v[1] = {szr};
@@ -665,7 +442,7 @@ __global__ __launch_bounds__(TJ) void kError(KParams k) {
   for (int64_t idx = int64_t(blockIdx.x) * TJ + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * TJ) {
     const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
     const double x = k.A1 + (k.gi0 + li) * k.h1, y = k.A2 + (k.gj0 + lj) * k.h2;
-    const double wv = k.w[li * k.pitch + lj];
+    const double wv = k.w[li * k.wpitch + lj];
     if (in_ellipse(x, y, k.cx, k.cy)) {
       const double e = wv - k.u_scale * (1.0 - k.cx * x * x - k.cy * y * y);
       e2 += e * e;

@@ -37,6 +37,12 @@ struct DevState {
   int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap
   unsigned ticket[4];
   unsigned pad[4];
+  // Single-sweep (fused) PCG: the 7 local/global sums of sweep k live in
+  // fs[k & 1] = {(r,z), (z,Az), (z,s), (p,s), (z,z), (z,p), (p,p)}, unweighted.
+  double fs[2][8];
+  double gprev;      // (r,z) consumed by the previous sweep (β denominator), h-weighted
+  int started;       // 0 until sweep S_0 (z_0, A z_0 and their dots) has run
+  int pad2[3];
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -70,18 +76,35 @@ struct KParams {
   double D_in, D_out;            // exact-arithmetic diagonal in the interior / exterior class
   double dinv_in, dinv_out;      // fast-arithmetic 1/D in the interior / exterior class
   double ih1sq, ih2sq;           // 1/h1², 1/h2² (fast arithmetic)
+  // Single-sweep layout (fused = 1): x[b] points at local (0,0) of the r-plane
+  // of buffer b; its p-plane is at +poff; both planes share row stride
+  // `pitch` (rows interleave r and p so the 2 halo rows of both fields are one
+  // contiguous message).  w has its own row stride `wpitch`.
+  int fused;
+  int64_t wpitch;
+  int64_t poff;
+  double* x[2];
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
 constexpr int kWPB = 4;          // waves per block
 constexpr int kSW = 128;         // columns per wave strip (2 per lane, 16-B accesses)
 constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live one per lane)
+constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
+constexpr int kFTImax = 60;      // fused sweep: max rows per work item (rows ib-2..ie+2 one per lane)
 
 void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
                  hipStream_t s);
 void launch_F(const KParams& k, int par, int variant, hipStream_t s);
 void launch_G(const KParams& k, int par, int variant, hipStream_t s);
 void launch_error(const KParams& k, hipStream_t s);
+// Single-sweep PCG (fused.hip): one kernel + one 7-scalar reduction per iteration.
+void launch_S(const KParams& k, int par, hipStream_t s);
+// y-direction halo strips of buffer b: pack columns {1,2} / {ny-1,ny} of r,p
+// into send_dn / send_up ([nx][4]); unpack recv_dn / recv_up into columns
+// {-1,0} / {ny+1,ny+2}.
+void launch_pack(const KParams& k, int b, hipStream_t s);
+void launch_unpack(const KParams& k, int b, hipStream_t s);
 // Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);
 // Debug/test ops (single-shot, no convergence logic).

@@ -98,25 +98,44 @@ class DeviceSolver {
   void enqueue_init();
   void enqueue_F(int par);
   void enqueue_G(int par);
+  void enqueue_S(int par);      // single-sweep iteration kernel
+  void enqueue_pack(int buf);   // single-sweep: y strips of buffer `buf` → send buffers
+  void enqueue_unpack(int buf); // single-sweep: recv buffers → y halo columns of `buf`
   void enqueue_error();
   double* red_F_dev();
   double* red_G_dev();
+  double* fs_dev(int par);
   double* err_dev();
-  std::vector<Exchange> halo_plan() const;  // device pointers of this rank's strips
+  // Halo exchange as ordered phases; after a phase with `unpack` set the
+  // received y strips are scattered into buffer `buf` (single-sweep layout:
+  // y phase, unpack, then x phase whose rows carry the corners).  The
+  // classic path has one phase (r: x rows + y strips).
+  struct HaloPhase {
+    std::vector<Exchange> ex;
+    bool unpack = false;
+  };
+  std::vector<HaloPhase> halo_phases(int buf) const;
+  std::vector<Exchange> halo_plan() const;  // classic: the single phase
+  bool fused() const { return fused_; }
   hipStream_t stream() const { return stream_; }
 
   // State / data access.
   void read_state(dev::DevState* out);
   void copy_w(double* host, bool owned_only = true);  // nx × ny row-major
-  void copy_field(int which, double* host);            // 0 r, 1 w, 2 p0, 3 p1: full (rows × pitch)
+  // 0 r, 1 w, 2 p0, 3 p1 (single-sweep: 0 r of x[0], 2 p of x[0], 3 p of
+  // x[1], 4 r of x[1]) as field_rows() × field_cols(), local (-h, -h) first.
+  void copy_field(int which, double* host);
+  int64_t field_rows() const;
+  int64_t field_cols() const;
   const Block& block() const { return blk_; }
   const Problem& problem() const { return prob_; }
   int chunk() const { return chunk_; }
   dev::KParams& params();
 
  private:
-  void build_tables();
+  void build_tables(int64_t rows_hi, int64_t cols_hi);
   void enqueue_iteration(int par);
+  void enqueue_exchange(int buf);
   void enqueue_chunk(int iters);
   bool graph_ready(int iters);
 
@@ -126,10 +145,13 @@ class DeviceSolver {
   std::unique_ptr<DeviceComm> self_;
   SolveOptions opt_;
   hipStream_t stream_ = nullptr;
-  double* fields_ = nullptr;  // r, w, p0, p1 (alloc each)
+  bool fused_ = false;
+  double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w
+  int64_t xsize_ = 0, wsize_ = 0, plane_ = 0;
   double* tables_ = nullptr;
   int* rowcls_ = nullptr;
-  double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each)
+  double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each; ×4 single-sweep)
+  int64_t hsize_ = 0;
   double* partial_ = nullptr;
   dev::DevState* st_ = nullptr;
   dev::DevState* hst_ = nullptr;  // pinned, 2 slots
@@ -142,14 +164,17 @@ class DeviceSolver {
 };
 
 // Per-row coefficient classes from the chord tables (see row_classes.cpp):
-// for each local row q ∈ [-1, nx+1], {in_lo, in_hi, out_lo, out_hi} such that
-// every face coefficient of node (q, lj) is exactly 1 for lj ∈ [in_lo, in_hi]
-// and exactly 1/eps for lj ∉ [out_lo, out_hi].  Conservative: anything else is
-// evaluated exactly.
-std::vector<int> row_classes(const double* colT, const double* rowT, int64_t nx, int64_t ny);
-// Chord tables of a block: (nx+4)×4 column entries {halfA, sB, eB, x} then
-// (ny+4)×4 row entries {sA, eA, halfB, y}, indexed by local index + 1.
-std::vector<double> chord_tables(const Problem& P, const Block& blk);
+// for each local row q ∈ [-1, rows_hi-1], {in_lo, in_hi, out_lo, out_hi} such
+// that every face coefficient of node (q, lj) is exactly 1 for lj ∈ [in_lo,
+// in_hi] and exactly 1/eps for lj ∉ [out_lo, out_hi], lj ∈ [-1, cols_hi].
+// Conservative: anything else is evaluated exactly.  (rows_hi+2) × 4 ints.
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi);
+// Chord tables of a block: (rows_hi+2)×4 column entries {halfA, sB, eB, x}
+// for li ∈ [-1, rows_hi], then (cols_hi+2)×4 row entries {sA, eA, halfB, y}
+// for lj ∈ [-1, cols_hi]; indexed by local index + 1.  The classic kernels
+// use rows_hi = nx+2, cols_hi = ny+2; the single-sweep kernel reaches two
+// halo nodes further and past ny into strip padding.
+std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi);
 // Host mirror of the kernels' coefficient path for local (li, lj) ∈
 // [0, nx+1] × [0, ny+1]: a(li, lj), b(li, lj) and the class (0 interior,
 // 1 exterior, 2 boundary band).  Row-major (nx+2) × (ny+2).

@@ -46,7 +46,11 @@ struct SolveOptions {
   bool use_graph = true;     // capture a chunk of iterations into a hipGraph
   bool timing = false;       // per-phase hipEvent timing (adds host sync)
   bool check_tol = true;     // false: never stop on ‖Δw‖ (fixed-iteration benchmarking)
-  int variant = 0;           // device kernel variant (0 = default fused marching)
+  int variant = 0;           // device arithmetic: 0 fast (1/h², 1/D), 1 reference expression trees
+  // Device algorithm: 0 auto (single-sweep when the variant / decomposition
+  // allow it), 1 classic two-kernel iteration (reference recurrence, 2
+  // reductions), 2 single-sweep (fused.hip: 1 kernel, 1 reduction).
+  int algo = 0;
 };
 
 struct SolveResult {

@@ -39,6 +39,8 @@ def build_parser():
     ap.add_argument("--max-iter", type=int, default=-1)
     ap.add_argument("--norm", choices=("weighted", "unweighted"), default="weighted")
     ap.add_argument("--variant", type=int, default=0, help="device arithmetic: 0 fast (default), 1 reference-exact")
+    ap.add_argument("--algo", choices=("auto", "classic", "fused"), default="auto",
+                    help="device iteration: fused single-sweep (1 kernel, 1 reduction) or classic (2 + 2)")
     ap.add_argument("--timing", action="store_true", help="per-phase device event timers")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json", action="store_true")
@@ -58,7 +60,8 @@ def main(argv=None) -> int:
     prob.norm = a.norm
     want_w = bool(a.dump or a.pgm)
     rep = solve(prob, backend=a.backend, ranks=a.ranks, threads=a.threads, decomp=a.decomp, init=a.init,
-                seed=a.seed, return_w=want_w, variant=a.variant, timing=a.timing, graph=not a.no_graph)
+                seed=a.seed, return_w=want_w, variant=a.variant, timing=a.timing, graph=not a.no_graph,
+                algo=a.algo)
     if rep.rank != 0:
         return 0
     if not a.quiet:

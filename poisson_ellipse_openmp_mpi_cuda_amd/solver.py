@@ -65,8 +65,11 @@ class SolveReport:
         return d
 
 
+ALGOS = {"auto": 0, "classic": 1, "fused": 2}
+
+
 def _options(init="zero", seed=1234, threads=1, chunk=0, graph=True, timing=False, check_tol=True, variant=0,
-             keep_history=False, log_every=0):
+             keep_history=False, log_every=0, algo="auto"):
     nat = native()
     o = nat.SolveOptions()
     o.init = nat.Init.Random if init == "random" else nat.Init.Zero
@@ -77,6 +80,7 @@ def _options(init="zero", seed=1234, threads=1, chunk=0, graph=True, timing=Fals
     o.timing = bool(timing)
     o.check_tol = bool(check_tol)
     o.variant = int(variant)
+    o.algo = ALGOS[algo] if isinstance(algo, str) else int(algo)
     o.keep_history = bool(keep_history)
     o.log_every = int(log_every)
     return o
@@ -125,7 +129,8 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
                            r.w[1:-1, 1:-1].cpu().numpy() if return_w else None)
     if backend == "hip-group":
         opt = _options(init, seed, chunk=kw.get("chunk", 0), timing=kw.get("timing", False),
-                       variant=kw.get("variant", 0), check_tol=kw.get("check_tol", True))
+                       variant=kw.get("variant", 0), check_tol=kw.get("check_tol", True),
+                       algo=kw.get("algo", "auto"))
         res, w = nat.device_solve_group(P, ranks, _decomp.mode_enum(decomp), opt, return_w)
         return _report(backend, prob, res, ranks, 1, init, None if w is None else np.asarray(w))
     # distributed backends
@@ -148,7 +153,7 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     else:
         world = _dist.env_rank_world()[1]
     opt = _options(init, seed, chunk=kw.get("chunk", 0), graph=kw.get("graph", True), timing=kw.get("timing", False),
-                   check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0))
+                   check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0), algo=kw.get("algo", "auto"))
     if world == 1:
         rank, comm = 0, None
         nat.set_device(0)

@@ -26,9 +26,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 @pytest.mark.parametrize("M,N,norm", [(40, 40, "weighted"), (40, 40, "unweighted"), (400, 600, "weighted"),
                                       (800, 1200, "weighted"), (2048, 2048, "weighted"), (10, 10, "unweighted")])
-@pytest.mark.parametrize("variant", [0, 1])
-def test_device_golden_iterations(gpu, M, N, norm, variant):
-    rep = solve(EllipseProblem(M, N, norm=norm), backend="hip", variant=variant)
+@pytest.mark.parametrize("variant,algo", [(0, "fused"), (0, "classic"), (1, "classic")])
+def test_device_golden_iterations(gpu, M, N, norm, variant, algo):
+    rep = solve(EllipseProblem(M, N, norm=norm), backend="hip", variant=variant, algo=algo)
     assert rep.converged
     assert rep.iters == GOLDEN_ITERS[(M, N, norm)]
     if (M, N) in GOLDEN_L2 and norm == "weighted":
@@ -39,22 +39,63 @@ def test_device_golden_iterations(gpu, M, N, norm, variant):
 def test_device_solution_matches_cpu_oracle(gpu, M, N):
     prob = EllipseProblem(M, N)
     ref = solve(prob, backend="serial", return_w=True)
-    for variant in (0, 1):
-        rep = solve(prob, backend="hip", return_w=True, variant=variant)
+    for variant, algo in ((0, "fused"), (0, "classic"), (1, "classic")):
+        rep = solve(prob, backend="hip", return_w=True, variant=variant, algo=algo)
         assert rep.iters == ref.iters
         np.testing.assert_allclose(rep.w, ref.w, rtol=0, atol=1e-10)
 
 
 @pytest.mark.parametrize("ranks,decomp", [(2, "aspect"), (3, "aspect"), (4, "aspect"), (6, "aspect"),
                                           (8, "reference"), (5, "aspect")])
-def test_virtual_ranks_match_single(gpu, ranks, decomp):
+@pytest.mark.parametrize("algo", ["fused", "classic"])
+def test_virtual_ranks_match_single(gpu, ranks, decomp, algo):
     prob = EllipseProblem(300, 420)
-    one = solve(prob, backend="hip", return_w=True)
-    grp = solve(prob, backend="hip-group", ranks=ranks, decomp=decomp, return_w=True)
+    one = solve(prob, backend="hip", return_w=True, algo=algo)
+    grp = solve(prob, backend="hip-group", ranks=ranks, decomp=decomp, return_w=True, algo=algo)
     assert grp.Px * grp.Py == ranks
     assert abs(grp.iters - one.iters) <= 1
     np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-9)
     assert grp.l2_err == pytest.approx(one.l2_err, rel=1e-6)
+
+
+@pytest.mark.parametrize("M,N,ranks,decomp", [(7, 7, 9, "aspect"), (9, 5, 4, "aspect"), (25, 13, 12, "aspect"),
+                                               (9, 9, 16, "aspect")])
+def test_fused_thin_blocks(gpu, M, N, ranks, decomp):
+    # blocks down to 2 rows / columns (3x3 of 2x2 blocks: every halo node and
+    # corner comes from a neighbour); 8x2 of 1-row blocks falls back to classic
+    prob = EllipseProblem(M, N)
+    one = solve(prob, backend="hip", return_w=True, algo="classic")
+    grp = solve(prob, backend="hip-group", ranks=ranks, decomp=decomp, return_w=True)
+    assert abs(grp.iters - one.iters) <= 1
+    np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("M,N", [(4096, 4096), (8192, 8192)])
+def test_fused_large_golden(gpu, M, N):
+    rep = solve(EllipseProblem(M, N), backend="hip", algo="fused")
+    assert rep.converged and rep.iters == GOLDEN_ITERS[(M, N, "weighted")]
+    assert rep.l2_err == pytest.approx(GOLDEN_L2[(M, N)], rel=5e-3)
+
+
+def test_fused_matches_classic_state(gpu, nat):
+    prob = EllipseProblem(300, 500)
+    blk = D.block(300, 500, 1, 0)
+    out = {}
+    for algo in (1, 2):
+        opt = nat.SolveOptions()
+        opt.algo = algo
+        opt.check_tol = False
+        s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
+        assert s.fused == (algo == 2)
+        s.reset()
+        s.run_iterations(40, False)
+        s.synchronize()
+        out[algo] = (s.state(), s.w())
+    (sc, wc), (sf, wf) = out[1], out[2]
+    assert sc["iter"] == sf["iter"] == 40
+    assert sf["alpha"] == pytest.approx(sc["alpha"], rel=1e-9)
+    assert sf["beta"] == pytest.approx(sc["beta"], rel=1e-9)
+    np.testing.assert_allclose(wf, wc, rtol=0, atol=1e-12 * np.abs(wc).max())
 
 
 def test_virtual_ranks_golden_grid(gpu):
