@@ -79,6 +79,7 @@ int main(int argc, char** argv) {
   opt.chunk = int(args.geti("chunk", 0));
   opt.use_graph = !args.flag("no-graph");
   opt.timing = args.flag("timing");
+  opt.check_tol = !args.flag("no-tol");  // fixed-iteration runs (with --max-iter) for profiling
   const DecompMode mode = args.get("decomp", "aspect") == "reference" ? DecompMode::Reference : DecompMode::Aspect;
 
   const int rank = env_int("PE_RANK", "RANK", 0);
@@ -92,7 +93,7 @@ int main(int argc, char** argv) {
     return 2;
   }
   set_device(local % ndev);
-  if (rank == 0)
+  if (rank == 0 && !args.flag("quiet"))
     std::cout << "HIP + RCCL 2D run with " << size * vranks << " ranks on " << device_name(local % ndev) << "; M="
               << P.M << ", N=" << P.N << std::endl;
 
@@ -112,10 +113,11 @@ int main(int argc, char** argv) {
     if (args.flag("json")) {
       std::printf("{\"M\": %d, \"N\": %d, \"ranks\": %d, \"Px\": %d, \"Py\": %d, \"iters\": %lld, \"converged\": %s, "
                   "\"t_solver\": %.6f, \"t_iterate\": %.6f, \"t_gpu\": %.6f, \"t_halo\": %.6f, \"t_reduce\": %.6f, "
-                  "\"iters_per_s\": %.3f, \"l2_err\": %.6e, \"max_err\": %.6e, \"max_outside\": %.6e, \"total\": %.6f}\n",
+                  "\"iters_per_s\": %.3f, \"l2_err\": %.6e, \"max_err\": %.6e, \"max_outside\": %.6e, \"total\": %.6f, "
+                  "\"algo\": \"%s\"}\n",
                   P.M, P.N, size * vranks, r.Px, r.Py, (long long)r.iters, r.converged ? "true" : "false", r.t.solver,
                   r.t.iterate, r.t.gpu, r.t.halo, r.t.reduce, r.iters / std::max(1e-12, r.t.iterate), r.l2_err,
-                  r.max_err, r.max_outside, total);
+                  r.max_err, r.max_outside, total, r.algo.c_str());
     } else {
       std::cout << format_result_legacy(P, r, size, "stage4");
       std::printf("   Process grid %dx%d | iters/s ~ %.1f | L2 error in D ~ %.6e | max error in D ~ %.6e\n", r.Px, r.Py,

@@ -156,6 +156,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("Px", &SolveResult::Px)
       .def_readonly("Py", &SolveResult::Py)
       .def_readonly("backend", &SolveResult::backend)
+      .def_readonly("algo", &SolveResult::algo)
       .def_property_readonly("timers", [](const SolveResult& r) { return timers_dict(r.t); });
 
   m.def("format_result_legacy", &format_result_legacy);
@@ -337,6 +338,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
+      .def_property_readonly("fields_address", &DeviceSolver::fields_address)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("blocks", [](DeviceSolver& s) { return dev::grid_blocks(s.params()); })
       .def_property_readonly("block", &DeviceSolver::block);

@@ -33,6 +33,17 @@ using clk = std::chrono::steady_clock;
 double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 }  // namespace
 
+// Field allocation.  PE_MALLOC=1 requests physically contiguous memory
+// (hipDeviceMallocContiguous) — an experiment on the allocation-dependent
+// speed of the streaming sweep.
+static void* field_alloc(size_t bytes) {
+  void* p = nullptr;
+  const char* e = std::getenv("PE_MALLOC");
+  if (e && std::atoi(e) == 1) PE_HIP_CHECK(hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous));
+  else PE_HIP_CHECK(hipMalloc(&p, bytes));
+  return p;
+}
+
 // Can the single-sweep kernel run this block?  It needs the fast arithmetic
 // variant and neighbours at least two nodes deep in every split direction
 // (its halo is two rows / columns deep).
@@ -57,8 +68,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   std::memset(&k, 0, sizeof(KParams));
   const int64_t nx = blk_.nx, ny = blk_.ny;
   int ti = fused_ ? 16 : 8;  // 8192² sweeps: classic 8 rows, single-sweep 16 (4 halo rows per item)
-  if (const char* e = std::getenv("PE_TI")) ti = std::max(1, std::atoi(e));
-  if (fused_) ti = std::min(ti, dev::kFTImax);
+  int ti_env = 0;
+  if (const char* e = std::getenv("PE_TI")) ti_env = std::atoi(e);
+  if (ti_env > 0) ti = ti_env;
 
   int64_t strips = 0, rows_hi = nx + 2, cols_hi = ny + 2;
   if (fused_) {
@@ -67,10 +79,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // r and p planes by row.
     strips = (ny + dev::kFSW - 1) / dev::kFSW;
     plane_ = ((dev::kFSW * strips + 4 + 7) / 8) * 8;
+    if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
     const int64_t rows = nx + 6;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
     wsize_ = ((rows * plane_ + 64 + 31) / 32) * 32;
-    PE_HIP_CHECK(hipMalloc(&fields_, sizeof(double) * (2 * xsize_ + wsize_)));
+    fields_ = static_cast<double*>(field_alloc(sizeof(double) * (2 * xsize_ + wsize_)));
     k.pitch = 2 * plane_;
     k.wpitch = plane_;
     k.poff = plane_;
@@ -147,13 +160,31 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // moment cover a compact window of rows (measured: long per-wave row
   // ranges spread over the whole array run 25 % slower than 8-16-row items
   // despite their halo-row re-reads, which then hit L2/MALL).
+  // Persistent grid: exactly the resident waves (a second partial round of
+  // blocks would run after the first finishes — a tail of up to one item
+  // per wave).
+  int cus = 256;
+  {
+    int dev = 0;
+    PE_HIP_CHECK(hipGetDevice(&dev));
+    PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  int per_cu = fused_ ? dev::resident_blocks_S() : dev::resident_blocks_classic(opt_.variant);
+  if (per_cu <= 0) per_cu = 4;
+  int wave_cap = cus * per_cu * dev::kWPB;
+  if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
+  // PE_TI=-1 (single-sweep): "bands" — one item per resident wave, the rows
+  // split into wave_cap/nstrips bands that the waves of a band march down
+  // together (halo rows re-read once per band, perfect balance).
+  if (fused_ && ti_env < 0) {
+    const int64_t bands = std::max<int64_t>(1, wave_cap / std::max<int64_t>(1, strips));
+    ti = int((nx + bands - 1) / bands);
+  }
   k.ti = ti;
   k.nstrips = int(strips);
   k.nitems = int(strips * ((nx + ti - 1) / ti));
   k.order = 0;
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
-  int wave_cap = 256 * 16;
-  if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
   const int per = (k.nitems + wave_cap - 1) / wave_cap;
   const int waves = (k.nitems + per - 1) / per;
   k.nblocks = std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
@@ -355,6 +386,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
+  res.algo = fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   reset();
@@ -646,6 +678,7 @@ SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, con
   PE_HIP_CHECK(hipFree(dp));
   for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
   res.backend = "hip-group";
+  res.algo = fused ? "fused" : "classic";
   res.Px = pg.Px;
   res.Py = pg.Py;
   res.t.solver = secs(t_start, clk::now());

@@ -34,7 +34,14 @@
 // x-neighbour needs are ONE contiguous message.  Local rows -1..nx+2 and
 // columns -1..ny+2 hold data (halo depth 2); everything a kernel reads past
 // that is zero padding, and non-interior nodes are masked to z = 0.
+#include <cstdlib>
+
 #include "kcommon.hpp"
+
+// The single-sweep formulation does not reproduce the reference rounding
+// anyway: let the compiler contract a*b+c into v_fma_f64.
+#pragma clang fp contract(fast)
+
 
 namespace pe {
 namespace dev {
@@ -45,24 +52,62 @@ constexpr int FSW = kFSW;
 
 __device__ __forceinline__ double2 dd(double a, double b) { return make_double2(a, b); }
 
-// Coefficients of row t for the lane's two columns: select-only when the
-// strip has no boundary-band node in that row, exact face lengths otherwise.
-__device__ __forceinline__ void crow(const KParams& k, const RowCls& rc, bool gen, int t, int c0, const TV& tv0,
-                                     const TV& tv1, CS& x0, CS& x1) {
-  if (!gen) {
-    x0 = cset_fast<false>(k, rc, c0);
-    x1 = cset_fast<false>(k, rc, c0 + 1);
+// Per-wave LDS copy of the strip's row-table entries (boundary-band rows
+// only read them; LDS reads are counted by lgkmcnt, so they never drain
+// the vector-memory prefetch queue).
+struct WaveTV {
+  double sA[128], eA[128], hB[130];
+};
+
+// Row descriptor carried through the 3-row pipeline: lane-resident interior
+// flags of the lane's two columns, and whether the strip has a boundary-band
+// node in this row (uniform).
+struct RowI {
+  bool in0, in1, gen;
+  int t;  // local row
+};
+constexpr int FSEG = 60;  // rows per row-class segment: rows s0-2 .. s0+61 live one per lane
+
+// Select-only coefficients of a band-free row: f = 1 inside, 1/eps outside;
+// d = 1/D accordingly.
+__device__ __forceinline__ double fsel(const KParams& k, bool in) { return in ? 1.0 : k.inv_eps; }
+__device__ __forceinline__ double dsel(const KParams& k, bool in) { return in ? k.dinv_in : k.dinv_out; }
+__device__ __forceinline__ double lapf(const KParams& k, double f, double pm, double p0, double pn, double pl,
+                                       double pr) {
+  return f * (((p0 - pm) - (pn - p0)) * k.ih1sq + ((p0 - pl) - (pr - p0)) * k.ih2sq);
+}
+__device__ __forceinline__ CS cs_gen(const KParams& k, const RowCls& rc, int q, int lj, const WaveTV& tv, int jl) {
+  const TV t{tv.sA[jl], tv.eA[jl], tv.hB[jl], tv.hB[jl + 1]};
+  return cset_rc(k, rc, q, lj, t);
+}
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+template <bool NT>
+__device__ __forceinline__ void st2(double* p, double2 v) {
+  if constexpr (NT) __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+  else *reinterpret_cast<double2*>(p) = v;
+}
+template <bool NT>
+__device__ __forceinline__ double2 ldw(const double* p) {
+  if constexpr (NT) {
+    const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+    return make_double2(t.x, t.y);
   } else {
-    x0 = cset_rc(k, rc, t, c0, tv0);
-    x1 = cset_rc(k, rc, t, c0 + 1, tv1);
+    return *reinterpret_cast<const double2*>(p);
   }
 }
 
-__global__ __launch_bounds__(TJ) void kS(KParams k, int par) {
+// OCC > 0 caps registers for OCC waves per SIMD (amdgpu_waves_per_eu); PF =
+// rows of loads in flight per wave; NT = non-temporal w and output streams
+// (they are not re-read within the sweep, so they should not evict the halo
+// rows neighbouring items re-read from L2).
+template <int OCC, int PF, bool NT>
+__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   if (st->done) return;
   __shared__ double sm[32];
   __shared__ int sflag;
+  __shared__ WaveTV tvs[kWPB];
 
   // ---- scalars of this sweep from the previous sweep's global sums ----
   const bool first = st->started == 0;
@@ -88,117 +133,185 @@ __global__ __launch_bounds__(TJ) void kS(KParams k, int par) {
     zc = 1.0;
   }
 
-  const double* __restrict__ X = k.x[par ^ 1];
-  double* __restrict__ Y = k.x[par];
-  double* __restrict__ W = k.w;
+  // Row pointers at column -1 (uniform, SGPR) + lane offset (unsigned VGPR).
+  const double* __restrict__ Xm = k.x[par ^ 1] - 1;
+  double* __restrict__ Ym = k.x[par] - 1;
+  double* __restrict__ Wm = k.w - 1;
   const int64_t pitch = k.pitch, poff = k.poff, wp = k.wpitch;
   const int nx = int(k.nx), ny = int(k.ny);
   const int lane = threadIdx.x & 63;
-  const int nw = gridDim.x * kWPB;
   double sg = 0.0, sd = 0.0, se = 0.0, sps = 0.0, szz = 0.0, szp = 0.0, spp = 0.0;
 
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  for (int item = blockIdx.x * kWPB + wid; item < k.nitems; item += nw) {
-    // chunk-major: the waves running at any moment cover a compact window of rows
-    const int s = item % k.nstrips, ch = item / k.nstrips;
+  WaveTV& tvw = tvs[wid];
+  // Item walk.  order 2: the chunks (row bands) are split into 8 contiguous
+  // ranges, one per XCD (blocks are dealt round-robin to the 8 XCDs), so the
+  // halo rows an item shares with the chunk above/below are re-read from the
+  // same L2; orders 0/1: global chunk-major / strip-major.
+  const int nchunks = (nx + k.ti - 1) / k.ti;
+  int it0, istride, ilimit, chunk0;
+  if (k.order == 2) {
+    const int x = blockIdx.x & 7, nbx = (int(gridDim.x) - x + 7) >> 3;
+    const int c_lo = (x * nchunks) >> 3, c_hi = ((x + 1) * nchunks) >> 3;
+    it0 = (int(blockIdx.x) >> 3) * kWPB + wid;
+    istride = nbx * kWPB;
+    ilimit = (c_hi - c_lo) * k.nstrips;
+    chunk0 = c_lo;
+  } else {
+    it0 = blockIdx.x * kWPB + wid;
+    istride = gridDim.x * kWPB;
+    ilimit = k.nitems;
+    chunk0 = 0;
+  }
+  for (int item = it0; item < ilimit; item += istride) {
+    const int s = (k.order == 1) ? item / nchunks : item % k.nstrips;
+    const int ch = chunk0 + ((k.order == 1) ? item % nchunks : item / k.nstrips);
     const int J = -1 + s * FSW;
     const int ib = 1 + ch * k.ti, ie = min(ib + k.ti - 1, nx);
-    const int c0 = J + 2 * lane;  // odd → 16-byte aligned pair (c0, c0+1)
+    const int c0 = J + 2 * lane;               // odd → 16-byte aligned pair (c0, c0+1)
+    const unsigned off = unsigned(c0 + 1);     // element offset from column -1
     const int64_t g0 = k.gj0 + c0;
     const bool lv0 = c0 <= ny + 2 && g0 >= 1 && g0 <= k.N - 1;
     const bool lv1 = c0 + 1 <= ny + 2 && g0 + 1 >= 1 && g0 + 1 <= k.N - 1;
     const bool inner = lane >= 1 && lane <= 62;
     const bool o0 = inner && c0 >= 1 && c0 <= ny;
     const bool o1 = inner && c0 + 1 <= ny;
-    const int jlo = J, jhi = J + 127;
-    const TV tv0 = tv_at(k, c0), tv1 = tv_at(k, c0 + 1);
-    // Row classes, lane t ↔ row ib-2+t.
-    const int4 rcv = lane <= ie - ib + 4 ? *reinterpret_cast<const int4*>(k.rowcls + (ib - 1 + lane) * 4)
-                                         : make_int4(1, 0, 0, -1);
-    auto cls = [&](int t, CS& x0, CS& x1) {
-      const RowCls rc = rcl_read(rcv, t - ib + 2);
-      crow(k, rc, has_gen(rc, jlo, jhi), t, c0, tv0, tv1, x0, x1);
+    const int jl0 = 2 * lane;
+    {  // strip chord entries → LDS (band rows only)
+      const double* t0 = k.rowT + (c0 + 1) * 4;
+      const double4 a = *reinterpret_cast<const double4*>(t0);
+      const double4 b = *reinterpret_cast<const double4*>(t0 + 4);
+      tvw.sA[jl0] = a.x;
+      tvw.eA[jl0] = a.y;
+      tvw.hB[jl0] = a.z;
+      tvw.sA[jl0 + 1] = b.x;
+      tvw.eA[jl0 + 1] = b.y;
+      tvw.hB[jl0 + 1] = b.z;
+      if (lane == 63) tvw.hB[128] = t0[10];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+    // Row classes of a 64-row segment, lane l ↔ row segbase+l; band rows as
+    // a scalar bit mask.  Reloaded every FSEG rows (items may be long).
+    int segbase = 0;
+    int4 rcv;
+    unsigned long long genmask = 0;
+    auto load_seg = [&](int base) {
+      segbase = base;
+      const int nr = ie + 3 - base;
+      rcv = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+      genmask = __ballot(lane < nr && has_gen(RowCls{rcv.x, rcv.y, rcv.z, rcv.w}, J, J + 127));
     };
-    auto rlive = [&](int t) {
-      const int64_t gt = k.gi0 + t;
-      return gt >= 1 && gt <= k.M - 1;
+    load_seg(ib - 2);
+    auto rinfo = [&](int t) {
+      RowI r;
+      r.t = t;
+      const int l = t - segbase;
+      const int lo = __builtin_amdgcn_readlane(rcv.x, l), hi = __builtin_amdgcn_readlane(rcv.y, l);
+      r.in0 = c0 >= lo && c0 <= hi;
+      r.in1 = c0 + 1 >= lo && c0 + 1 <= hi;
+      r.gen = (genmask >> l) & 1ull;
+      return r;
+    };
+    auto dval = [&](const RowI& R, int t, double& d0, double& d1) {
+      if (!R.gen) {
+        d0 = dsel(k, R.in0);
+        d1 = dsel(k, R.in1);
+      } else {
+        const RowCls rc = rcl_read(rcv, R.t - segbase);
+        d0 = cs_gen(k, rc, t, c0, tvw, jl0).d;
+        d1 = cs_gen(k, rc, t, c0 + 1, tvw, jl0 + 1).d;
+      }
+    };
+    // (A u)(row t) for both columns; d0/d1 = 1/D of row t.
+    auto apply = [&](const RowI& R, int t, const double2& um, const double2& u0, const double2& un, double ul,
+                     double ur, double& a0, double& a1, double& d0, double& d1) {
+      if (!R.gen) {
+        const double f0 = fsel(k, R.in0), f1 = fsel(k, R.in1);
+        a0 = lapf(k, f0, um.x, u0.x, un.x, ul, u0.y);
+        a1 = lapf(k, f1, um.y, u0.y, un.y, u0.x, ur);
+        d0 = dsel(k, R.in0);
+        d1 = dsel(k, R.in1);
+      } else {
+        const RowCls rc = rcl_read(rcv, R.t - segbase);
+        const CS x0 = cs_gen(k, rc, t, c0, tvw, jl0), x1 = cs_gen(k, rc, t, c0 + 1, tvw, jl0 + 1);
+        a0 = stencil<false>(k, x0, um.x, u0.x, un.x, ul, u0.y);
+        a1 = stencil<false>(k, x1, um.y, u0.y, un.y, u0.x, ur);
+        d0 = x0.d;
+        d1 = x1.d;
+      }
     };
 
-    const double* xr = X + int64_t(ib - 2) * pitch + c0;
-    // prologue: p_k on rows ib-2, ib-1; rows ib, ib+1 queued
-    const double2 rA = ld2(xr), pA = ld2(xr + poff);                          // row ib-2
-    double2 rin1 = ld2(xr + pitch);                                           // row ib-1: r_{k-1}(i+1) at step i
-    const double2 pB = ld2(xr + pitch + poff);
-    double2 rQ0 = ld2(xr + 2 * pitch), pQ0 = ld2(xr + 2 * pitch + poff);      // row ib   (queued)
-    double2 rQ1 = ld2(xr + 3 * pitch), pQ1 = ld2(xr + 3 * pitch + poff);      // row ib+1 (queued)
-    xr += 4 * pitch;                                                          // → row ib+2
-    double2 pa, pb;  // p_k rows i, i+1 at loop step i
-    {
-      CS x0, x1;
-      cls(ib - 2, x0, x1);
-      pa = dd(zc * (rA.x * x0.d) + beta * pA.x, zc * (rA.y * x1.d) + beta * pA.y);
-      cls(ib - 1, x0, x1);
-      pb = dd(zc * (rin1.x * x0.d) + beta * pB.x, zc * (rin1.y * x1.d) + beta * pB.y);
+    // prologue: p_k on rows ib-2, ib-1; x rows ib .. ib+PF-1 and w rows
+    // ib-2 .. ib-3+PF queued
+    const double* xb = Xm + int64_t(ib - 2) * pitch;
+    const double2 rA = ld2(xb + off), pA = ld2(xb + poff + off);
+    double2 rin1 = ld2(xb + pitch + off);  // r_{k-1}(i+1) at step i
+    const double2 pB = ld2(xb + pitch + poff + off);
+    double2 rq[PF], pq[PF], wq[PF];
+#pragma unroll
+    for (int q = 0; q < PF; ++q) {
+      const double* xr = Xm + int64_t(min(ib + q, ie + 2)) * pitch;
+      rq[q] = ld2(xr + off);
+      pq[q] = ld2(xr + poff + off);
+      wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
     }
-    double2 wQ0 = dd(0.0, 0.0), wQ1 = dd(0.0, 0.0);
+    RowI R0 = rinfo(ib - 2), R1 = rinfo(ib - 1);
+    double2 pa, pb;  // p_k rows i, i+1 at step i
+    {
+      double d0, d1;
+      dval(R0, ib - 2, d0, d1);
+      pa = dd(zc * (rA.x * d0) + beta * pA.x, zc * (rA.y * d1) + beta * pA.y);
+      dval(R1, ib - 1, d0, d1);
+      pb = dd(zc * (rin1.x * d0) + beta * pB.x, zc * (rin1.y * d1) + beta * pB.y);
+    }
     double2 sI = dd(0.0, 0.0), rkI = dd(0.0, 0.0), zM = dd(0.0, 0.0), zI = dd(0.0, 0.0);
-    const double* wr = W + int64_t(ib) * wp + c0;  // w(i+2) at step i = ib-2
 
     for (int i = ib - 2; i <= ie; ++i) {
-      // ---- prefetch: x row i+4, w row i+2 (rows past nx+2 are padding) ----
-      const double2 rN = ld2(xr), pN = ld2(xr + poff);
-      const double2 wN = ld2(wr);
-      xr += pitch;
-      wr += wp;
+      if (i > ib && (i - ib) % FSEG == 0) load_seg(i - 2);  // rows i-2 .. i+61
+      // ---- prefetch x row i+2+PF and w row i+PF, clamped to the rows this
+      // item reads (a clamped re-read hits L2; no predicated loads) ----
+      const double* xn = Xm + int64_t(min(i + 2 + PF, ie + 2)) * pitch;
+      const double2 rN = ld2(xn + off), pN = ld2(xn + poff + off);
+      const double2 wN = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
+      const double2 rQ0 = rq[0], pQ0 = pq[0], wQ0 = wq[0];
 
       // p_k(i+2) = z_{k-1} + β p_{k-1}
-      CS y0, y1;
-      cls(i + 2, y0, y1);
-      const double2 pc = dd(zc * (rQ0.x * y0.d) + beta * pQ0.x, zc * (rQ0.y * y1.d) + beta * pQ0.y);
+      const RowI R2 = rinfo(i + 2);
+      double d20, d21;
+      dval(R2, i + 2, d20, d21);
+      const double2 pc = dd(zc * (rQ0.x * d20) + beta * pQ0.x, zc * (rQ0.y * d21) + beta * pQ0.y);
 
       // s(i+1) = A p_k, r_k(i+1), z_k(i+1)
-      CS x0, x1;
-      cls(i + 1, x0, x1);
-      const double pl = dpp_shr1(pb.y), pr = dpp_shl1(pb.x);
-      const double s0 = stencil<false>(k, x0, pa.x, pb.x, pc.x, pl, pb.y);
-      const double s1 = stencil<false>(k, x1, pa.y, pb.y, pc.y, pb.x, pr);
+      double s0, s1, d10, d11;
+      apply(R1, i + 1, pa, pb, pc, dpp_shr1(pb.y), dpp_shl1(pb.x), s0, s1, d10, d11);
       const double rk0 = rin1.x - alpha * s0, rk1 = rin1.y - alpha * s1;
-      const bool rl = rlive(i + 1);
-      const double zn0 = (rl && lv0) ? rk0 * x0.d : 0.0;
-      const double zn1 = (rl && lv1) ? rk1 * x1.d : 0.0;
+      const int64_t gr = k.gi0 + i + 1;
+      const bool rl = gr >= 1 && gr <= k.M - 1;
+      const double zn0 = (rl && lv0) ? rk0 * d10 : 0.0;
+      const double zn1 = (rl && lv1) ? rk1 * d11 : 0.0;
 
       if (i >= ib) {
-        // q(i) = A z_k, the 7 sums, and the row-i outputs
-        CS q0c, q1c;
-        cls(i, q0c, q1c);
-        const double zl = dpp_shr1(zI.y), zr = dpp_shl1(zI.x);
-        const double q0 = stencil<false>(k, q0c, zM.x, zI.x, zn0, zl, zI.y);
-        const double q1 = stencil<false>(k, q1c, zM.y, zI.y, zn1, zI.x, zr);
-        if (o0) {
-          sg += rkI.x * zI.x;
-          sd += zI.x * q0;
-          se += zI.x * sI.x;
-          sps += pa.x * sI.x;
-          szz += zI.x * zI.x;
-          szp += zI.x * pa.x;
-          spp += pa.x * pa.x;
-        }
-        if (o1) {
-          sg += rkI.y * zI.y;
-          sd += zI.y * q1;
-          se += zI.y * sI.y;
-          sps += pa.y * sI.y;
-          szz += zI.y * zI.y;
-          szp += zI.y * pa.y;
-          spp += pa.y * pa.y;
-        }
-        double* yr = Y + int64_t(i) * pitch + c0;
-        double* wd = W + int64_t(i) * wp + c0;
+        // q(i) = A z_k, the 7 sums, the row-i outputs
+        double q0, q1, e0, e1;
+        apply(R0, i, zM, zI, dd(zn0, zn1), dpp_shr1(zI.y), dpp_shl1(zI.x), q0, q1, e0, e1);
+        const double zo0 = o0 ? zI.x : 0.0, po0 = o0 ? pa.x : 0.0;
+        const double zo1 = o1 ? zI.y : 0.0, po1 = o1 ? pa.y : 0.0;
+        sg += rkI.x * zo0 + rkI.y * zo1;
+        sd += zo0 * q0 + zo1 * q1;
+        se += zo0 * sI.x + zo1 * sI.y;
+        sps += po0 * sI.x + po1 * sI.y;
+        szz += zo0 * zo0 + zo1 * zo1;
+        szp += zo0 * po0 + zo1 * po1;
+        spp += po0 * po0 + po1 * po1;
+        double* yr = Ym + int64_t(i) * pitch + off;
+        double* wd = Wm + int64_t(i) * wp + off;
         const double2 wv = dd(wQ0.x + alpha * pa.x, wQ0.y + alpha * pa.y);
         if (o1) {
-          *reinterpret_cast<double2*>(yr) = rkI;
-          *reinterpret_cast<double2*>(yr + poff) = pa;
-          *reinterpret_cast<double2*>(wd) = wv;
+          st2<NT>(yr, rkI);
+          st2<NT>(yr + poff, pa);
+          st2<NT>(wd, wv);
         } else if (o0) {
           yr[0] = rkI.x;
           yr[poff] = pa.x;
@@ -225,6 +338,8 @@ __global__ __launch_bounds__(TJ) void kS(KParams k, int par) {
         }
       }
       // ---- shift the register window ----
+      R0 = R1;
+      R1 = R2;
       zM = zI;
       zI = dd(zn0, zn1);
       sI = dd(s0, s1);
@@ -232,12 +347,15 @@ __global__ __launch_bounds__(TJ) void kS(KParams k, int par) {
       pa = pb;
       pb = pc;
       rin1 = rQ0;
-      rQ0 = rQ1;
-      pQ0 = pQ1;
-      rQ1 = rN;
-      pQ1 = pN;
-      wQ0 = wQ1;
-      wQ1 = wN;
+#pragma unroll
+      for (int q = 0; q + 1 < PF; ++q) {
+        rq[q] = rq[q + 1];
+        pq[q] = pq[q + 1];
+        wq[q] = wq[q + 1];
+      }
+      rq[PF - 1] = rN;
+      pq[PF - 1] = pN;
+      wq[PF - 1] = wN;
     }
   }
 
@@ -317,8 +435,42 @@ __global__ void kUnpack(KParams k, int b) {
 
 }  // namespace
 
+// Kernel configuration (PE_SKERNEL, for tuning sweeps): 0 default = 4 rows
+// of loads in flight per wave + non-temporal w/output streams (8192² sweep:
+// 1373 it/s vs 1119 for 2 rows / temporal at 3 waves per SIMD — the sweep is
+// bound by HBM latency per wave, not by occupancy), 1 = 2 rows temporal,
+// 2 = 3 rows non-temporal, 3 = 5 rows non-temporal.
+static int s_cfg() {
+  static const int v = [] {
+    const char* e = std::getenv("PE_SKERNEL");
+    return e ? std::atoi(e) : 0;
+  }();
+  return v;
+}
+
+template <class F>
+static auto with_kS(F&& f) {
+  switch (s_cfg()) {
+    case 1: return f(kS<0, 2, false>);
+    case 2: return f(kS<0, 3, true>);
+    case 3: return f(kS<0, 5, true>);
+    default: return f(kS<0, 4, true>);
+  }
+}
+
 void launch_S(const KParams& k, int par, hipStream_t s) {
-  hipLaunchKernelGGL(kS, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
+  with_kS([&](auto kern) {
+    hipLaunchKernelGGL(kern, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
+    return 0;
+  });
+}
+
+int resident_blocks_S() {
+  return with_kS([](auto kern) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, TJ, 0) != hipSuccess) n = 0;
+    return n;
+  });
 }
 
 void launch_pack(const KParams& k, int b, hipStream_t s) {

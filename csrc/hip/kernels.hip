@@ -29,6 +29,8 @@
 // the 1-D chord tables.  Dot products end in a deterministic last-workgroup
 // reduction (agent-scope release/acquire ticket; partials summed in block
 // order), so results are bitwise reproducible run to run.
+#include <algorithm>
+
 #include "kcommon.hpp"
 
 namespace pe {
@@ -520,6 +522,18 @@ __global__ void kCoef(KParams k, double* a, double* b, double* D) {
 }  // namespace
 
 int grid_blocks(const KParams& k) { return k.nblocks; }
+
+int resident_blocks_classic(int variant) {
+  int n = 0, m = 0;
+  if (variant == 1) {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kF<true>, TJ, 0) != hipSuccess) n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, kG<true>, TJ, 0) != hipSuccess) m = 0;
+  } else {
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kF<false>, TJ, 0) != hipSuccess) n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&m, kG<false>, TJ, 0) != hipSuccess) m = 0;
+  }
+  return std::min(n, m);
+}
 
 static unsigned flat_blocks(const KParams& k) {
   const int64_t n = (k.nx + 2) * (k.ny + 2);

@@ -91,7 +91,6 @@ constexpr int kWPB = 4;          // waves per block
 constexpr int kSW = 128;         // columns per wave strip (2 per lane, 16-B accesses)
 constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live one per lane)
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
-constexpr int kFTImax = 60;      // fused sweep: max rows per work item (rows ib-2..ie+2 one per lane)
 
 void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
                  hipStream_t s);
@@ -111,6 +110,10 @@ void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hip
 void launch_apply_A(const KParams& k, const double* p, double* Ap, hipStream_t s);
 void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t s);
 int grid_blocks(const KParams& k);
+// Resident 256-thread blocks per CU of the marching kernels (occupancy API;
+// 0 when unavailable).  Sizes the persistent grids.
+int resident_blocks_S();
+int resident_blocks_classic(int variant);
 
 }  // namespace dev
 }  // namespace pe

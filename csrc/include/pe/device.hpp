@@ -117,6 +117,7 @@ class DeviceSolver {
   std::vector<HaloPhase> halo_phases(int buf) const;
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
+  uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   hipStream_t stream() const { return stream_; }
 
   // State / data access.

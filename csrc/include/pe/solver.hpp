@@ -64,6 +64,7 @@ struct SolveResult {
   std::vector<double> history;
   int Px = 1, Py = 1;
   std::string backend;
+  std::string algo;      // device: "fused" (single-sweep) or "classic"
 };
 
 // ---- CPU backends (reference stage0..3 equivalents) -----------------------

@@ -52,6 +52,7 @@ class SolveReport:
     init: str = "zero"
     w: Optional[np.ndarray] = None
     rank: int = 0
+    algo: str = ""
 
     @property
     def iters_per_s(self) -> float:
@@ -91,7 +92,8 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         backend=backend, M=prob.M, N=prob.N, ranks=ranks, Px=res.Px, Py=res.Py, threads=threads,
         iters=int(res.iters), converged=bool(res.converged), breakdown=bool(res.breakdown),
         last_diff=float(res.last_diff), timers=dict(res.timers), l2_err=float(res.l2_err),
-        max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank)
+        max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank,
+        algo=str(getattr(res, "algo", "")))
 
 
 def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str = "aspect",
