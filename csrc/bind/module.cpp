@@ -339,6 +339,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)
+      .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("blocks", [](DeviceSolver& s) { return dev::grid_blocks(s.params()); })
       .def_property_readonly("block", &DeviceSolver::block);

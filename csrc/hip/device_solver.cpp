@@ -83,16 +83,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const int64_t rows = nx + 6;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
     wsize_ = ((rows * plane_ + 64 + 31) / 32) * 32;
-    fields_ = static_cast<double*>(field_alloc(sizeof(double) * (2 * xsize_ + wsize_)));
     k.pitch = 2 * plane_;
     k.wpitch = plane_;
     k.poff = plane_;
-    k.x[0] = fields_ + k.pitch + 1;  // local (0, 0): row -1, column -1 at element 0
-    k.x[1] = fields_ + xsize_ + k.pitch + 1;
-    k.w = fields_ + 2 * xsize_ + plane_ + 1;
-    k.r = k.x[0];
-    k.p[0] = k.x[0] + plane_;
-    k.p[1] = k.x[1] + plane_;
+    fields_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_));
+    xalt_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_));
+    walt_ = static_cast<double*>(field_alloc(sizeof(double) * wsize_));
+    set_fused_fields(fields_, xalt_, walt_);
     hsize_ = std::max<int64_t>(1, nx) * 4;
     rows_hi = nx + 3;
     cols_hi = dev::kFSW * strips + 3;
@@ -198,6 +195,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
+  if (fused_) choose_placement();
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -208,6 +206,102 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
 }
 
+void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
+  KParams& k = *kp_;
+  fields_ = x0;
+  xalt_ = x1;
+  walt_ = w;
+  k.x[0] = x0 + k.pitch + 1;  // local (0, 0): row -1, column -1 at element 0
+  k.x[1] = x1 + k.pitch + 1;
+  k.w = w + plane_ + 1;
+  k.r = k.x[0];
+  k.p[0] = k.x[0] + plane_;
+  k.p[1] = k.x[1] + plane_;
+}
+
+// Memory-placement autotune (single-sweep, large blocks).  The same sweep
+// runs at two distinct speeds depending on which physical memory its arrays
+// land in (8192²: ≈1380 vs ≈1510 it/s; stable per allocation; consecutive
+// allocations come in slow and fast runs of several GB; no dependence on
+// row padding, virtual address or TLB misses — the slow placements show ~1.7×
+// the DRAM credit stalls; docs/PERFORMANCE.md).  Try up to
+// PE_PLACEMENT_TRIES (default 8) candidate allocations, each after a
+// PE_PLACEMENT_SKIP_GB (default 8) spacer so it lands in another region;
+// time a few local sweeps on real data (no communication) and keep the
+// fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
+void DeviceSolver::choose_placement() {
+  const double pts = double(blk_.nx) * double(blk_.ny);
+  int tries = pts >= double(1 << 22) ? 8 : 1;
+  if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
+  double skip_gb = 8.0;
+  if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
+  if (tries <= 1) return;
+  // spacers are transient; never let the search take more than 40 % of the
+  // free memory (several solvers may share the device)
+  {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+      const double per_try = skip_gb * double(1ull << 30) + double(sizeof(double) * (2 * xsize_ + wsize_));
+      tries = std::min<int>(tries, std::max(1, int(0.4 * double(free_b) / per_try)));
+    }
+  }
+  if (tries <= 1) return;
+  struct Cand {
+    double *x0, *x1, *w;
+    float ms;
+  };
+  std::vector<Cand> c;
+  std::vector<void*> spacers;
+  c.push_back(Cand{fields_, xalt_, walt_, 0.f});
+  for (int t = 0; t < tries; ++t) {
+    if (t > 0) {
+      void* sp = nullptr;
+      if (skip_gb > 0 && hipMalloc(&sp, size_t(skip_gb * double(1ull << 30))) != hipSuccess) break;
+      if (sp) spacers.push_back(sp);
+      void *a = nullptr, *b = nullptr, *w = nullptr;
+      if (hipMalloc(&a, sizeof(double) * xsize_) != hipSuccess) break;
+      if (hipMalloc(&b, sizeof(double) * xsize_) != hipSuccess) {
+        (void)hipFree(a);
+        break;
+      }
+      if (hipMalloc(&w, sizeof(double) * wsize_) != hipSuccess) {
+        (void)hipFree(a);
+        (void)hipFree(b);
+        break;
+      }
+      c.push_back(Cand{static_cast<double*>(a), static_cast<double*>(b), static_cast<double*>(w), 0.f});
+    }
+    set_fused_fields(c[t].x0, c[t].x1, c[t].w);
+    enqueue_init();
+    dev::launch_S(*kp_, 1, stream_);  // S_0 on real data (local sums only)
+    for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+    for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+    PE_HIP_CHECK(hipEventSynchronize(t1_));
+    PE_HIP_CHECK(hipEventElapsedTime(&c[t].ms, t0_, t1_));
+    // The two placements differ by ~9 %: a candidate 5 % faster than the
+    // slowest one seen is in the fast class — stop there.
+    float worst = 0.f;
+    for (const Cand& x : c) worst = std::max(worst, x.ms);
+    if (t > 0 && c[t].ms < 0.95f * worst) break;
+  }
+  (void)hipGetLastError();  // clear a failed search allocation
+  size_t best = 0;
+  for (size_t i = 1; i < c.size(); ++i)
+    if (c[i].ms < c[best].ms) best = i;
+  for (size_t i = 0; i < c.size(); ++i)
+    if (i != best) {
+      PE_HIP_CHECK(hipFree(c[i].x0));
+      PE_HIP_CHECK(hipFree(c[i].x1));
+      PE_HIP_CHECK(hipFree(c[i].w));
+    }
+  for (void* sp : spacers) PE_HIP_CHECK(hipFree(sp));
+  set_fused_fields(c[best].x0, c[best].x1, c[best].w);
+  placement_ms_.clear();
+  for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
+}
+
 DeviceSolver::~DeviceSolver() {
   if (graph_) (void)hipGraphExecDestroy(graph_);
   (void)hipEventDestroy(ev_[0]);
@@ -215,6 +309,8 @@ DeviceSolver::~DeviceSolver() {
   (void)hipEventDestroy(t0_);
   (void)hipEventDestroy(t1_);
   (void)hipFree(fields_);
+  if (xalt_) (void)hipFree(xalt_);
+  if (walt_) (void)hipFree(walt_);
   (void)hipFree(tables_);
   (void)hipFree(rowcls_);
   (void)hipFree(halo_);
@@ -282,7 +378,13 @@ double* DeviceSolver::err_dev() { return st_->err; }
 
 void DeviceSolver::enqueue_init() {
   const int64_t n = fused_ ? 2 * xsize_ + wsize_ : 4 * blk_.alloc;
-  PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * n, stream_));
+  if (fused_) {
+    PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * xsize_, stream_));
+    PE_HIP_CHECK(hipMemsetAsync(xalt_, 0, sizeof(double) * xsize_, stream_));
+    PE_HIP_CHECK(hipMemsetAsync(walt_, 0, sizeof(double) * wsize_, stream_));
+  } else {
+    PE_HIP_CHECK(hipMemsetAsync(fields_, 0, sizeof(double) * n, stream_));
+  }
   PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * hsize_ * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
   dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
@@ -312,6 +414,7 @@ void DeviceSolver::enqueue_iteration(int par) {
 
 bool DeviceSolver::graph_ready(int iters) {
   if (graph_ && graph_iters_ == iters) return true;
+  if (iters & 1) throw std::logic_error("graph chunks must have an even length");
   if (graph_) {
     PE_HIP_CHECK(hipGraphExecDestroy(graph_));
     graph_ = nullptr;
@@ -327,13 +430,24 @@ bool DeviceSolver::graph_ready(int iters) {
 }
 
 void DeviceSolver::enqueue_chunk(int iters) {
-  if (opt_.use_graph && comm_->capturable() && (iters % 2) == 0) {
-    graph_ready(iters);
+  // The captured graph starts at parity 0 and has an even length; iterations
+  // that would break the p / x ping-pong parity run eagerly.
+  int it = 0;
+  if (opt_.use_graph && comm_->capturable() && par_ == 0 && iters >= 2) {
+    const int n = iters - (iters & 1);
+    graph_ready(n);
     PE_HIP_CHECK(hipGraphLaunch(graph_, stream_));
-  } else {
-    for (int it = 0; it < iters; ++it) enqueue_iteration(it & 1);
+    it = n;
+  }
+  for (; it < iters; ++it) {
+    enqueue_iteration(par_);
+    par_ ^= 1;
   }
   PE_HIP_CHECK(hipGetLastError());
+}
+
+void DeviceSolver::enqueue_wflush() {
+  if (fused_) dev::launch_wflush(*kp_, stream_);
 }
 
 void DeviceSolver::read_state(DevState* out) {
@@ -344,6 +458,7 @@ void DeviceSolver::read_state(DevState* out) {
 void DeviceSolver::synchronize() { PE_HIP_CHECK(hipStreamSynchronize(stream_)); }
 
 void DeviceSolver::reset() {
+  par_ = 0;
   enqueue_init();
   if (fused_) {
     // r⁰ (and p = 0) in x[0] → halos → sweep S_0 (z₀, A z₀ and their sums,
@@ -364,8 +479,7 @@ void DeviceSolver::run_iterations(int64_t iters, bool use_graph) {
   opt_.use_graph = use_graph;
   int64_t done = 0;
   while (done < iters) {
-    int64_t n = std::min<int64_t>(chunk_, iters - done);
-    if (n >= 2) n -= (n & 1);
+    const int64_t n = std::min<int64_t>(chunk_, iters - done);
     enqueue_chunk(int(n));
     done += n;
   }
@@ -442,6 +556,7 @@ SolveResult DeviceSolver::solve() {
       read_state(&hs);
       if (hs.done || k >= cap) break;
     }
+    par_ = int(k & 1);
     for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
   } else {
     int64_t enq = 0;
@@ -472,6 +587,7 @@ SolveResult DeviceSolver::solve() {
   if (!opt_.timing) res.t.gpu = ms * 1e-3;
 
   DevState hs;
+  enqueue_wflush();
   if (opt_.compute_error) {
     dev::launch_error(*kp_, stream_);
     comm_->allreduce_sum(st_->err, 1, stream_);
@@ -504,6 +620,7 @@ SolveResult DeviceSolver::solve() {
 
 void DeviceSolver::copy_w(double* host, bool owned_only) {
   const KParams& k = *kp_;
+  enqueue_wflush();
   if (owned_only) {
     PE_HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * blk_.ny, k.w + k.wpitch + 1, sizeof(double) * k.wpitch,
                                   sizeof(double) * blk_.ny, blk_.nx, hipMemcpyDeviceToHost, stream_));
@@ -638,6 +755,7 @@ SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, con
   for (int r = 0; r < ranks; ++r) s[r]->synchronize();
   res.t.iterate = secs(t_loop, clk::now());
   res.t.gpu = res.t.iterate;
+  for (int r = 0; r < ranks; ++r) s[r]->enqueue_wflush();
   if (opt.compute_error) {
     for (int r = 0; r < ranks; ++r) s[r]->enqueue_error();
     reduce(dp + 2 * ranks, 1, 0);

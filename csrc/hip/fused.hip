@@ -97,11 +97,33 @@ __device__ __forceinline__ double2 ldw(const double* p) {
   }
 }
 
+// Pointwise w += a1·p_{k-1} + a2·p_k over the owned nodes (rare paths:
+// convergence / iteration cap in a deferring sweep, breakdown, host flush).
+// p_k = zc·D⁻¹r_{k-1} + β p_{k-1} from the input buffer xin.
+__device__ void w_pointwise(const KParams& k, const double* xin, double a1, double a2, double zc, double beta) {
+  const int64_t n = k.nx * k.ny;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
+    const double r = xin[li * k.pitch + lj], pold = xin[li * k.pitch + k.poff + lj];
+    const double pk = zc * (r * cset_mem<false>(k, li, lj).d) + beta * pold;
+    double& w = k.w[li * k.wpitch + lj];
+    w = w + a1 * pold + a2 * pk;
+  }
+}
+
 // OCC > 0 caps registers for OCC waves per SIMD (amdgpu_waves_per_eu); PF =
 // rows of loads in flight per wave; NT = non-temporal w and output streams
 // (they are not re-read within the sweep, so they should not evict the halo
 // rows neighbouring items re-read from L2).
-template <int OCC, int PF, bool NT>
+//
+// WM — deferred solution update.  w_{k+1} = w_k + α_k p_k needs a w read and
+// write (16 of the 48 B/point) every sweep; but sweep k+1 still holds p_k
+// (its input), so odd sweeps (WM = 0) leave α_k p_k pending and even sweeps
+// (WM = 2) apply w += α_{k-1} p_{k-1} + α_k p_k: 40 B/point per iteration on
+// average.  A deferring sweep that is the last one (converged / cap) applies
+// its own term pointwise; a breakdown applies the pending one; the host
+// flushes a pending term (launch_wflush) before w is read.
+template <int OCC, int PF, bool NT, int WM>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   if (st->done) return;
@@ -119,11 +141,13 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     g = R[0] * hh;
     beta = st->iter == 0 ? 0.0 : g / st->gprev;
     const double den = R[1] * hh + 2.0 * beta * (R[2] * hh) + beta * beta * (R[3] * hh);
-    if (fabs(den) < 1e-15) {  // breakdown: stop before touching w (reference :413)
+    if (fabs(den) < 1e-15) {  // breakdown: stop before this sweep's w term (reference :413)
+      if (WM == 2 && st->wpend) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->status = 2;
         st->iter = kiter;
         st->done = 1;
+        st->wpend = 0;
       }
       return;
     }
@@ -131,7 +155,26 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     const double pn2 = fmax(R[4] + 2.0 * beta * R[5] + beta * beta * R[6], 0.0);
     diff = k.weighted ? fabs(alpha) * sqrt(pn2 * hh) : fabs(alpha) * sqrt(pn2);
     zc = 1.0;
+    const bool conv = k.check_tol && diff < k.tol;
+    if (WM == 0 && (conv || kiter >= k.max_iter)) {
+      // last sweep of the solve: only w changes (w += α_k p_k, pointwise)
+      w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->gprev = g;
+        st->rz_cur = g;
+        st->alpha = alpha;
+        st->beta = beta;
+        st->last_diff = diff;
+        st->iter = kiter;
+        st->status = conv ? 1 : 3;
+        st->done = 1;
+        st->wpend = 0;
+      }
+      return;
+    }
   }
+  // α of the pending term left by the previous (deferring) sweep
+  const double alpha_prev = (WM == 2 && st->wpend) ? st->alpha : 0.0;
 
   // Row pointers at column -1 (uniform, SGPR) + lane offset (unsigned VGPR).
   const double* __restrict__ Xm = k.x[par ^ 1] - 1;
@@ -255,7 +298,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       const double* xr = Xm + int64_t(min(ib + q, ie + 2)) * pitch;
       rq[q] = ld2(xr + off);
       pq[q] = ld2(xr + poff + off);
-      wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
+      if constexpr (WM == 2) wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
+      else wq[q] = dd(0.0, 0.0);
     }
     RowI R0 = rinfo(ib - 2), R1 = rinfo(ib - 1);
     double2 pa, pb;  // p_k rows i, i+1 at step i
@@ -267,6 +311,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       pb = dd(zc * (rin1.x * d0) + beta * pB.x, zc * (rin1.y * d1) + beta * pB.y);
     }
     double2 sI = dd(0.0, 0.0), rkI = dd(0.0, 0.0), zM = dd(0.0, 0.0), zI = dd(0.0, 0.0);
+    double2 qa = pA, qb = pB;  // p_{k-1} rows i, i+1 (WM == 2: the pending term)
 
     for (int i = ib - 2; i <= ie; ++i) {
       if (i > ib && (i - ib) % FSEG == 0) load_seg(i - 2);  // rows i-2 .. i+61
@@ -274,7 +319,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       // item reads (a clamped re-read hits L2; no predicated loads) ----
       const double* xn = Xm + int64_t(min(i + 2 + PF, ie + 2)) * pitch;
       const double2 rN = ld2(xn + off), pN = ld2(xn + poff + off);
-      const double2 wN = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
+      double2 wN = dd(0.0, 0.0);
+      if constexpr (WM == 2) wN = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
       const double2 rQ0 = rq[0], pQ0 = pq[0], wQ0 = wq[0];
 
       // p_k(i+2) = z_{k-1} + β p_{k-1}
@@ -307,15 +353,15 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         spp += po0 * po0 + po1 * po1;
         double* yr = Ym + int64_t(i) * pitch + off;
         double* wd = Wm + int64_t(i) * wp + off;
-        const double2 wv = dd(wQ0.x + alpha * pa.x, wQ0.y + alpha * pa.y);
+        const double2 wv = dd(wQ0.x + alpha_prev * qa.x + alpha * pa.x, wQ0.y + alpha_prev * qa.y + alpha * pa.y);
         if (o1) {
           st2<NT>(yr, rkI);
           st2<NT>(yr + poff, pa);
-          st2<NT>(wd, wv);
+          if constexpr (WM == 2) st2<NT>(wd, wv);
         } else if (o0) {
           yr[0] = rkI.x;
           yr[poff] = pa.x;
-          wd[0] = wv.x;
+          if constexpr (WM == 2) wd[0] = wv.x;
         }
         // y-direction halo strips (columns 1,2 and ny-1,ny) → send buffers
         if (k.has[DOWN] && o0 && c0 == 1) {
@@ -346,6 +392,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       rkI = dd(rk0, rk1);
       pa = pb;
       pb = pc;
+      qa = qb;
+      qb = pQ0;
       rin1 = rQ0;
 #pragma unroll
       for (int q = 0; q + 1 < PF; ++q) {
@@ -370,6 +418,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     if (threadIdx.x == 0) {
 #pragma unroll
       for (int n = 0; n < 7; ++n) st->fs[par][n] = t[n];
+      st->wpend = WM == 0 ? 1 : 0;
+      st->wpar = par;
       if (first) {
         st->started = 1;
       } else {
@@ -391,6 +441,20 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     }
   }
 }
+
+// Apply a pending α_k p_k (p_k = p-plane of x[wpar]) before w is read.
+__global__ void kWFlush(KParams k) {
+  DevState* st = k.st;
+  if (!st->wpend) return;
+  const double a = st->alpha;
+  const double* p = k.x[st->wpar] + k.poff;
+  const int64_t n = k.nx * k.ny;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
+    k.w[li * k.wpitch + lj] += a * p[li * k.pitch + lj];
+  }
+}
+__global__ void kWFlushDone(KParams k) { k.st->wpend = 0; }
 
 // y-direction halo strips of buffer b (one thread per owned row).
 __global__ void kPack(KParams k, int b) {
@@ -448,29 +512,40 @@ static int s_cfg() {
   return v;
 }
 
-template <class F>
+template <int WM, class F>
 static auto with_kS(F&& f) {
   switch (s_cfg()) {
-    case 1: return f(kS<0, 2, false>);
-    case 2: return f(kS<0, 3, true>);
-    case 3: return f(kS<0, 5, true>);
-    default: return f(kS<0, 4, true>);
+    case 1: return f(kS<0, 2, false, WM>);
+    case 2: return f(kS<0, 3, true, WM>);
+    case 3: return f(kS<0, 5, true, WM>);
+    default: return f(kS<0, 4, true, WM>);
   }
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s) {
-  with_kS([&](auto kern) {
+  auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
     return 0;
-  });
+  };
+  // odd iterations (par 0) defer their w term, even ones (par 1) apply both
+  if (par == 0) with_kS<0>(go);
+  else with_kS<2>(go);
+}
+
+void launch_wflush(const KParams& k, hipStream_t s) {
+  const int64_t n = k.nx * k.ny;
+  const unsigned b = unsigned(std::min<int64_t>(4096, std::max<int64_t>(1, (n + 255) / 256)));
+  hipLaunchKernelGGL(kWFlush, dim3(b), dim3(256), 0, s, k);
+  hipLaunchKernelGGL(kWFlushDone, dim3(1), dim3(1), 0, s, k);
 }
 
 int resident_blocks_S() {
-  return with_kS([](auto kern) {
+  auto occ = [](auto kern) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, TJ, 0) != hipSuccess) n = 0;
     return n;
-  });
+  };
+  return std::min(with_kS<0>(occ), with_kS<2>(occ));
 }
 
 void launch_pack(const KParams& k, int b, hipStream_t s) {

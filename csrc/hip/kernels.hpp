@@ -42,7 +42,9 @@ struct DevState {
   double fs[2][8];
   double gprev;      // (r,z) consumed by the previous sweep (β denominator), h-weighted
   int started;       // 0 until sweep S_0 (z_0, A z_0 and their dots) has run
-  int pad2[3];
+  int wpend;         // 1: α·p_k of the last (deferring) sweep not yet added to w
+  int wpar;          // buffer x[wpar] holding that p_k
+  int pad2;
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -103,6 +105,8 @@ void launch_S(const KParams& k, int par, hipStream_t s);
 // into send_dn / send_up ([nx][4]); unpack recv_dn / recv_up into columns
 // {-1,0} / {ny+1,ny+2}.
 void launch_pack(const KParams& k, int b, hipStream_t s);
+// Add a pending deferred w term (no-op when none is pending).
+void launch_wflush(const KParams& k, hipStream_t s);
 void launch_unpack(const KParams& k, int b, hipStream_t s);
 // Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);

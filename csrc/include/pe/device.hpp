@@ -102,6 +102,7 @@ class DeviceSolver {
   void enqueue_pack(int buf);   // single-sweep: y strips of buffer `buf` → send buffers
   void enqueue_unpack(int buf); // single-sweep: recv buffers → y halo columns of `buf`
   void enqueue_error();
+  void enqueue_wflush();        // single-sweep: add a deferred α·p term to w (no-op if none)
   double* red_F_dev();
   double* red_G_dev();
   double* fs_dev(int par);
@@ -118,6 +119,7 @@ class DeviceSolver {
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
+  const std::vector<float>& placement_ms() const { return placement_ms_; }
   hipStream_t stream() const { return stream_; }
 
   // State / data access.
@@ -135,6 +137,8 @@ class DeviceSolver {
 
  private:
   void build_tables(int64_t rows_hi, int64_t cols_hi);
+  void set_fused_fields(double* x0, double* x1, double* w);
+  void choose_placement();
   void enqueue_iteration(int par);
   void enqueue_exchange(int buf);
   void enqueue_chunk(int iters);
@@ -148,6 +152,9 @@ class DeviceSolver {
   hipStream_t stream_ = nullptr;
   bool fused_ = false;
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w
+  double* xalt_ = nullptr;    // single-sweep: x1 (separate allocation)
+  double* walt_ = nullptr;    // single-sweep: w
+  std::vector<float> placement_ms_;  // per-candidate sweep time of the placement search
   int64_t xsize_ = 0, wsize_ = 0, plane_ = 0;
   double* tables_ = nullptr;
   int* rowcls_ = nullptr;
@@ -160,6 +167,7 @@ class DeviceSolver {
   hipGraphExec_t graph_ = nullptr;
   int graph_iters_ = 0;
   int chunk_ = 16;
+  int par_ = 0;  // parity of the next iteration (x / p ping-pong)
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
 };

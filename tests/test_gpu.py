@@ -77,7 +77,9 @@ def test_fused_large_golden(gpu, M, N):
     assert rep.l2_err == pytest.approx(GOLDEN_L2[(M, N)], rel=5e-3)
 
 
-def test_fused_matches_classic_state(gpu, nat):
+@pytest.mark.parametrize("iters", [40, 41])
+def test_fused_matches_classic_state(gpu, nat, iters):
+    # odd counts end on a deferring sweep: w() must flush the pending α·p term
     prob = EllipseProblem(300, 500)
     blk = D.block(300, 500, 1, 0)
     out = {}
@@ -88,14 +90,52 @@ def test_fused_matches_classic_state(gpu, nat):
         s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
         assert s.fused == (algo == 2)
         s.reset()
-        s.run_iterations(40, False)
+        s.run_iterations(iters, False)
         s.synchronize()
         out[algo] = (s.state(), s.w())
     (sc, wc), (sf, wf) = out[1], out[2]
-    assert sc["iter"] == sf["iter"] == 40
+    assert sc["iter"] == sf["iter"] == iters
     assert sf["alpha"] == pytest.approx(sc["alpha"], rel=1e-9)
     assert sf["beta"] == pytest.approx(sc["beta"], rel=1e-9)
     np.testing.assert_allclose(wf, wc, rtol=0, atol=1e-12 * np.abs(wc).max())
+
+
+@pytest.mark.parametrize("algo", [1, 2])
+def test_run_iterations_parity_across_calls(gpu, nat, algo):
+    # 3 + 4 + 5 iterations (graph and eager, odd boundaries) == 12 in one call
+    prob = EllipseProblem(200, 260)
+    blk = D.block(200, 260, 1, 0)
+    res = []
+    for parts in ([12], [3, 4, 5]):
+        opt = nat.SolveOptions()
+        opt.algo = algo
+        opt.check_tol = False
+        opt.chunk = 4
+        s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
+        s.reset()
+        for n in parts:
+            s.run_iterations(n, True)
+        s.synchronize()
+        res.append((s.state()["iter"], s.w()))
+    assert res[0][0] == res[1][0] == 12
+    assert np.array_equal(res[0][1], res[1][1])
+
+
+@pytest.mark.parametrize("M,N", [(40, 40), (400, 600), (10, 10)])
+def test_fused_odd_convergence_and_cap(gpu, M, N):
+    # convergence on a deferring (odd) sweep and an odd iteration cap both
+    # leave a complete w
+    prob = EllipseProblem(M, N)
+    a = solve(prob, backend="hip", return_w=True, algo="classic")
+    b = solve(prob, backend="hip", return_w=True, algo="fused")
+    assert a.iters == b.iters
+    np.testing.assert_allclose(b.w, a.w, rtol=0, atol=1e-10)
+    capped = EllipseProblem(M, N)
+    capped.max_iter = 7
+    c = solve(capped, backend="hip", return_w=True, algo="classic")
+    d = solve(capped, backend="hip", return_w=True, algo="fused")
+    assert c.iters == d.iters == 7 and not d.converged
+    np.testing.assert_allclose(d.w, c.w, rtol=0, atol=1e-9 * max(1e-30, np.abs(c.w).max()))
 
 
 def test_virtual_ranks_golden_grid(gpu):

@@ -24,5 +24,5 @@ for rep in range(1):
     for i, s in enumerate(solvers):
         dt = s.time_iterations(300, True)
         a = s.fields_address
-        print(f"rep {rep} solver {i}: {300 / dt:.1f} it/s  base=0x{a:x} mod2M=0x{a % (2 << 20):x} mod1G=0x{a % (1 << 30):x}",
+        print(f"rep {rep} solver {i}: {300 / dt:.1f} it/s  placement_ms={[round(x, 3) for x in s.placement_ms]}",
               flush=True)
