@@ -177,17 +177,25 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const int64_t bands = std::max<int64_t>(1, wave_cap / std::max<int64_t>(1, strips));
     ti = int((nx + bands - 1) / bands);
   }
+  const bool big = double(nx) * double(ny) >= double(1 << 24);
+  if (fused_ && ti_env == 0) ti = big ? 16 : 8;  // sweeps: 8192² dynamic 16 rows; ≤ 4096² static 8
   k.ti = ti;
   k.nstrips = int(strips);
   k.nitems = int(strips * ((nx + ti - 1) / ti));
-  k.order = 0;
+  // Single-sweep item order: the per-XCD dynamic queue (order 3) when the
+  // block is large (8192²: +8 % — boundary-band strips cost more, a static
+  // deal leaves waves idle), static chunk-major otherwise (small blocks: the
+  // queue's pull latency and the extra reduction launch do not pay).
+  k.order = (fused_ && big) ? 3 : 0;
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
+  if (!fused_ && k.order > 1) k.order = 0;
   const int per = (k.nitems + wave_cap - 1) / wave_cap;
   const int waves = (k.nitems + per - 1) / per;
   k.nblocks = std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
   const int64_t npart = 8 * std::max<int64_t>(int64_t(k.nblocks), 4096);
-  PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * npart));
+  PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + (fused_ ? 8 * int64_t(k.nitems) : 0))));
   k.partial = partial_;
+  k.itemsum = fused_ ? partial_ + npart : nullptr;
   k.ih1sq = 1.0 / k.h1sq;
   k.ih2sq = 1.0 / k.h2sq;
   k.D_in = (1.0 + 1.0) / k.h1sq + (1.0 + 1.0) / k.h2sq;

@@ -111,6 +111,63 @@ __device__ void w_pointwise(const KParams& k, const double* xin, double a1, doub
   }
 }
 
+// Scalars of sweep k from the previous sweep's global sums (pure function
+// of the device state: the sweep kernel and the item-reduction kernel both
+// evaluate it and get the same bits).
+struct Scal {
+  bool first;
+  long long kiter;
+  double g, alpha, beta, diff, zc, den;
+};
+__device__ __forceinline__ Scal sweep_scalars(const KParams& k, const DevState* st, int par) {
+  Scal c;
+  c.first = st->started == 0;
+  c.kiter = st->iter + 1;
+  c.g = c.alpha = c.beta = c.diff = c.zc = 0.0;
+  c.den = 1.0;
+  if (!c.first) {
+    const double hh = k.h1 * k.h2;
+    const double* R = st->fs[par ^ 1];
+    c.g = R[0] * hh;
+    c.beta = st->iter == 0 ? 0.0 : c.g / st->gprev;
+    c.den = R[1] * hh + 2.0 * c.beta * (R[2] * hh) + c.beta * c.beta * (R[3] * hh);
+    c.alpha = c.g / c.den;
+    const double pn2 = fmax(R[4] + 2.0 * c.beta * R[5] + c.beta * c.beta * R[6], 0.0);
+    c.diff = k.weighted ? fabs(c.alpha) * sqrt(pn2 * hh) : fabs(c.alpha) * sqrt(pn2);
+    c.zc = 1.0;
+  }
+  return c;
+}
+
+// State update after a sweep's sums t[7] are known (one thread).
+template <int WM>
+__device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, int par, const Scal& c,
+                                               const double (&t)[7]) {
+#pragma unroll
+  for (int n = 0; n < 7; ++n) st->fs[par][n] = t[n];
+  st->wpend = WM == 0 ? 1 : 0;
+  st->wpar = par;
+  if (c.first) {
+    st->started = 1;
+  } else {
+    st->gprev = c.g;
+    st->rz_cur = c.g;
+    st->alpha = c.alpha;
+    st->beta = c.beta;
+    st->last_diff = c.diff;
+    st->iter = c.kiter;
+    if (k.check_tol && c.diff < k.tol) {
+      st->status = 1;
+      st->done = 1;
+    } else if (c.kiter >= k.max_iter) {
+      st->status = 3;
+      st->done = 1;
+    }
+  }
+#pragma unroll
+  for (int x = 0; x < 8; ++x) __hip_atomic_store(&st->qhead[x][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // OCC > 0 caps registers for OCC waves per SIMD (amdgpu_waves_per_eu); PF =
 // rows of loads in flight per wave; NT = non-temporal w and output streams
 // (they are not re-read within the sweep, so they should not evict the halo
@@ -132,16 +189,12 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   __shared__ WaveTV tvs[kWPB];
 
   // ---- scalars of this sweep from the previous sweep's global sums ----
-  const bool first = st->started == 0;
-  const long long kiter = st->iter + 1;
-  const double hh = k.h1 * k.h2;
-  double alpha = 0.0, beta = 0.0, zc = 0.0, g = 0.0, diff = 0.0;
+  const Scal sc = sweep_scalars(k, st, par);
+  const bool first = sc.first;
+  const long long kiter = sc.kiter;
+  const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
   if (!first) {
-    const double* R = st->fs[par ^ 1];
-    g = R[0] * hh;
-    beta = st->iter == 0 ? 0.0 : g / st->gprev;
-    const double den = R[1] * hh + 2.0 * beta * (R[2] * hh) + beta * beta * (R[3] * hh);
-    if (fabs(den) < 1e-15) {  // breakdown: stop before this sweep's w term (reference :413)
+    if (fabs(sc.den) < 1e-15) {  // breakdown: stop before this sweep's w term (reference :413)
       if (WM == 2 && st->wpend) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
         st->status = 2;
@@ -151,10 +204,6 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       }
       return;
     }
-    alpha = g / den;
-    const double pn2 = fmax(R[4] + 2.0 * beta * R[5] + beta * beta * R[6], 0.0);
-    diff = k.weighted ? fabs(alpha) * sqrt(pn2 * hh) : fabs(alpha) * sqrt(pn2);
-    zc = 1.0;
     const bool conv = k.check_tol && diff < k.tol;
     if (WM == 0 && (conv || kiter >= k.max_iter)) {
       // last sweep of the solve: only w changes (w += α_k p_k, pointwise)
@@ -187,16 +236,24 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
 
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   WaveTV& tvw = tvs[wid];
-  // Item walk.  order 2: the chunks (row bands) are split into 8 contiguous
-  // ranges, one per XCD (blocks are dealt round-robin to the 8 XCDs), so the
-  // halo rows an item shares with the chunk above/below are re-read from the
-  // same L2; orders 0/1: global chunk-major / strip-major.
+  // Item walk.  order 3 (default): dynamic — the chunks (row bands) are
+  // split into 8 contiguous ranges, one per XCD shard (blocks are dealt
+  // round-robin to the 8 XCDs), and the waves of shard x pull (strip, chunk)
+  // items in chunk-major order from a device-scope counter of their own
+  // (≤ 88 pulls/µs per counter; the next item is requested while the current
+  // one runs).  Boundary-band strips cost more than interior ones, so pulling
+  // beats any static deal; consecutive chunks stay on one XCD (halo rows
+  // re-read from its L2).  order 2: the same ranges dealt statically; 0/1:
+  // static global chunk-major / strip-major.
   const int nchunks = (nx + k.ti - 1) / k.ti;
+  const int nsh = min(8, int(gridDim.x));  // shards (every shard must own blocks)
+  const int xs = int(blockIdx.x) % nsh;
   int it0, istride, ilimit, chunk0;
-  if (k.order == 2) {
-    const int x = blockIdx.x & 7, nbx = (int(gridDim.x) - x + 7) >> 3;
-    const int c_lo = (x * nchunks) >> 3, c_hi = ((x + 1) * nchunks) >> 3;
-    it0 = (int(blockIdx.x) >> 3) * kWPB + wid;
+  unsigned* head = &st->qhead[xs][0];
+  if (k.order >= 2) {
+    const int nbx = (int(gridDim.x) - xs + nsh - 1) / nsh;
+    const int c_lo = (xs * nchunks) / nsh, c_hi = ((xs + 1) * nchunks) / nsh;
+    it0 = (int(blockIdx.x) / nsh) * kWPB + wid;
     istride = nbx * kWPB;
     ilimit = (c_hi - c_lo) * k.nstrips;
     chunk0 = c_lo;
@@ -206,7 +263,16 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     ilimit = k.nitems;
     chunk0 = 0;
   }
-  for (int item = it0; item < ilimit; item += istride) {
+  const bool dyn = k.order == 3;
+  auto pull = [&]() -> int {
+    unsigned v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return __builtin_amdgcn_readfirstlane(int(v));
+  };
+  int item = dyn ? pull() : it0;
+  while (item < ilimit) {
+    unsigned nxt_v = 0;  // next item, requested now, read after this one
+    if (dyn && lane == 0) nxt_v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int s = (k.order == 1) ? item / nchunks : item % k.nstrips;
     const int ch = chunk0 + ((k.order == 1) ? item % nchunks : item / k.nstrips);
     const int J = -1 + s * FSW;
@@ -405,7 +471,25 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       pq[PF - 1] = pN;
       wq[PF - 1] = wN;
     }
+    if (dyn) {
+      // per-item sums (wave-reduced) in a fixed slot: the reduction kernel
+      // adds them in item order, so the result does not depend on which
+      // wave pulled which item
+      double v[7] = {sg, sd, se, sps, szz, szp, spp};
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+        for (int n = 0; n < 7; ++n) v[n] += __shfl_xor(v[n], o, 64);
+      if (lane == 0) {
+        double* dst = k.itemsum + 8 * (int64_t(ch) * k.nstrips + s);
+#pragma unroll
+        for (int n = 0; n < 7; ++n) dst[n] = v[n];
+      }
+      sg = sd = se = sps = szz = szp = spp = 0.0;
+    }
+    item = dyn ? __builtin_amdgcn_readfirstlane(int(nxt_v)) : item + istride;
   }
+  if (dyn) return;  // kRed reduces the item sums and finalizes
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   block_reduce<7, false>(v, sm);
@@ -416,28 +500,36 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
     if (threadIdx.x == 0) {
-#pragma unroll
-      for (int n = 0; n < 7; ++n) st->fs[par][n] = t[n];
-      st->wpend = WM == 0 ? 1 : 0;
-      st->wpar = par;
-      if (first) {
-        st->started = 1;
-      } else {
-        st->gprev = g;
-        st->rz_cur = g;
-        st->alpha = alpha;
-        st->beta = beta;
-        st->last_diff = diff;
-        st->iter = kiter;
-        if (k.check_tol && diff < k.tol) {
-          st->status = 1;
-          st->done = 1;
-        } else if (kiter >= k.max_iter) {
-          st->status = 3;
-          st->done = 1;
-        }
-      }
+      sweep_finalize<WM>(k, st, par, sc, t);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// Dynamic-queue sweeps: deterministic reduction of the per-item sums (item
+// order, fixed per-block ranges) and the state update.
+template <int WM>
+__global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
+  DevState* st = k.st;
+  if (st->done) return;  // includes a breakdown / last sweep handled by kS
+  __shared__ double sm[32];
+  __shared__ int sflag;
+  const Scal sc = sweep_scalars(k, st, par);
+  const int64_t n = k.nitems, lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (int64_t i = lo + threadIdx.x; i < hi; i += TJ)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) v[q] += k.itemsum[8 * i + q];
+  block_reduce<7, false>(v, sm);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) k.partial[7 * size_t(blockIdx.x) + q] = v[q];
+  if (arrive_last(&st->ticket[1], gridDim.x, &sflag)) {
+    double t[7];
+    reduce_partials<7>(k.partial, gridDim.x, t, sm);
+    if (threadIdx.x == 0) {
+      sweep_finalize<WM>(k, st, par, sc, t);
+      __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -530,6 +622,11 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(go);
   else with_kS<2>(go);
+  if (k.order == 3) {
+    const unsigned rb = unsigned(std::max(1, std::min(64, (k.nitems + 255) / 256)));
+    if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(rb), dim3(TJ), 0, s, k, par);
+    else hipLaunchKernelGGL(kRed<2>, dim3(rb), dim3(TJ), 0, s, k, par);
+  }
 }
 
 void launch_wflush(const KParams& k, hipStream_t s) {

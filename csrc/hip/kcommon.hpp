@@ -236,6 +236,17 @@ __device__ __forceinline__ CS cset_fast(const KParams& k, const RowCls& c, int64
   return cs;
 }
 
+// Division-free face coefficient (single-sweep path): l·(1/h) and ·(1/eps)
+// instead of the reference's l/h and /eps — one rounding apart, and it keeps
+// boundary-band rows (4 coefficients × 3 uses per row) from costing 24 fp64
+// divisions per lane and row.
+__device__ __forceinline__ double fcoef_fast(double l, double h, double inv_h, double inv_eps) {
+  if (fabs(l - h) < 1e-9) return 1.0;
+  if (l < 1e-9) return inv_eps;
+  const double t = l * inv_h;
+  return t + (1.0 - t) * inv_eps;
+}
+
 // cset with the row class already in SGPRs (fast arithmetic).
 __device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, int64_t q, int64_t lj, const TV& t) {
   CS x;
@@ -246,10 +257,13 @@ __device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, int64_t
     x.a0 = x.a1 = x.b0 = x.b1 = k.inv_eps;
     x.d = k.dinv_out;
   } else {
-    x.a0 = coefA(k, q, t);
-    x.a1 = coefA(k, q + 1, t);
-    x.b0 = coefB(k, q, t.hB);
-    x.b1 = coefB(k, q, t.hB1);
+    const double ih1 = -k.nih1, ih2 = -k.nih2;
+    const double* ct = k.colT + (q + 1) * 4;
+    const double half0 = cload(ct), half1 = cload(ct + 4), sB = cload(ct + 1), eB = cload(ct + 2);
+    x.a0 = fcoef_fast(chord_len(half0, t.sA, t.eA), k.h2, ih2, k.inv_eps);
+    x.a1 = fcoef_fast(chord_len(half1, t.sA, t.eA), k.h2, ih2, k.inv_eps);
+    x.b0 = fcoef_fast(chord_len(t.hB, sB, eB), k.h1, ih1, k.inv_eps);
+    x.b1 = fcoef_fast(chord_len(t.hB1, sB, eB), k.h1, ih1, k.inv_eps);
     x.d = 1.0 / ((x.a1 + x.a0) * k.ih1sq + (x.b1 + x.b0) * k.ih2sq);
   }
   return x;

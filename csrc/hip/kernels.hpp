@@ -45,6 +45,7 @@ struct DevState {
   int wpend;         // 1: α·p_k of the last (deferring) sweep not yet added to w
   int wpar;          // buffer x[wpar] holding that p_k
   int pad2;
+  unsigned qhead[8][16];  // single-sweep work queue heads, one 64-B line per XCD shard
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -73,7 +74,8 @@ struct KParams {
   int nstrips;                   // 128-column wave strips across ny (+ halo column)
   int nitems;                    // nstrips × ceil(nx / ti)
   int nblocks;                   // persistent grid size of the marching kernels
-  int order;                     // item order: 0 chunk-major (compact active window), 1 strip-major
+  int order;                     // item order: 0 chunk-major (compact active window), 1 strip-major,
+                                 // 2 per-XCD chunk ranges, 3 per-XCD dynamic queue (single-sweep)
   int check_tol;                 // 0 → never stop on ‖Δw‖ (fixed-iteration runs)
   double D_in, D_out;            // exact-arithmetic diagonal in the interior / exterior class
   double dinv_in, dinv_out;      // fast-arithmetic 1/D in the interior / exterior class
@@ -86,6 +88,7 @@ struct KParams {
   int64_t wpitch;
   int64_t poff;
   double* x[2];
+  double* itemsum;               // dynamic single-sweep: per-item sums [nitems][8]
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)

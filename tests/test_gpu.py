@@ -138,6 +138,21 @@ def test_fused_odd_convergence_and_cap(gpu, M, N):
     np.testing.assert_allclose(d.w, c.w, rtol=0, atol=1e-9 * max(1e-30, np.abs(c.w).max()))
 
 
+@pytest.mark.parametrize("order", ["0", "2", "3"])
+def test_fused_item_orders_deterministic(gpu, order, monkeypatch):
+    # order 3 = per-XCD dynamic work queue: which wave takes which item varies
+    # run to run, the per-item sums keep the result bitwise reproducible
+    monkeypatch.setenv("PE_ORDER", order)
+    prob = EllipseProblem(800, 1200)
+    a = solve(prob, backend="hip", return_w=True, algo="fused")
+    b = solve(prob, backend="hip", return_w=True, algo="fused")
+    assert a.iters == b.iters == 989
+    assert np.array_equal(a.w, b.w)
+    monkeypatch.setenv("PE_ORDER", "0")
+    c = solve(prob, backend="hip", return_w=True, algo="fused")
+    np.testing.assert_allclose(a.w, c.w, rtol=0, atol=1e-10)
+
+
 def test_virtual_ranks_golden_grid(gpu):
     rep = solve(EllipseProblem(1600, 2400), backend="hip-group", ranks=4)
     assert rep.iters == GOLDEN_ITERS[(1600, 2400, "weighted")]
