@@ -166,7 +166,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     PE_HIP_CHECK(hipGetDevice(&dev));
     PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = fused_ ? dev::resident_blocks_S() : dev::resident_blocks_classic(opt_.variant);
+  int per_cu = fused_ ? dev::resident_blocks_S(2) : dev::resident_blocks_classic(opt_.variant);
   if (per_cu <= 0) per_cu = 4;
   int wave_cap = cus * per_cu * dev::kWPB;
   if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
@@ -189,10 +189,18 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.order = (fused_ && big) ? 3 : 0;
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
   if (!fused_ && k.order > 1) k.order = 0;
-  const int per = (k.nitems + wave_cap - 1) / wave_cap;
-  const int waves = (k.nitems + per - 1) / per;
-  k.nblocks = std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
-  const int64_t npart = 8 * std::max<int64_t>(int64_t(k.nblocks), 4096);
+  auto grid_for = [&](int cap) {
+    const int per = (k.nitems + cap - 1) / cap;
+    const int waves = (k.nitems + per - 1) / per;
+    return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
+  };
+  k.nblocks = grid_for(wave_cap);
+  k.nblocks0 = k.nblocks;
+  if (fused_ && !std::getenv("PE_WAVES")) {
+    const int per0 = dev::resident_blocks_S(0);
+    if (per0 > 0) k.nblocks0 = grid_for(cus * per0 * dev::kWPB);
+  }
+  const int64_t npart = 8 * std::max<int64_t>(int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + (fused_ ? 8 * int64_t(k.nitems) : 0))));
   k.partial = partial_;
   k.itemsum = fused_ ? partial_ + npart : nullptr;

@@ -517,9 +517,17 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
   const Scal sc = sweep_scalars(k, st, par);
   const int64_t n = k.nitems, lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
-  for (int64_t i = lo + threadIdx.x; i < hi; i += TJ)
-#pragma unroll
-    for (int q = 0; q < 7; ++q) v[q] += k.itemsum[8 * i + q];
+  for (int64_t i = lo + threadIdx.x; i < hi; i += TJ) {
+    const double4* src = reinterpret_cast<const double4*>(k.itemsum + 8 * i);
+    const double4 a = src[0], b = src[1];
+    v[0] += a.x;
+    v[1] += a.y;
+    v[2] += a.z;
+    v[3] += a.w;
+    v[4] += b.x;
+    v[5] += b.y;
+    v[6] += b.z;
+  }
   block_reduce<7, false>(v, sm);
   if (threadIdx.x == 0)
 #pragma unroll
@@ -615,17 +623,22 @@ static auto with_kS(F&& f) {
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s) {
+  // each variant runs on its own resident grid (the deferring one needs
+  // fewer registers: 3 waves/SIMD instead of 2)
+  const int nb = par == 0 ? k.nblocks0 : k.nblocks;
   auto go = [&](auto kern) {
-    hipLaunchKernelGGL(kern, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
+    hipLaunchKernelGGL(kern, dim3(nb), dim3(TJ), 0, s, k, par);
     return 0;
   };
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(go);
   else with_kS<2>(go);
   if (k.order == 3) {
-    const unsigned rb = unsigned(std::max(1, std::min(64, (k.nitems + 255) / 256)));
-    if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(rb), dim3(TJ), 0, s, k, par);
-    else hipLaunchKernelGGL(kRed<2>, dim3(rb), dim3(TJ), 0, s, k, par);
+    int rb = 16;  // few arrivals on the ticket: the fan-in, not the 2 MB, sets the time
+    if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
+    rb = std::max(1, std::min(rb, (k.nitems + 255) / 256));
+    if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
+    else hipLaunchKernelGGL(kRed<2>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
   }
 }
 
@@ -636,13 +649,13 @@ void launch_wflush(const KParams& k, hipStream_t s) {
   hipLaunchKernelGGL(kWFlushDone, dim3(1), dim3(1), 0, s, k);
 }
 
-int resident_blocks_S() {
+int resident_blocks_S(int wm) {
   auto occ = [](auto kern) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, TJ, 0) != hipSuccess) n = 0;
     return n;
   };
-  return std::min(with_kS<0>(occ), with_kS<2>(occ));
+  return wm == 0 ? with_kS<0>(occ) : with_kS<2>(occ);
 }
 
 void launch_pack(const KParams& k, int b, hipStream_t s) {

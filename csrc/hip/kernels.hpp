@@ -74,6 +74,7 @@ struct KParams {
   int nstrips;                   // 128-column wave strips across ny (+ halo column)
   int nitems;                    // nstrips × ceil(nx / ti)
   int nblocks;                   // persistent grid size of the marching kernels
+  int nblocks0;                  // single-sweep: grid of the deferring (w-free) sweep
   int order;                     // item order: 0 chunk-major (compact active window), 1 strip-major,
                                  // 2 per-XCD chunk ranges, 3 per-XCD dynamic queue (single-sweep)
   int check_tol;                 // 0 → never stop on ‖Δw‖ (fixed-iteration runs)
@@ -119,7 +120,7 @@ void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t 
 int grid_blocks(const KParams& k);
 // Resident 256-thread blocks per CU of the marching kernels (occupancy API;
 // 0 when unavailable).  Sizes the persistent grids.
-int resident_blocks_S();
+int resident_blocks_S(int wm);  // wm 0: deferring sweep, 2: applying sweep
 int resident_blocks_classic(int variant);
 
 }  // namespace dev
