@@ -166,7 +166,19 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     PE_HIP_CHECK(hipGetDevice(&dev));
     PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  int per_cu = fused_ ? dev::resident_blocks_S(2) : dev::resident_blocks_classic(opt_.variant);
+  // rows per item and item order first: they select the sweep kernel variant
+  // whose occupancy sizes the grid
+  const bool big = double(nx) * double(ny) >= double(1 << 24);
+  if (fused_ && ti_env == 0) ti = big ? 16 : 8;  // sweeps: 8192² dynamic 16 rows; ≤ 4096² static 8
+  // Single-sweep item order: the per-XCD dynamic queue (order 3) when the
+  // block is large (8192²: +8 % — boundary-band strips cost more, a static
+  // deal leaves waves idle), static chunk-major otherwise (small blocks: the
+  // queue's pull latency and the extra reduction launch do not pay).
+  k.order = (fused_ && big) ? 3 : 0;
+  if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
+  if (!fused_ && k.order > 1) k.order = 0;
+  k.ti = (fused_ && ti_env < 0) ? 1 << 20 : ti;  // bands mode: long items → general kernel
+  int per_cu = fused_ ? dev::resident_blocks_S(k, 2) : dev::resident_blocks_classic(opt_.variant);
   if (per_cu <= 0) per_cu = 4;
   int wave_cap = cus * per_cu * dev::kWPB;
   if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
@@ -177,18 +189,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const int64_t bands = std::max<int64_t>(1, wave_cap / std::max<int64_t>(1, strips));
     ti = int((nx + bands - 1) / bands);
   }
-  const bool big = double(nx) * double(ny) >= double(1 << 24);
-  if (fused_ && ti_env == 0) ti = big ? 16 : 8;  // sweeps: 8192² dynamic 16 rows; ≤ 4096² static 8
   k.ti = ti;
   k.nstrips = int(strips);
   k.nitems = int(strips * ((nx + ti - 1) / ti));
-  // Single-sweep item order: the per-XCD dynamic queue (order 3) when the
-  // block is large (8192²: +8 % — boundary-band strips cost more, a static
-  // deal leaves waves idle), static chunk-major otherwise (small blocks: the
-  // queue's pull latency and the extra reduction launch do not pay).
-  k.order = (fused_ && big) ? 3 : 0;
-  if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
-  if (!fused_ && k.order > 1) k.order = 0;
   auto grid_for = [&](int cap) {
     const int per = (k.nitems + cap - 1) / cap;
     const int waves = (k.nitems + per - 1) / per;
@@ -197,7 +200,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.nblocks = grid_for(wave_cap);
   k.nblocks0 = k.nblocks;
   if (fused_ && !std::getenv("PE_WAVES")) {
-    const int per0 = dev::resident_blocks_S(0);
+    const int per0 = dev::resident_blocks_S(k, 0);
     if (per0 > 0) k.nblocks0 = grid_for(cus * per0 * dev::kWPB);
   }
   const int64_t npart = 8 * std::max<int64_t>(int64_t(std::max(k.nblocks, k.nblocks0)), 4096);

@@ -613,7 +613,7 @@ static int s_cfg() {
 }
 
 template <int WM, class F>
-static auto with_kS(F&& f) {
+static auto with_kS(const KParams&, F&& f) {
   switch (s_cfg()) {
     case 1: return f(kS<0, 2, false, WM>);
     case 2: return f(kS<0, 3, true, WM>);
@@ -631,8 +631,8 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
     return 0;
   };
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
-  if (par == 0) with_kS<0>(go);
-  else with_kS<2>(go);
+  if (par == 0) with_kS<0>(k, go);
+  else with_kS<2>(k, go);
   if (k.order == 3) {
     int rb = 16;  // few arrivals on the ticket: the fan-in, not the 2 MB, sets the time
     if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
@@ -649,13 +649,13 @@ void launch_wflush(const KParams& k, hipStream_t s) {
   hipLaunchKernelGGL(kWFlushDone, dim3(1), dim3(1), 0, s, k);
 }
 
-int resident_blocks_S(int wm) {
+int resident_blocks_S(const KParams& k, int wm) {
   auto occ = [](auto kern) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, TJ, 0) != hipSuccess) n = 0;
     return n;
   };
-  return wm == 0 ? with_kS<0>(occ) : with_kS<2>(occ);
+  return wm == 0 ? with_kS<0>(k, occ) : with_kS<2>(k, occ);
 }
 
 void launch_pack(const KParams& k, int b, hipStream_t s) {

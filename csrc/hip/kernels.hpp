@@ -120,7 +120,8 @@ void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t 
 int grid_blocks(const KParams& k);
 // Resident 256-thread blocks per CU of the marching kernels (occupancy API;
 // 0 when unavailable).  Sizes the persistent grids.
-int resident_blocks_S(int wm);  // wm 0: deferring sweep, 2: applying sweep
+int resident_blocks_S(const KParams& k, int wm);  // wm 0: deferring sweep, 2: applying sweep
+// (k.ti / k.order select the kernel variant: set them first)
 int resident_blocks_classic(int variant);
 
 }  // namespace dev

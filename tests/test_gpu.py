@@ -290,3 +290,26 @@ def test_two_process_device_path_host_staged(gpu):
     assert len(lines) == 1
     d = json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
+
+
+@pytest.mark.parametrize("nproc,decomp", [(4, "aspect"), (3, "aspect")])
+def test_multi_process_2d_host_staged(gpu, nproc, decomp):
+    """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
+    rows through the x phase of the single-sweep halo) — and 3×1 — match the
+    single-process solution (gathered w)."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host")
+    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}.npy")
+    os.makedirs(os.path.dirname(outp), exist_ok=True)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+           "poisson_ellipse_openmp_mpi_cuda_amd", "--json", "--quiet", "--decomp", decomp, "--dump", outp, "300", "420"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
+    one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
+    assert abs(d["iters"] - one.iters) <= 1
+    w = np.load(outp)
+    np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)

@@ -1,0 +1,10 @@
+set -o pipefail
+cd $GRAFT_REPO_ROOT
+O=$GRAFT_REPO_ROOT/gpurun_out/quick2; mkdir -p $O
+timeout -k 10 60 bin/pe_hip --json --quiet 400 600 > $O/smoke.txt 2>&1 && timeout -k 10 60 bin/pe_hip --json --quiet --vranks 6 700 500 >> $O/smoke.txt 2>&1 || { cat $O/smoke.txt; exit 1; }
+cut -c1-110 $O/smoke.txt
+timeout -k 10 900 python -m pytest tests -m gpu -x -q > $O/pytest.txt 2>&1 || { tail -40 $O/pytest.txt; exit 1; }
+tail -1 $O/pytest.txt
+timeout -k 10 300 python tools/cfg_probe.py PE_ORDER=3 PE_SKERNEL=8 PE_ORDER=3 > $O/cfg.txt 2>&1 || { tail $O/cfg.txt; exit 1; }
+PROBE_GRID=2900 timeout -k 10 300 python tools/cfg_probe.py PE_ORDER=0 PE_SKERNEL=8 PE_ORDER=0,PE_TI=16 PE_ORDER=3,PE_TI=16 >> $O/cfg.txt 2>&1 || { tail $O/cfg.txt; exit 1; }
+grep -v amdgpu.ids $O/cfg.txt
