@@ -46,7 +46,7 @@ int main(int argc, char** argv) {
   const std::string backend = args.get("backend", "serial");
   int ranks = int(args.geti("ranks", 1));
   int threads = int(args.geti("threads", backend == "omp" ? 4 : 1));
-  const DecompMode mode = args.get("decomp", "reference") == "aspect" ? DecompMode::Aspect : DecompMode::Reference;
+  const std::string decomp = args.get("decomp", "reference");
   SolveOptions opt;
   opt.init = args.get("init", "zero") == "random" ? Init::Random : Init::Zero;
   opt.seed = uint64_t(args.geti("seed", 1234));
@@ -62,7 +62,7 @@ int main(int argc, char** argv) {
               << (threads > 1 ? " MPI processes; " : " processes; ") << "M=" << P.M << ", N=" << P.N << std::endl;
   for (int t : sweep) {
     opt.threads = t;
-    SolveResult r = cpu_pcg_threads(P, ranks, mode, opt);
+    SolveResult r = cpu_pcg_threads(P, process_grid_from_spec(decomp, ranks, P.M, P.N), opt);
     if (args.flag("json")) {
       std::printf("{\"M\": %d, \"N\": %d, \"backend\": \"%s\", \"ranks\": %d, \"threads\": %d, \"Px\": %d, \"Py\": %d, "
                   "\"iters\": %lld, \"converged\": %s, \"t_solver\": %.6f, \"t_iterate\": %.6f, \"t_halo\": %.6f, "

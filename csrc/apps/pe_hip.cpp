@@ -80,7 +80,7 @@ int main(int argc, char** argv) {
   opt.use_graph = !args.flag("no-graph");
   opt.timing = args.flag("timing");
   opt.check_tol = !args.flag("no-tol");  // fixed-iteration runs (with --max-iter) for profiling
-  const DecompMode mode = args.get("decomp", "aspect") == "reference" ? DecompMode::Reference : DecompMode::Aspect;
+  const std::string decomp = args.get("decomp", "aspect");
 
   const int rank = env_int("PE_RANK", "RANK", 0);
   const int size = env_int("PE_WORLD_SIZE", "WORLD_SIZE", 1);
@@ -99,11 +99,11 @@ int main(int argc, char** argv) {
 
   SolveResult r;
   if (vranks > 1) {
-    r = device_solve_group(P, vranks, mode, opt);
+    r = device_solve_group(P, process_grid_from_spec(decomp, vranks, P.M, P.N), opt);
   } else {
     std::unique_ptr<DeviceComm> comm;
     if (size > 1) comm = make_rccl_comm(exchange_uid(rank, size), rank, size);
-    const ProcessGrid pg = choose_process_grid(size, P.M, P.N, mode);
+    const ProcessGrid pg = process_grid_from_spec(decomp, size, P.M, P.N);
     const Block blk = decompose(P.M, P.N, pg, rank);
     DeviceSolver solver(P, blk, comm.get(), opt);
     r = solver.solve();

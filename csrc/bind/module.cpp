@@ -71,7 +71,11 @@ PYBIND11_MODULE(_native, m) {
 
   py::enum_<Norm>(m, "Norm").value("Weighted", Norm::Weighted).value("Unweighted", Norm::Unweighted);
   py::enum_<Init>(m, "Init").value("Zero", Init::Zero).value("Random", Init::Random);
-  py::enum_<DecompMode>(m, "DecompMode").value("Reference", DecompMode::Reference).value("Aspect", DecompMode::Aspect);
+  py::enum_<DecompMode>(m, "DecompMode")
+      .value("Reference", DecompMode::Reference)
+      .value("Aspect", DecompMode::Aspect)
+      .value("Rows", DecompMode::Rows)
+      .value("Cols", DecompMode::Cols);
 
   py::class_<Problem>(m, "Problem")
       .def(py::init<>())
@@ -123,6 +127,7 @@ PYBIND11_MODULE(_native, m) {
   m.def("choose_process_grid", &choose_process_grid, py::arg("P"), py::arg("M"), py::arg("N"),
         py::arg("mode") = DecompMode::Aspect);
   m.def("choose_process_grid_reference", &choose_process_grid_reference);
+  m.def("process_grid_from_spec", &process_grid_from_spec, py::arg("spec"), py::arg("P"), py::arg("M"), py::arg("N"));
   m.def("halo_cost", &halo_cost);
   m.def("decompose", &decompose, py::arg("M"), py::arg("N"), py::arg("pg"), py::arg("rank"), py::arg("align") = 8);
 
@@ -177,6 +182,20 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("prob"), py::arg("ranks") = 1, py::arg("mode") = DecompMode::Reference, py::arg("opt") = SolveOptions(),
       py::arg("return_w") = false);
+  m.def(
+      "cpu_solve_grid",
+      [](const Problem& P, const ProcessGrid& pg, const SolveOptions& opt, bool return_w) {
+        std::vector<double> w;
+        SolveResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = cpu_pcg_threads(P, pg, opt, return_w ? &w : nullptr);
+        }
+        py::object wa = py::none();
+        if (return_w) wa = to_array(std::move(w), P.M - 1, P.N - 1);
+        return py::make_tuple(r, wa);
+      },
+      py::arg("prob"), py::arg("grid"), py::arg("opt") = SolveOptions(), py::arg("return_w") = false);
 
   // One rank of a multi-process CPU run; the transport is Python callbacks
   // (torch.distributed, typically gloo).  exchange_fn receives a list of
@@ -359,6 +378,21 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("prob"), py::arg("ranks"), py::arg("mode") = DecompMode::Aspect, py::arg("opt") = SolveOptions(),
       py::arg("return_w") = false);
+
+  m.def(
+      "device_solve_group_grid",
+      [](const Problem& P, const ProcessGrid& pg, const SolveOptions& opt, bool return_w) {
+        std::vector<double> w;
+        SolveResult r;
+        {
+          py::gil_scoped_release nogil;
+          r = device_solve_group(P, pg, opt, return_w ? &w : nullptr);
+        }
+        py::object wa = py::none();
+        if (return_w) wa = to_array(std::move(w), P.M - 1, P.N - 1);
+        return py::make_tuple(r, wa);
+      },
+      py::arg("prob"), py::arg("grid"), py::arg("opt") = SolveOptions(), py::arg("return_w") = false);
 
   // Single-shot device ops for numerics tests: `p` is a full local field
   // (rows × pitch, halo included); returns arrays of the same shape.

@@ -31,6 +31,8 @@ double halo_cost(int M, int N, int Px, int Py) {
 ProcessGrid choose_process_grid(int P, int M, int N, DecompMode mode) {
   if (P < 1) throw std::invalid_argument("process count must be >= 1");
   if (mode == DecompMode::Reference) return choose_process_grid_reference(P);
+  if (mode == DecompMode::Rows) return ProcessGrid{P, 1};
+  if (mode == DecompMode::Cols) return ProcessGrid{1, P};
   ProcessGrid best{P, 1};
   double best_cost = std::numeric_limits<double>::infinity();
   for (int Px = 1; Px <= P; ++Px) {
@@ -44,6 +46,20 @@ ProcessGrid choose_process_grid(int P, int M, int N, DecompMode mode) {
     }
   }
   return best;
+}
+
+ProcessGrid process_grid_from_spec(const std::string& spec, int P, int M, int N) {
+  if (spec == "reference") return choose_process_grid(P, M, N, DecompMode::Reference);
+  if (spec == "aspect") return choose_process_grid(P, M, N, DecompMode::Aspect);
+  if (spec == "rows") return choose_process_grid(P, M, N, DecompMode::Rows);
+  if (spec == "cols") return choose_process_grid(P, M, N, DecompMode::Cols);
+  const auto x = spec.find('x');
+  if (x == std::string::npos || x == 0 || x + 1 >= spec.size())
+    throw std::invalid_argument("decomposition must be reference|aspect|rows|cols|<Px>x<Py>, got '" + spec + "'");
+  ProcessGrid g{std::stoi(spec.substr(0, x)), std::stoi(spec.substr(x + 1))};
+  if (g.Px < 1 || g.Py < 1 || g.Px * g.Py != P)
+    throw std::invalid_argument("process grid " + spec + " does not match " + std::to_string(P) + " ranks");
+  return g;
 }
 
 static void split_1d(int64_t total, int parts, int idx, int64_t& start, int64_t& count) {

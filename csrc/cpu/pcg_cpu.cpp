@@ -345,7 +345,12 @@ SolveResult cpu_pcg(const Problem& P, const Block& blk, HostComm& comm, const So
 
 SolveResult cpu_pcg_threads(const Problem& P, int ranks, DecompMode mode, const SolveOptions& opt,
                             std::vector<double>* w_out) {
-  const ProcessGrid pg = choose_process_grid(ranks, P.M, P.N, mode);
+  return cpu_pcg_threads(P, choose_process_grid(ranks, P.M, P.N, mode), opt, w_out);
+}
+
+SolveResult cpu_pcg_threads(const Problem& P, const ProcessGrid& pg, const SolveOptions& opt,
+                            std::vector<double>* w_out) {
+  const int ranks = pg.Px * pg.Py;
   auto group = make_thread_group(ranks);
   std::vector<SolveResult> results(ranks);
   std::vector<std::vector<double>> blocks(ranks);

@@ -673,8 +673,13 @@ void DeviceSolver::copy_field(int which, double* host) {
 // ---------------------------------------------------------------------------
 SolveResult device_solve_group(const Problem& P, int ranks, DecompMode mode, const SolveOptions& opt,
                                std::vector<double>* w_out) {
+  return device_solve_group(P, choose_process_grid(ranks, P.M, P.N, mode), opt, w_out);
+}
+
+SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const SolveOptions& opt,
+                               std::vector<double>* w_out) {
   const auto t_start = clk::now();
-  const ProcessGrid pg = choose_process_grid(ranks, P.M, P.N, mode);
+  const int ranks = pg.Px * pg.Py;
   std::vector<std::unique_ptr<DeviceSolver>> s;
   std::vector<Block> blks;
   for (int r = 0; r < ranks; ++r) {

@@ -17,7 +17,10 @@
 
 namespace pe {
 
-enum class DecompMode : int { Reference = 0, Aspect = 1 };
+// Reference: the reference's floor(sqrt) rule; Aspect: minimum halo cost;
+// Rows: P×1 (x-direction slabs: one contiguous halo message per side, no
+// strided phase); Cols: 1×P.
+enum class DecompMode : int { Reference = 0, Aspect = 1, Rows = 2, Cols = 3 };
 
 struct ProcessGrid {
   int Px = 1, Py = 1;
@@ -46,6 +49,8 @@ struct Block {
 
 ProcessGrid choose_process_grid(int P, int M, int N, DecompMode mode);
 ProcessGrid choose_process_grid_reference(int P);
+// "reference" | "aspect" | "rows" | "cols" | "<Px>x<Py>" (explicit; Px·Py must equal P).
+ProcessGrid process_grid_from_spec(const std::string& spec, int P, int M, int N);
 
 // `align` = alignment (in elements) of each row's first owned element (lj=1).
 Block decompose(int M, int N, const ProcessGrid& pg, int rank, int align = 8);

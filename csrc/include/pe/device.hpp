@@ -195,5 +195,7 @@ void host_coefficients(const Problem& P, const Block& blk, std::vector<double>& 
 // device-to-device copies + a cross-stream reduction kernel.
 SolveResult device_solve_group(const Problem& prob, int ranks, DecompMode mode, const SolveOptions& opt,
                                std::vector<double>* w_out = nullptr);
+SolveResult device_solve_group(const Problem& prob, const ProcessGrid& pg, const SolveOptions& opt,
+                               std::vector<double>* w_out = nullptr);
 
 }  // namespace pe

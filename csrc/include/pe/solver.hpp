@@ -79,6 +79,8 @@ SolveResult cpu_pcg(const Problem& prob, const Block& blk, HostComm& comm,
 // ((M-1) × (N-1), row-major in i) when non-null.
 SolveResult cpu_pcg_threads(const Problem& prob, int ranks, DecompMode mode,
                             const SolveOptions& opt, std::vector<double>* w_out = nullptr);
+SolveResult cpu_pcg_threads(const Problem& prob, const ProcessGrid& pg, const SolveOptions& opt,
+                            std::vector<double>* w_out = nullptr);
 
 // Legacy-format report lines (reference stdout formats, §2.9 of SURVEY).
 std::string format_result_legacy(const Problem& prob, const SolveResult& r, int nranks,

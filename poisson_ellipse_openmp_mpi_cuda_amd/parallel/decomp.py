@@ -1,36 +1,47 @@
 """2D domain decomposition (Python view of the native implementation).
 
 Reference: choose_process_grid / decompose_2d / neighbour map
-(stage2-mpi/poisson_mpi_decomp.cpp:60-111, :246-252).  ``reference`` mode
-reproduces the reference's Px = floor(sqrt(P))-then-divisor rule; ``aspect``
-mode (default) minimises the per-rank halo cost, preferring contiguous
-x-direction rows over strided y-direction columns (e.g. 8 ranks on 8192² →
-4×2, 2 ranks on 4096² → 2×1, the BASELINE.json configurations).
+(stage2-mpi/poisson_mpi_decomp.cpp:60-111, :246-252).  A decomposition spec
+is one of
+
+* ``reference`` — the reference's Px = floor(sqrt(P))-then-divisor rule,
+* ``aspect`` (default) — minimum per-rank halo cost, preferring contiguous
+  x-direction rows over strided y-direction columns (8 ranks on 8192² →
+  4×2, 2 ranks on 4096² → 2×1, the BASELINE.json configurations),
+* ``rows`` / ``cols`` — P×1 / 1×P slabs,
+* ``"<Px>x<Py>"`` — an explicit grid (``"4x2"``).
 """
 
 from __future__ import annotations
 
 from .._loader import native
 
-MODES = ("aspect", "reference")
+MODES = ("aspect", "reference", "rows", "cols")
 
 
 def mode_enum(mode: str):
     nat = native()
     if mode not in MODES:
         raise ValueError(f"decomposition mode must be one of {MODES}")
-    return nat.DecompMode.Aspect if mode == "aspect" else nat.DecompMode.Reference
+    return {"aspect": nat.DecompMode.Aspect, "reference": nat.DecompMode.Reference, "rows": nat.DecompMode.Rows,
+            "cols": nat.DecompMode.Cols}[mode]
+
+
+def grid(P: int, M: int, N: int, spec: str = "aspect"):
+    """Native ProcessGrid for a decomposition spec (mode name or "PxxPy")."""
+    try:
+        return native().process_grid_from_spec(spec, P, M, N)
+    except Exception as e:  # noqa: BLE001 - surface as ValueError
+        raise ValueError(str(e)) from None
 
 
 def process_grid(P: int, M: int, N: int, mode: str = "aspect"):
-    pg = native().choose_process_grid(P, M, N, mode_enum(mode))
+    pg = grid(P, M, N, mode)
     return pg.Px, pg.Py
 
 
 def block(M: int, N: int, P: int, rank: int, mode: str = "aspect"):
-    nat = native()
-    pg = nat.choose_process_grid(P, M, N, mode_enum(mode))
-    return nat.decompose(M, N, pg, rank)
+    return native().decompose(M, N, grid(P, M, N, mode), rank)
 
 
 def blocks(M: int, N: int, P: int, mode: str = "aspect"):

@@ -112,8 +112,8 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
         t = 1 if backend == "serial" else max(1, threads)
         nranks = ranks if backend == "ranks" else 1
         opt = _options(init, seed, t, keep_history=kw.get("keep_history", False), log_every=kw.get("log_every", 0))
-        res, w = nat.cpu_solve(P, nranks, _decomp.mode_enum(decomp if backend == "ranks" else "reference"), opt,
-                               return_w)
+        res, w = nat.cpu_solve_grid(P, _decomp.grid(nranks, prob.M, prob.N, decomp if backend == "ranks" else "reference"),
+                                    opt, return_w)
         return _report(backend, prob, res, nranks, t, init, None if w is None else np.asarray(w))
     if backend == "torch":
         import torch
@@ -133,7 +133,7 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
         opt = _options(init, seed, chunk=kw.get("chunk", 0), timing=kw.get("timing", False),
                        variant=kw.get("variant", 0), check_tol=kw.get("check_tol", True),
                        algo=kw.get("algo", "auto"))
-        res, w = nat.device_solve_group(P, ranks, _decomp.mode_enum(decomp), opt, return_w)
+        res, w = nat.device_solve_group_grid(P, _decomp.grid(ranks, prob.M, prob.N, decomp), opt, return_w)
         return _report(backend, prob, res, ranks, 1, init, None if w is None else np.asarray(w))
     # distributed backends
     from .parallel import dist as _dist

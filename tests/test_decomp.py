@@ -4,6 +4,8 @@ neighbour symmetry (reference: stage2-mpi/poisson_mpi_decomp.cpp:60-111,
 
 import math
 
+import numpy as np
+
 import pytest
 
 from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
@@ -70,3 +72,27 @@ def test_neighbour_symmetry(P):
                 assert (nb.i0, nb.i1) == (b.i0, b.i1)
         assert (b.nbr[0] < 0) == (b.px == 0) and (b.nbr[1] < 0) == (b.px == b.Px - 1)
         assert (b.nbr[2] < 0) == (b.py == 0) and (b.nbr[3] < 0) == (b.py == b.Py - 1)
+
+
+@pytest.mark.parametrize("spec,P,expect", [("rows", 8, (8, 1)), ("cols", 4, (1, 4)), ("4x2", 8, (4, 2)),
+                                           ("1x1", 1, (1, 1)), ("reference", 8, (2, 4)), ("aspect", 8, (4, 2))])
+def test_grid_specs(spec, P, expect):
+    assert D.process_grid(P, 8192, 8192, spec) == expect
+
+
+@pytest.mark.parametrize("spec,P", [("3x3", 8), ("bogus", 4), ("0x4", 4), ("x2", 2)])
+def test_grid_spec_errors(spec, P):
+    with pytest.raises(ValueError):
+        D.process_grid(P, 100, 100, spec)
+
+
+@pytest.mark.parametrize("spec", ["2x3", "rows", "cols", "1x6"])
+def test_thread_ranks_explicit_grid_matches_serial(spec):
+    from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem, solve
+
+    prob = EllipseProblem(60, 48)
+    a = solve(prob, backend="serial", return_w=True)
+    b = solve(prob, backend="ranks", ranks=6, decomp=spec, return_w=True)
+    assert (b.Px, b.Py) == D.process_grid(6, 60, 48, spec)
+    assert a.iters == b.iters
+    np.testing.assert_allclose(b.w, a.w, rtol=0, atol=1e-12)
