@@ -124,5 +124,10 @@ int main(int argc, char** argv) {
                   r.iters / std::max(1e-12, r.t.iterate), r.l2_err, r.max_err);
     }
   }
+  if (r.nonfinite) {
+    std::fprintf(stderr, "pe_hip: a reduced scalar became NaN/Inf at iteration %lld; solve stopped\n",
+                 (long long)r.iters);
+    return 3;
+  }
   return 0;
 }

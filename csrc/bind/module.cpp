@@ -152,6 +152,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("iters", &SolveResult::iters)
       .def_readonly("converged", &SolveResult::converged)
       .def_readonly("breakdown", &SolveResult::breakdown)
+      .def_readonly("nonfinite", &SolveResult::nonfinite)
       .def_readonly("last_diff", &SolveResult::last_diff)
       .def_readonly("zr", &SolveResult::zr)
       .def_readonly("l2_err", &SolveResult::l2_err)

@@ -239,6 +239,10 @@ SolveResult cpu_pcg(const Problem& P, const Block& blk, HostComm& comm, const So
     comm.allreduce_sum(&den, 1);
     auto t4 = clk::now();
     res.t.reduce += secs(t3, t4);
+    if (!std::isfinite(den) || !std::isfinite(zr_old)) {  // failure detection: NaN/Inf in the reduced scalars
+      res.nonfinite = true;
+      break;
+    }
     if (std::fabs(den) < 1e-15) {
       res.breakdown = true;
       break;

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <thread>
 
 #include "../hip/kernels.hpp"
 #include "pe/device.hpp"
@@ -151,6 +152,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.recv_up = halo_ + 3 * hsize_;
   k.st = st_;
   k.check_tol = opt_.check_tol ? 1 : 0;
+  // Failure-detection hooks: PE_FAULT_INJECT=nan@iter:K poisons
+  // the reduced sums after iteration K (the solver must stop with a
+  // non-finite status), PE_FAULT_INJECT=stall makes the host believe the
+  // device never finishes (the watchdog must fire); PE_WATCHDOG_S sets the
+  // no-progress limit of the host loop.
+  if (const char* e = std::getenv("PE_FAULT_INJECT")) {
+    const std::string f = e;
+    if (f.rfind("nan@iter:", 0) == 0) k.fault_iter = std::atoll(f.c_str() + 9);
+    if (f == "stall") fault_stall_ = true;
+  }
+  if (const char* e = std::getenv("PE_WATCHDOG_S")) watchdog_s_ = std::atof(e);
   // Work decomposition: wave strips (128 columns classic, 124 output
   // columns single-sweep) × `ti`-row chunks, dealt round-robin (chunk-major)
   // to a persistent grid of ~16 waves per CU, so the waves running at any
@@ -465,6 +477,22 @@ void DeviceSolver::enqueue_chunk(int iters) {
   PE_HIP_CHECK(hipGetLastError());
 }
 
+void DeviceSolver::wait_event(hipEvent_t ev) {
+  const auto t0 = clk::now();
+  for (;;) {
+    const hipError_t q = fault_stall_ ? hipErrorNotReady : hipEventQuery(ev);
+    if (q == hipSuccess) return;
+    if (q != hipErrorNotReady) PE_HIP_CHECK(q);
+    comm_->check_async();
+    if (watchdog_s_ > 0 && secs(t0, clk::now()) > watchdog_s_) {
+      comm_->abort();
+      throw std::runtime_error("watchdog: device made no progress for " + std::to_string(watchdog_s_) +
+                               " s (communicator aborted)");
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(20));
+  }
+}
+
 void DeviceSolver::enqueue_wflush() {
   if (fused_) dev::launch_wflush(*kp_, stream_);
 }
@@ -594,7 +622,7 @@ SolveResult DeviceSolver::solve() {
       if (inflight.empty()) break;
       const int s = inflight.front();
       inflight.pop_front();
-      PE_HIP_CHECK(hipEventSynchronize(ev_[s]));
+      wait_event(ev_[s]);
       if (hst_[s].done) stop = true;
     }
   }
@@ -616,6 +644,7 @@ SolveResult DeviceSolver::solve() {
   res.iters = hs.iter;
   res.converged = hs.status == 1;
   res.breakdown = hs.status == 2;
+  res.nonfinite = hs.status == 4;
   res.last_diff = hs.last_diff;
   res.zr = hs.rz_cur;
   if (opt_.compute_error) {
@@ -798,6 +827,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   res.iters = hs.iter;
   res.converged = hs.status == 1;
   res.breakdown = hs.status == 2;
+  res.nonfinite = hs.status == 4;
   res.last_diff = hs.last_diff;
   res.zr = hs.rz_cur;
   if (opt.compute_error) {

@@ -145,6 +145,7 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
                                                const double (&t)[7]) {
 #pragma unroll
   for (int n = 0; n < 7; ++n) st->fs[par][n] = t[n];
+  if (k.fault_iter > 0 && c.kiter == k.fault_iter) st->fs[par][1] = __builtin_nan("");  // PE_FAULT_INJECT=nan@iter:K
   st->wpend = WM == 0 ? 1 : 0;
   st->wpar = par;
   if (c.first) {
@@ -194,10 +195,11 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   const long long kiter = sc.kiter;
   const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
   if (!first) {
-    if (fabs(sc.den) < 1e-15) {  // breakdown: stop before this sweep's w term (reference :413)
-      if (WM == 2 && st->wpend) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
+    const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
+    if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
+      if (WM == 2 && st->wpend && !bad) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->status = 2;
+        st->status = bad ? 4 : 2;
         st->iter = kiter;
         st->done = 1;
         st->wpend = 0;

@@ -243,9 +243,10 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
 
   const double den = (st->red_F[0] * k.h1) * k.h2;
   const long long kiter = st->iter + 1;
-  if (fabs(den) < 1e-15) {  // breakdown: stop before touching w (reference :413)
+  const bool bad = !isfinite(den) || !isfinite(st->rz_cur);
+  if (bad || fabs(den) < 1e-15) {  // breakdown / non-finite: stop before touching w (reference :413)
     if (blockIdx.x == 0 && threadIdx.x == 0) {
-      st->status = 2;
+      st->status = bad ? 4 : 2;
       st->iter = kiter;
       st->done = 1;
     }
@@ -369,6 +370,7 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
     reduce_partials<1>(k.partial, gridDim.x, t, sm);
     if (threadIdx.x == 0) {
       st->red_G[0] = t[0];
+      if (k.fault_iter > 0 && kiter == k.fault_iter) st->rz_cur = __builtin_nan("");  // fault injection
       st->alpha = alpha;
       st->last_diff = diff;
       st->iter = kiter;

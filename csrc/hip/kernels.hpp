@@ -34,7 +34,7 @@ struct DevState {
   double alpha, beta, last_diff;
   long long iter;    // completed iterations
   int done;          // 1 → every later kernel is a no-op
-  int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap
+  int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap, 4 non-finite scalars
   unsigned ticket[4];
   unsigned pad[4];
   // Single-sweep (fused) PCG: the 7 local/global sums of sweep k live in
@@ -90,6 +90,7 @@ struct KParams {
   int64_t poff;
   double* x[2];
   double* itemsum;               // dynamic single-sweep: per-item sums [nitems][8]
+  long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)

@@ -81,6 +81,19 @@ class RcclComm final : public DeviceComm {
   }
   bool capturable() const override { return std::getenv("PE_RCCL_GRAPH") != nullptr; }
   std::string name() const override { return "rccl"; }
+  void check_async() override {
+    if (!comm_) return;
+    ncclResult_t r = ncclSuccess;
+    if (ncclCommGetAsyncError(comm_, &r) != ncclSuccess || (r != ncclSuccess && r != ncclInProgress)) {
+      const std::string msg = std::string("RCCL asynchronous error: ") + ncclGetErrorString(r);
+      abort();
+      throw std::runtime_error(msg);
+    }
+  }
+  void abort() override {
+    if (comm_) (void)ncclCommAbort(comm_);
+    comm_ = nullptr;
+  }
 
  private:
   ncclComm_t comm_;

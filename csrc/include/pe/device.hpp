@@ -41,6 +41,10 @@ class DeviceComm {
   virtual void barrier(hipStream_t s) = 0;
   virtual bool capturable() const { return false; }
   virtual std::string name() const = 0;
+  // Failure detection: poll asynchronous transport errors (throws), and
+  // abort the communicator so peers blocked in it fail instead of hanging.
+  virtual void check_async() {}
+  virtual void abort() {}
 };
 
 class SelfDeviceComm final : public DeviceComm {
@@ -141,6 +145,7 @@ class DeviceSolver {
   void choose_placement();
   void enqueue_iteration(int par);
   void enqueue_exchange(int buf);
+  void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
   void enqueue_chunk(int iters);
   bool graph_ready(int iters);
 
@@ -168,6 +173,8 @@ class DeviceSolver {
   int graph_iters_ = 0;
   int chunk_ = 16;
   int par_ = 0;  // parity of the next iteration (x / p ping-pong)
+  double watchdog_s_ = 0;   // PE_WATCHDOG_S: abort if a chunk makes no progress this long (0 = off)
+  bool fault_stall_ = false;  // PE_FAULT_INJECT=stall: pretend the device never finishes (watchdog test)
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
 };

@@ -57,6 +57,7 @@ struct SolveResult {
   int64_t iters = 0;
   bool converged = false;
   bool breakdown = false;
+  bool nonfinite = false;  // a reduced scalar became NaN/Inf (device status 4)
   double last_diff = 0;  // ‖w^{k+1}-w^k‖ at the last iteration
   double zr = 0;         // final (z, r)
   Timers t;

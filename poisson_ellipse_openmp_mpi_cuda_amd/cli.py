@@ -77,6 +77,9 @@ def main(argv=None) -> int:
         if a.pgm:
             _dump.write_pgm(a.pgm, rep.w)
     sys.stdout.flush()
+    if rep.nonfinite:
+        print("error: a reduced scalar became NaN/Inf; solve stopped", file=sys.stderr)
+        return 3
     return 0
 
 

@@ -53,6 +53,7 @@ class SolveReport:
     w: Optional[np.ndarray] = None
     rank: int = 0
     algo: str = ""
+    nonfinite: bool = False
 
     @property
     def iters_per_s(self) -> float:
@@ -93,7 +94,7 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         iters=int(res.iters), converged=bool(res.converged), breakdown=bool(res.breakdown),
         last_diff=float(res.last_diff), timers=dict(res.timers), l2_err=float(res.l2_err),
         max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank,
-        algo=str(getattr(res, "algo", "")))
+        algo=str(getattr(res, "algo", "")), nonfinite=bool(getattr(res, "nonfinite", False)))
 
 
 def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str = "aspect",

@@ -63,3 +63,10 @@ def test_general_ellipse_family_analytic_error():
     prob = EllipseProblem(128, 128, A2=-1.0, B2=1.0, cy=1.0)
     rep = solve(prob, backend="omp", threads=4)
     assert rep.converged and rep.l2_err < 1e-2
+
+
+def test_cpu_nonfinite_detected():
+    from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem, solve
+
+    rep = solve(EllipseProblem(40, 40, F=float("nan")), backend="serial")
+    assert rep.nonfinite and not rep.converged and rep.iters <= 1

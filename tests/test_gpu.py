@@ -46,7 +46,7 @@ def test_device_solution_matches_cpu_oracle(gpu, M, N):
 
 
 @pytest.mark.parametrize("ranks,decomp", [(2, "aspect"), (3, "aspect"), (4, "aspect"), (6, "aspect"),
-                                          (8, "reference"), (5, "aspect")])
+                                          (8, "reference"), (5, "aspect"), (4, "rows"), (6, "2x3"), (3, "cols")])
 @pytest.mark.parametrize("algo", ["fused", "classic"])
 def test_virtual_ranks_match_single(gpu, ranks, decomp, algo):
     prob = EllipseProblem(300, 420)
@@ -313,3 +313,18 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp):
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
     np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("algo", ["fused", "classic"])
+def test_fault_injection_nan_stops_cleanly(gpu, algo, monkeypatch):
+    monkeypatch.setenv("PE_FAULT_INJECT", "nan@iter:20")
+    rep = solve(EllipseProblem(400, 600), backend="hip", algo=algo)
+    assert rep.nonfinite and not rep.converged
+    assert 20 <= rep.iters <= 23
+
+
+def test_watchdog_fires_on_stall(gpu, monkeypatch):
+    monkeypatch.setenv("PE_FAULT_INJECT", "stall")
+    monkeypatch.setenv("PE_WATCHDOG_S", "0.5")
+    with pytest.raises(RuntimeError, match="watchdog"):
+        solve(EllipseProblem(200, 300), backend="hip")
