@@ -80,6 +80,9 @@ int main(int argc, char** argv) {
   opt.use_graph = !args.flag("no-graph");
   opt.timing = args.flag("timing");
   opt.check_tol = !args.flag("no-tol");  // fixed-iteration runs (with --max-iter) for profiling
+  opt.checkpoint_path = args.get("checkpoint", "");
+  opt.checkpoint_every = args.geti("checkpoint-every", 0);
+  opt.resume_path = args.get("resume", "");
   const std::string decomp = args.get("decomp", "aspect");
 
   const int rank = env_int("PE_RANK", "RANK", 0);

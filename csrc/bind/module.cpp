@@ -146,7 +146,10 @@ PYBIND11_MODULE(_native, m) {
       .def_readwrite("timing", &SolveOptions::timing)
       .def_readwrite("check_tol", &SolveOptions::check_tol)
       .def_readwrite("variant", &SolveOptions::variant)
-      .def_readwrite("algo", &SolveOptions::algo);
+      .def_readwrite("algo", &SolveOptions::algo)
+      .def_readwrite("checkpoint_every", &SolveOptions::checkpoint_every)
+      .def_readwrite("checkpoint_path", &SolveOptions::checkpoint_path)
+      .def_readwrite("resume_path", &SolveOptions::resume_path);
 
   py::class_<SolveResult>(m, "SolveResult")
       .def_readonly("iters", &SolveResult::iters)
@@ -358,6 +361,8 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
+      .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
+      .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)
       .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })

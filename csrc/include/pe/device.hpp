@@ -126,6 +126,11 @@ class DeviceSolver {
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   hipStream_t stream() const { return stream_; }
 
+  // Checkpoint / resume of the full device state of this rank (raw fields,
+  // halo buffers, scalar block, iteration parity).  Synchronizes the stream.
+  void save_checkpoint(const std::string& path);
+  void load_checkpoint(const std::string& path);
+
   // State / data access.
   void read_state(dev::DevState* out);
   void copy_w(double* host, bool owned_only = true);  // nx × ny row-major

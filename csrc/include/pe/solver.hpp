@@ -51,6 +51,13 @@ struct SolveOptions {
   // allow it), 1 classic two-kernel iteration (reference recurrence, 2
   // reductions), 2 single-sweep (fused.hip: 1 kernel, 1 reduction).
   int algo = 0;
+  // Checkpoint / resume (device solver): every `checkpoint_every` iterations
+  // (at the next chunk boundary) each rank writes `<checkpoint_path>.r<rank>`
+  // (raw device state: fields, halo buffers, scalar block); `resume_path`
+  // continues a solve from such files bitwise-identically.
+  int64_t checkpoint_every = 0;
+  std::string checkpoint_path;
+  std::string resume_path;
 };
 
 struct SolveResult {

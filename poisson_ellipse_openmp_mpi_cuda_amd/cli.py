@@ -43,6 +43,9 @@ def build_parser():
     ap.add_argument("--algo", choices=("auto", "classic", "fused"), default="auto",
                     help="device iteration: fused single-sweep (1 kernel, 1 reduction) or classic (2 + 2)")
     ap.add_argument("--timing", action="store_true", help="per-phase device event timers")
+    ap.add_argument("--checkpoint", default=None, help="hip: checkpoint file prefix (one file per rank: PREFIX.r<rank>)")
+    ap.add_argument("--checkpoint-every", type=int, default=0, help="hip: iterations between checkpoints")
+    ap.add_argument("--resume", default=None, help="hip: resume from checkpoint prefix")
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--quiet", action="store_true", help="suppress the legacy lines")
@@ -62,7 +65,7 @@ def main(argv=None) -> int:
     want_w = bool(a.dump or a.pgm)
     rep = solve(prob, backend=a.backend, ranks=a.ranks, threads=a.threads, decomp=a.decomp, init=a.init,
                 seed=a.seed, return_w=want_w, variant=a.variant, timing=a.timing, graph=not a.no_graph,
-                algo=a.algo)
+                algo=a.algo, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every, resume=a.resume)
     if rep.rank != 0:
         return 0
     if not a.quiet:

@@ -71,7 +71,7 @@ ALGOS = {"auto": 0, "classic": 1, "fused": 2}
 
 
 def _options(init="zero", seed=1234, threads=1, chunk=0, graph=True, timing=False, check_tol=True, variant=0,
-             keep_history=False, log_every=0, algo="auto"):
+             keep_history=False, log_every=0, algo="auto", checkpoint_every=0, checkpoint=None, resume=None):
     nat = native()
     o = nat.SolveOptions()
     o.init = nat.Init.Random if init == "random" else nat.Init.Zero
@@ -84,6 +84,9 @@ def _options(init="zero", seed=1234, threads=1, chunk=0, graph=True, timing=Fals
     o.variant = int(variant)
     o.algo = ALGOS[algo] if isinstance(algo, str) else int(algo)
     o.keep_history = bool(keep_history)
+    o.checkpoint_every = int(checkpoint_every)
+    o.checkpoint_path = str(checkpoint or "")
+    o.resume_path = str(resume or "")
     o.log_every = int(log_every)
     return o
 
@@ -156,7 +159,9 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     else:
         world = _dist.env_rank_world()[1]
     opt = _options(init, seed, chunk=kw.get("chunk", 0), graph=kw.get("graph", True), timing=kw.get("timing", False),
-                   check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0), algo=kw.get("algo", "auto"))
+                   check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0), algo=kw.get("algo", "auto"),
+                   checkpoint_every=kw.get("checkpoint_every", 0), checkpoint=kw.get("checkpoint"),
+                   resume=kw.get("resume"))
     if world == 1:
         rank, comm = 0, None
         nat.set_device(0)

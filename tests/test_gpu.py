@@ -328,3 +328,21 @@ def test_watchdog_fires_on_stall(gpu, monkeypatch):
     monkeypatch.setenv("PE_WATCHDOG_S", "0.5")
     with pytest.raises(RuntimeError, match="watchdog"):
         solve(EllipseProblem(200, 300), backend="hip")
+
+
+@pytest.mark.parametrize("algo", ["fused", "classic"])
+def test_checkpoint_resume_bitwise(gpu, algo, tmp_path):
+    prob = EllipseProblem(400, 600)
+    ck = str(tmp_path / "ck")
+    full = solve(prob, backend="hip", return_w=True, algo=algo, checkpoint=ck, checkpoint_every=200, chunk=8)
+    assert full.iters == 546 and os.path.exists(ck + ".r0")
+    res = solve(prob, backend="hip", return_w=True, algo=algo, resume=ck, chunk=8)
+    assert res.converged and res.iters == full.iters
+    assert np.array_equal(res.w, full.w)
+
+
+def test_resume_rejects_mismatch(gpu, tmp_path):
+    ck = str(tmp_path / "ck")
+    solve(EllipseProblem(200, 300), backend="hip", checkpoint=ck, checkpoint_every=50, chunk=8)
+    with pytest.raises(RuntimeError, match="does not match"):
+        solve(EllipseProblem(210, 300), backend="hip", resume=ck)
