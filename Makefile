@@ -23,7 +23,7 @@ CXXFLAGS  += $(COMMON) -fopenmp -D__HIP_PLATFORM_AMD__ -I$(ROCM)/include
 # ROCm 7.0 runtime bundled with PyTorch.
 HIPFLAGS  += $(COMMON) --offload-arch=$(ARCH) -ffp-contract=off -mcode-object-version=5 \
              -fno-gpu-rdc -munsafe-fp-atomics
-LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lgomp -lpthread -Wl,-rpath,$(ROCM)/lib
+LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lgomp -lpthread -Wl,-rpath,$(ROCM)/lib
 
 CORE_SRC  := csrc/core/decomp.cpp csrc/core/thread_comm.cpp csrc/core/report.cpp csrc/cpu/pcg_cpu.cpp
 HOST_SRC  := csrc/hip/device_solver.cpp csrc/hip/rccl_comm.cpp csrc/hip/runtime.cpp csrc/core/row_classes.cpp
@@ -38,7 +38,7 @@ HEADERS   := $(wildcard csrc/include/pe/*.hpp) $(wildcard csrc/hip/*.hpp) csrc/a
 
 EXT       := $(PKG)/_native$(EXT_SUF)
 
-.PHONY: all cpu clean
+.PHONY: all cpu clean asan tsan
 all: $(EXT) $(BIN)/pe_hip $(BIN)/pe_cpu $(BIN)/pe_launch
 cpu: $(BIN)/pe_cpu
 
@@ -68,6 +68,21 @@ $(BIN)/pe_hip: $(BUILD)/apps/pe_hip.o $(CORE_OBJ) $(HOST_OBJ) $(HIP_OBJ)
 $(BIN)/pe_launch: $(BUILD)/apps/pe_launch.o
 	@mkdir -p $(BIN)
 	$(CXX) -o $@ $^ -lpthread
+
+# Host sanitizer builds of the CPU solver (the GPU pool has no device
+# ASan / XNACK): AddressSanitizer + UBSan, and ThreadSanitizer for the
+# thread-rank transport (run with --threads 1: libgomp is not TSan-built).
+SAN_SRC   := $(CORE_SRC) csrc/apps/pe_cpu.cpp
+asan: $(BIN)/pe_cpu_asan
+tsan: $(BIN)/pe_cpu_tsan
+$(BIN)/pe_cpu_asan: $(SAN_SRC) $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) -O1 -g -std=c++17 -Wall -Wno-unknown-pragmas -Icsrc/include -fopenmp -fno-omit-frame-pointer \
+	  -fsanitize=address,undefined -fno-sanitize-recover=undefined $(SAN_SRC) -o $@ -lpthread
+$(BIN)/pe_cpu_tsan: $(SAN_SRC) $(HEADERS)
+	@mkdir -p $(BIN)
+	$(CXX) -O1 -g -std=c++17 -Wall -Wno-unknown-pragmas -Icsrc/include -fopenmp -fsanitize=thread $(SAN_SRC) \
+	  -o $@ -lpthread
 
 clean:
 	rm -rf $(BUILD) $(BIN) $(EXT)

@@ -83,6 +83,7 @@ int main(int argc, char** argv) {
   opt.checkpoint_path = args.get("checkpoint", "");
   opt.checkpoint_every = args.geti("checkpoint-every", 0);
   opt.resume_path = args.get("resume", "");
+  opt.log_every = int(args.geti("log-every", 0));
   const std::string decomp = args.get("decomp", "aspect");
 
   const int rank = env_int("PE_RANK", "RANK", 0);

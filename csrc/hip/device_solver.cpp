@@ -22,6 +22,8 @@
 #include <limits>
 #include <thread>
 
+#include <rocprofiler-sdk-roctx/roctx.h>
+
 #include "../hip/kernels.hpp"
 #include "pe/device.hpp"
 
@@ -31,6 +33,11 @@ using dev::DevState;
 using dev::KParams;
 
 namespace {
+// Host-side phase ranges for rocprofv3 --marker-trace (no-ops without a tool).
+struct Range {
+  explicit Range(const char* n) { roctxRangePushA(n); }
+  ~Range() { roctxRangePop(); }
+};
 using clk = std::chrono::steady_clock;
 double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 }  // namespace
@@ -164,6 +171,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     if (f == "stall") fault_stall_ = true;
   }
   if (const char* e = std::getenv("PE_WATCHDOG_S")) watchdog_s_ = std::atof(e);
+  if (opt_.keep_history) {  // per-iteration ‖Δw‖ on the device (capped at 2²⁴ iterations)
+    k.hist_n = std::min<long long>(prob_.iter_cap(), 1LL << 24);
+    PE_HIP_CHECK(hipMalloc(&hist_, sizeof(double) * size_t(std::max<long long>(1, k.hist_n))));
+    k.hist = hist_;
+  }
   // Work decomposition: wave strips (128 columns classic, 124 output
   // columns single-sweep) × `ti`-row chunks, dealt round-robin (chunk-major)
   // to a persistent grid of ~16 waves per CU, so the waves running at any
@@ -262,6 +274,7 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
 // time a few local sweeps on real data (no communication) and keep the
 // fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
 void DeviceSolver::choose_placement() {
+  Range range("pe.placement_search");
   const double pts = double(blk_.nx) * double(blk_.ny);
   int tries = pts >= double(1 << 22) ? 8 : 1;
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
@@ -347,6 +360,7 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(rowcls_);
   (void)hipFree(halo_);
   (void)hipFree(partial_);
+  if (hist_) (void)hipFree(hist_);
   (void)hipFree(st_);
   (void)hipHostFree(hst_);
   (void)hipStreamDestroy(stream_);
@@ -495,6 +509,7 @@ void ck_io(FILE* f, void* host, size_t n, bool write, const std::string& path) {
 }  // namespace
 
 void DeviceSolver::save_checkpoint(const std::string& path) {
+  Range range("pe.checkpoint");
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
   std::vector<std::pair<void*, size_t>> bufs;
   if (fused_) {
@@ -645,6 +660,7 @@ double DeviceSolver::time_iterations(int64_t iters, bool use_graph) {
 }
 
 SolveResult DeviceSolver::solve() {
+  Range range("pe.solve");
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
@@ -668,6 +684,7 @@ SolveResult DeviceSolver::solve() {
 
   const int64_t cap = prob_.iter_cap();
   const auto t_loop = clk::now();
+  roctxRangePushA("pe.iterate");
   PE_HIP_CHECK(hipEventRecord(t0_, stream_));
   if (opt_.timing) {
     // Eager, per-phase event timing (host sync per chunk; diagnostic mode).
@@ -720,6 +737,7 @@ SolveResult DeviceSolver::solve() {
   } else {
     int64_t enq = start_iter;
     int64_t next_ck = ck_every > 0 ? (start_iter / ck_every + 1) * ck_every : std::numeric_limits<int64_t>::max();
+    int64_t next_log = opt_.log_every > 0 ? opt_.log_every : 0;
     int slot = 0;
     std::deque<int> inflight;
     bool stop = false;
@@ -744,6 +762,11 @@ SolveResult DeviceSolver::solve() {
       inflight.pop_front();
       wait_event(ev_[s]);
       if (hst_[s].done) stop = true;
+      if (opt_.log_every > 0 && blk_.rank == 0 && hst_[s].iter >= next_log) {  // chunk-granular progress log
+        std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[s].iter,
+                     hst_[s].last_diff, hst_[s].rz_cur);
+        while (next_log <= hst_[s].iter) next_log += opt_.log_every;
+      }
     }
   }
   PE_HIP_CHECK(hipEventRecord(t1_, stream_));
@@ -751,6 +774,7 @@ SolveResult DeviceSolver::solve() {
   float ms = 0;
   PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
   res.t.iterate = secs(t_loop, clk::now());
+  roctxRangePop();
   if (!opt_.timing) res.t.gpu = ms * 1e-3;
 
   DevState hs;
@@ -766,6 +790,10 @@ SolveResult DeviceSolver::solve() {
   res.breakdown = hs.status == 2;
   res.nonfinite = hs.status == 4;
   res.last_diff = hs.last_diff;
+  if (hist_ && hs.iter > 0) {
+    res.history.resize(size_t(std::min<long long>(hs.iter, kp_->hist_n)));
+    PE_HIP_CHECK(hipMemcpy(res.history.data(), hist_, sizeof(double) * res.history.size(), hipMemcpyDeviceToHost));
+  }
   res.zr = hs.rz_cur;
   if (opt_.compute_error) {
     res.l2_err = std::sqrt(hs.err[0] * prob_.h1() * prob_.h2());

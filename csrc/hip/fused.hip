@@ -156,6 +156,7 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
     st->alpha = c.alpha;
     st->beta = c.beta;
     st->last_diff = c.diff;
+    if (k.hist && c.kiter <= k.hist_n) k.hist[c.kiter - 1] = c.diff;
     st->iter = c.kiter;
     if (k.check_tol && c.diff < k.tol) {
       st->status = 1;
@@ -216,6 +217,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         st->alpha = alpha;
         st->beta = beta;
         st->last_diff = diff;
+        if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = diff;
         st->iter = kiter;
         st->status = conv ? 1 : 3;
         st->done = 1;

@@ -373,6 +373,7 @@ __global__ __launch_bounds__(TJ) void kG(KParams k, int par) {
       if (k.fault_iter > 0 && kiter == k.fault_iter) st->rz_cur = __builtin_nan("");  // fault injection
       st->alpha = alpha;
       st->last_diff = diff;
+      if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = diff;
       st->iter = kiter;
       if (k.check_tol && diff < k.tol) {
         st->status = 1;

@@ -91,6 +91,8 @@ struct KParams {
   double* x[2];
   double* itemsum;               // dynamic single-sweep: per-item sums [nitems][8]
   long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
+  double* hist;                  // keep_history: ‖Δw‖ of iteration k at hist[k-1] (k ≤ hist_n)
+  long long hist_n;
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)

@@ -171,6 +171,7 @@ class DeviceSolver {
   double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each; ×4 single-sweep)
   int64_t hsize_ = 0;
   double* partial_ = nullptr;
+  double* hist_ = nullptr;
   dev::DevState* st_ = nullptr;
   dev::DevState* hst_ = nullptr;  // pinned, 2 slots
   std::unique_ptr<dev::KParams> kp_;

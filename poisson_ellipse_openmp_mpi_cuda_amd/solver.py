@@ -54,6 +54,7 @@ class SolveReport:
     rank: int = 0
     algo: str = ""
     nonfinite: bool = False
+    history: Optional[list] = None  # ‖Δw‖ per iteration (keep_history=True)
 
     @property
     def iters_per_s(self) -> float:
@@ -97,7 +98,8 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         iters=int(res.iters), converged=bool(res.converged), breakdown=bool(res.breakdown),
         last_diff=float(res.last_diff), timers=dict(res.timers), l2_err=float(res.l2_err),
         max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank,
-        algo=str(getattr(res, "algo", "")), nonfinite=bool(getattr(res, "nonfinite", False)))
+        algo=str(getattr(res, "algo", "")), nonfinite=bool(getattr(res, "nonfinite", False)),
+        history=list(res.history) if len(res.history) else None)
 
 
 def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str = "aspect",
@@ -161,7 +163,8 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     opt = _options(init, seed, chunk=kw.get("chunk", 0), graph=kw.get("graph", True), timing=kw.get("timing", False),
                    check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0), algo=kw.get("algo", "auto"),
                    checkpoint_every=kw.get("checkpoint_every", 0), checkpoint=kw.get("checkpoint"),
-                   resume=kw.get("resume"))
+                   resume=kw.get("resume"), keep_history=kw.get("keep_history", False),
+                   log_every=kw.get("log_every", 0))
     if world == 1:
         rank, comm = 0, None
         nat.set_device(0)

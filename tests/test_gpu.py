@@ -346,3 +346,13 @@ def test_resume_rejects_mismatch(gpu, tmp_path):
     solve(EllipseProblem(200, 300), backend="hip", checkpoint=ck, checkpoint_every=50, chunk=8)
     with pytest.raises(RuntimeError, match="does not match"):
         solve(EllipseProblem(210, 300), backend="hip", resume=ck)
+
+
+@pytest.mark.parametrize("algo", ["fused", "classic"])
+def test_device_history_matches_cpu(gpu, algo):
+    prob = EllipseProblem(200, 300)
+    c = solve(prob, backend="serial", keep_history=True)
+    d = solve(prob, backend="hip", keep_history=True, algo=algo)
+    assert len(d.history) == d.iters == c.iters
+    np.testing.assert_allclose(d.history, c.history, rtol=1e-6)
+    assert d.history[-1] < prob.tol <= d.history[-2]
