@@ -361,6 +361,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
+      .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)

@@ -240,6 +240,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
   if (fused_) choose_placement();
+  setup_overlap();
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -261,6 +262,41 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
   k.r = k.x[0];
   k.p[0] = k.x[0] + plane_;
   k.p[1] = k.x[1] + plane_;
+}
+
+// Halo/interior overlap (multi-rank single-sweep): the items whose outputs
+// are sent to a neighbour (first / last two owned rows and columns) run in a
+// small launch on a high-priority stream; the exchange starts as soon as
+// that launch is done, while the interior items run on the solver stream.
+// PE_OVERLAP=0 disables.
+void DeviceSolver::setup_overlap() {
+  const KParams& k = *kp_;
+  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
+  const char* e = std::getenv("PE_OVERLAP");
+  overlap_ = fused_ && comm_->size() > 1 && nb && !(e && std::atoi(e) == 0);
+  if (!overlap_) return;
+  std::vector<int> b, in;
+  const int64_t nchunks = (blk_.nx + k.ti - 1) / k.ti;
+  for (int64_t ch = 0; ch < nchunks; ++ch)
+    for (int s = 0; s < k.nstrips; ++s) {
+      const int64_t ib = 1 + ch * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+      const int64_t J = -1 + int64_t(s) * dev::kFSW;
+      const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
+      const bool bnd = (blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
+                       (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1);
+      (bnd ? b : in).push_back(int(ch * k.nstrips + s));
+    }
+  nlist_b_ = int(b.size());
+  nlist_i_ = int(in.size());
+  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int) * std::max<size_t>(1, b.size() + in.size())));
+  if (!b.empty()) PE_HIP_CHECK(hipMemcpy(ilist_, b.data(), sizeof(int) * b.size(), hipMemcpyHostToDevice));
+  if (!in.empty())
+    PE_HIP_CHECK(hipMemcpy(ilist_ + b.size(), in.data(), sizeof(int) * in.size(), hipMemcpyHostToDevice));
+  int least = 0, greatest = 0;
+  PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));
+  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_start_, hipEventDisableTiming));
+  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
 }
 
 // Memory-placement autotune (single-sweep, large blocks).  The same sweep
@@ -361,6 +397,10 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(halo_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
+  if (ilist_) (void)hipFree(ilist_);
+  if (hs_) (void)hipStreamDestroy(hs_);
+  if (ev_start_) (void)hipEventDestroy(ev_start_);
+  if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   (void)hipFree(st_);
   (void)hipHostFree(hst_);
   (void)hipStreamDestroy(stream_);
@@ -445,6 +485,29 @@ void DeviceSolver::enqueue_unpack(int buf) { dev::launch_unpack(*kp_, buf, strea
 void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 
 void DeviceSolver::enqueue_iteration(int par) {
+  if (fused_ && overlap_) {
+    KParams kb = *kp_, ki = *kp_;
+    kb.ilist = ilist_;
+    kb.nilist = nlist_b_;
+    kb.list_role = 1;
+    kb.nblocks = kb.nblocks0 = std::max(1, std::min(kp_->nblocks, (nlist_b_ + dev::kWPB - 1) / dev::kWPB));
+    ki.ilist = ilist_ + nlist_b_;
+    ki.nilist = nlist_i_;
+    ki.list_role = 2;
+    PE_HIP_CHECK(hipEventRecord(ev_start_, stream_));
+    PE_HIP_CHECK(hipStreamWaitEvent(hs_, ev_start_, 0));
+    dev::launch_S(kb, par, hs_);  // boundary items first, on the high-priority stream
+    for (const HaloPhase& ph : halo_phases(par)) {
+      comm_->exchange(ph.ex, hs_);
+      if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
+    }
+    PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
+    dev::launch_S(ki, par, stream_);  // interior items, overlapping the exchange
+    PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
+    dev::launch_red(*kp_, par, stream_);
+    comm_->allreduce_sum(st_->fs[par], 7, stream_);
+    return;
+  }
   if (fused_) {
     dev::launch_S(*kp_, par, stream_);
     enqueue_exchange(par);

@@ -197,6 +197,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
   if (!first) {
     const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
+    const bool last = bad || fabs(sc.den) < 1e-15 || (WM == 0 && ((k.check_tol && diff < k.tol) || kiter >= k.max_iter));
+    if (last && k.list_role == 2) return;  // the boundary launch of this sweep handles it
     if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
       if (WM == 2 && st->wpend && !bad) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -267,7 +269,18 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     ilimit = k.nitems;
     chunk0 = 0;
   }
-  const bool dyn = k.order == 3;
+  // Explicit item list (halo/interior overlap): a static walk over it, item
+  // sums per item like the dynamic queue (the reduction kernel adds both
+  // launches' items in item order).
+  const bool listed = k.ilist != nullptr;
+  if (listed) {
+    it0 = blockIdx.x * kWPB + wid;
+    istride = gridDim.x * kWPB;
+    ilimit = k.nilist;
+    chunk0 = 0;
+  }
+  const bool dyn = k.order == 3 && !listed;
+  const bool persum = dyn || listed;
   auto pull = [&]() -> int {
     unsigned v = 0;
     if (lane == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -277,8 +290,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   while (item < ilimit) {
     unsigned nxt_v = 0;  // next item, requested now, read after this one
     if (dyn && lane == 0) nxt_v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int s = (k.order == 1) ? item / nchunks : item % k.nstrips;
-    const int ch = chunk0 + ((k.order == 1) ? item % nchunks : item / k.nstrips);
+    const int gitem = listed ? cload(k.ilist + item) : item;
+    const int s = (k.order == 1 && !listed) ? gitem / nchunks : gitem % k.nstrips;
+    const int ch = chunk0 + ((k.order == 1 && !listed) ? gitem % nchunks : gitem / k.nstrips);
     const int J = -1 + s * FSW;
     const int ib = 1 + ch * k.ti, ie = min(ib + k.ti - 1, nx);
     const int c0 = J + 2 * lane;               // odd → 16-byte aligned pair (c0, c0+1)
@@ -475,7 +489,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       pq[PF - 1] = pN;
       wq[PF - 1] = wN;
     }
-    if (dyn) {
+    if (persum) {
       // per-item sums (wave-reduced) in a fixed slot: the reduction kernel
       // adds them in item order, so the result does not depend on which
       // wave pulled which item
@@ -493,7 +507,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     }
     item = dyn ? __builtin_amdgcn_readfirstlane(int(nxt_v)) : item + istride;
   }
-  if (dyn) return;  // kRed reduces the item sums and finalizes
+  if (persum) return;  // kRed reduces the item sums and finalizes
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   block_reduce<7, false>(v, sm);
@@ -637,7 +651,11 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(k, go);
   else with_kS<2>(k, go);
-  if (k.order == 3) {
+  if (k.order == 3 && !k.ilist) launch_red(k, par, s);
+}
+
+void launch_red(const KParams& k, int par, hipStream_t s) {
+  {
     int rb = 16;  // few arrivals on the ticket: the fan-in, not the 2 MB, sets the time
     if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
     rb = std::max(1, std::min(rb, (k.nitems + 255) / 256));

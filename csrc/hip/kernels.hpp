@@ -93,6 +93,12 @@ struct KParams {
   long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
   double* hist;                  // keep_history: ‖Δw‖ of iteration k at hist[k-1] (k ≤ hist_n)
   long long hist_n;
+  // Halo/interior overlap: this launch walks only the listed items (global
+  // chunk-major indices); role 1 = boundary launch (owns the last-sweep /
+  // breakdown paths), 2 = interior launch (returns on them).
+  const int* ilist;
+  int nilist;
+  int list_role;
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
@@ -108,6 +114,8 @@ void launch_G(const KParams& k, int par, int variant, hipStream_t s);
 void launch_error(const KParams& k, hipStream_t s);
 // Single-sweep PCG (fused.hip): one kernel + one 7-scalar reduction per iteration.
 void launch_S(const KParams& k, int par, hipStream_t s);
+// Deterministic reduction of per-item sums + state update (dynamic / listed sweeps).
+void launch_red(const KParams& k, int par, hipStream_t s);
 // y-direction halo strips of buffer b: pack columns {1,2} / {ny-1,ny} of r,p
 // into send_dn / send_up ([nx][4]); unpack recv_dn / recv_up into columns
 // {-1,0} / {ny+1,ny+2}.

@@ -122,6 +122,7 @@ class DeviceSolver {
   std::vector<HaloPhase> halo_phases(int buf) const;
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
+  bool overlap() const { return overlap_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   hipStream_t stream() const { return stream_; }
@@ -147,6 +148,7 @@ class DeviceSolver {
  private:
   void build_tables(int64_t rows_hi, int64_t cols_hi);
   void set_fused_fields(double* x0, double* x1, double* w);
+  void setup_overlap();
   void choose_placement();
   void enqueue_iteration(int par);
   void enqueue_exchange(int buf);
@@ -172,6 +174,12 @@ class DeviceSolver {
   int64_t hsize_ = 0;
   double* partial_ = nullptr;
   double* hist_ = nullptr;
+  // halo/interior overlap (multi-rank single-sweep)
+  bool overlap_ = false;
+  int* ilist_ = nullptr;  // boundary items, then interior items
+  int nlist_b_ = 0, nlist_i_ = 0;
+  hipStream_t hs_ = nullptr;
+  hipEvent_t ev_start_ = nullptr, ev_halo_ = nullptr;
   dev::DevState* st_ = nullptr;
   dev::DevState* hst_ = nullptr;  // pinned, 2 slots
   std::unique_ptr<dev::KParams> kp_;

@@ -292,15 +292,16 @@ def test_two_process_device_path_host_staged(gpu):
     assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
 
 
-@pytest.mark.parametrize("nproc,decomp", [(4, "aspect"), (3, "aspect")])
-def test_multi_process_2d_host_staged(gpu, nproc, decomp):
+@pytest.mark.parametrize("nproc,decomp,overlap", [(4, "aspect", "1"), (3, "aspect", "1"), (4, "aspect", "0")])
+def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap):
     """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
     rows through the x phase of the single-sweep halo) — and 3×1 — match the
-    single-process solution (gathered w)."""
+    single-process solution (gathered w); with and without the boundary /
+    interior overlap on two streams."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host")
-    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}.npy")
+    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap)
+    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
