@@ -494,6 +494,10 @@ void DeviceSolver::enqueue_iteration(int par) {
     ki.ilist = ilist_ + nlist_b_;
     ki.nilist = nlist_i_;
     ki.list_role = 2;
+    // the interior grid leaves the boundary launch's slots free, so both run
+    // at once whichever the dispatcher starts first
+    ki.nblocks = std::max(1, kp_->nblocks - kb.nblocks);
+    ki.nblocks0 = std::max(1, kp_->nblocks0 - kb.nblocks);
     PE_HIP_CHECK(hipEventRecord(ev_start_, stream_));
     PE_HIP_CHECK(hipStreamWaitEvent(hs_, ev_start_, 0));
     dev::launch_S(kb, par, hs_);  // boundary items first, on the high-priority stream
