@@ -228,7 +228,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const int per0 = dev::resident_blocks_S(k, 0);
     if (per0 > 0) k.nblocks0 = grid_for(cus * per0 * dev::kWPB);
   }
-  const int64_t npart = 8 * std::max<int64_t>(int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
+  // block partials: interior grid, then (overlap) the boundary grid after it
+  const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + (fused_ ? 8 * int64_t(k.nitems) : 0))));
   k.partial = partial_;
   k.itemsum = fused_ ? partial_ + npart : nullptr;
@@ -491,6 +492,8 @@ void DeviceSolver::enqueue_iteration(int par) {
     kb.nilist = nlist_b_;
     kb.list_role = 1;
     kb.nblocks = kb.nblocks0 = std::max(1, std::min(kp_->nblocks, (nlist_b_ + dev::kWPB - 1) / dev::kWPB));
+    kb.pb_off = ki.pb_off = std::max(kp_->nblocks, kp_->nblocks0);  // after the interior partials
+    kb.pb_n = ki.pb_n = kb.nblocks;
     ki.ilist = ilist_ + nlist_b_;
     ki.nilist = nlist_i_;
     ki.list_role = 2;
@@ -506,9 +509,8 @@ void DeviceSolver::enqueue_iteration(int par) {
       if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
     }
     PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
-    dev::launch_S(ki, par, stream_);  // interior items, overlapping the exchange
+    dev::launch_S(ki, par, stream_);  // interior items (finalizes the sweep), overlapping the exchange
     PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
-    dev::launch_red(*kp_, par, stream_);
     comm_->allreduce_sum(st_->fs[par], 7, stream_);
     return;
   }
@@ -856,6 +858,7 @@ SolveResult DeviceSolver::solve() {
   res.converged = hs.status == 1;
   res.breakdown = hs.status == 2;
   res.nonfinite = hs.status == 4;
+  if (hs.status == 5) throw std::runtime_error("single-sweep: boundary partials never arrived (internal error)");
   res.last_diff = hs.last_diff;
   if (hist_ && hs.iter > 0) {
     res.history.resize(size_t(std::min<long long>(hs.iter, kp_->hist_n)));
@@ -1043,6 +1046,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   res.converged = hs.status == 1;
   res.breakdown = hs.status == 2;
   res.nonfinite = hs.status == 4;
+  if (hs.status == 5) throw std::runtime_error("single-sweep: boundary partials never arrived (internal error)");
   res.last_diff = hs.last_diff;
   res.zr = hs.rz_cur;
   if (opt.compute_error) {

@@ -269,9 +269,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     ilimit = k.nitems;
     chunk0 = 0;
   }
-  // Explicit item list (halo/interior overlap): a static walk over it, item
-  // sums per item like the dynamic queue (the reduction kernel adds both
-  // launches' items in item order).
+  // Explicit item list (halo/interior overlap): a static walk over it.  The
+  // boundary launch publishes its block partials; the interior launch's last
+  // block waits for them and reduces both sets in a fixed order.
   const bool listed = k.ilist != nullptr;
   if (listed) {
     it0 = blockIdx.x * kWPB + wid;
@@ -280,7 +280,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     chunk0 = 0;
   }
   const bool dyn = k.order == 3 && !listed;
-  const bool persum = dyn || listed;
+  const bool persum = dyn;
   auto pull = [&]() -> int {
     unsigned v = 0;
     if (lane == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -511,14 +511,47 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   block_reduce<7, false>(v, sm);
+  // boundary launch (role 1): partials after the interior ones, own ticket
+  double* part = k.partial + (k.list_role == 1 ? 7 * size_t(k.pb_off) : 0);
+  unsigned* ticket = &st->ticket[k.list_role == 1 ? 2 : 0];
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int n = 0; n < 7; ++n) k.partial[7 * size_t(blockIdx.x) + n] = v[n];
-  if (arrive_last(&st->ticket[0], gridDim.x, &sflag)) {
+    for (int n = 0; n < 7; ++n) part[7 * size_t(blockIdx.x) + n] = v[n];
+  if (arrive_last(ticket, gridDim.x, &sflag)) {
+    if (k.list_role == 1) {  // publish: every boundary partial is visible to this block
+      if (threadIdx.x == 0) {
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(&st->bflag, kiter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
+    if (k.list_role == 2) {
+      // wait for the boundary launch of this sweep (it owns reserved slots, so
+      // it always runs; bounded spin as a safety net)
+      if (threadIdx.x == 0) {
+        long long spins = 0;
+        while (__hip_atomic_load(&st->bflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kiter &&
+               ++spins < (1ll << 28))
+          __builtin_amdgcn_s_sleep(2);
+        sflag = spins < (1ll << 28);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      }
+      __syncthreads();
+      const int ok = sflag;
+      double tb[7];
+      reduce_partials<7>(k.partial + 7 * size_t(k.pb_off), unsigned(k.pb_n), tb, sm);
+#pragma unroll
+      for (int n = 0; n < 7; ++n) t[n] = t[n] + tb[n];
+      if (threadIdx.x == 0 && !ok) {  // never observed: report instead of hanging
+        st->status = 5;
+        st->done = 1;
+      }
+    }
     if (threadIdx.x == 0) {
-      sweep_finalize<WM>(k, st, par, sc, t);
+      if (!st->done) sweep_finalize<WM>(k, st, par, sc, t);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }

@@ -34,7 +34,7 @@ struct DevState {
   double alpha, beta, last_diff;
   long long iter;    // completed iterations
   int done;          // 1 → every later kernel is a no-op
-  int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap, 4 non-finite scalars
+  int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap, 4 non-finite scalars, 5 internal
   unsigned ticket[4];
   unsigned pad[4];
   // Single-sweep (fused) PCG: the 7 local/global sums of sweep k live in
@@ -46,6 +46,7 @@ struct DevState {
   int wpar;          // buffer x[wpar] holding that p_k
   int pad2;
   unsigned qhead[8][16];  // single-sweep work queue heads, one 64-B line per XCD shard
+  long long bflag;        // overlap: iteration whose boundary-launch partials are published
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -99,6 +100,7 @@ struct KParams {
   const int* ilist;
   int nilist;
   int list_role;
+  int pb_off, pb_n;              // boundary launch: its partials at partial[7*pb_off ...], pb_n blocks
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
