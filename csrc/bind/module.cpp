@@ -273,6 +273,14 @@ PYBIND11_MODULE(_native, m) {
       },
       py::arg("uid"), py::arg("rank"), py::arg("size"));
   m.def(
+      "make_delay_comm",
+      [](int size, double exchange_us, double allreduce_us) {
+        auto h = std::make_unique<CommHandle>();
+        h->comm = make_delay_comm(size, exchange_us, allreduce_us);
+        return h;
+      },
+      py::arg("size"), py::arg("exchange_us"), py::arg("allreduce_us"));
+  m.def(
       "make_host_staged_comm",
       [](int rank, int size, py::function reduce_fn, py::function exchange_fn, py::function barrier_fn) {
         auto reduce = [reduce_fn](double* buf, int n, bool is_max) {

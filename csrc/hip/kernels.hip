@@ -526,6 +526,18 @@ __global__ void kCoef(KParams k, double* a, double* b, double* D) {
 
 int grid_blocks(const KParams& k) { return k.nblocks; }
 
+// Test transport: a busy wait of `us` microseconds on the stream (one wave).
+__global__ void kDelay(long long ticks) {
+  const long long t0 = wall_clock64();
+  while (wall_clock64() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+}
+void launch_delay(double us, hipStream_t s) {
+  int rate_khz = 100000;  // wall_clock64 runs at a fixed 100 MHz on CDNA
+  (void)hipDeviceGetAttribute(&rate_khz, hipDeviceAttributeWallClockRate, 0);
+  const long long ticks = (long long)(us * 1e-3 * double(rate_khz));
+  hipLaunchKernelGGL(kDelay, dim3(1), dim3(64), 0, s, ticks);
+}
+
 int resident_blocks_classic(int variant) {
   int n = 0, m = 0;
   if (variant == 1) {

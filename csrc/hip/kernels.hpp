@@ -131,6 +131,7 @@ void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hip
 void launch_apply_A(const KParams& k, const double* p, double* Ap, hipStream_t s);
 void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t s);
 int grid_blocks(const KParams& k);
+void launch_delay(double us, hipStream_t s);  // test transport: stream-ordered busy wait
 // Resident 256-thread blocks per CU of the marching kernels (occupancy API;
 // 0 when unavailable).  Sizes the persistent grids.
 int resident_blocks_S(const KParams& k, int wm);  // wm 0: deferring sweep, 2: applying sweep

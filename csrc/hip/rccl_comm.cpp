@@ -20,6 +20,7 @@
 #include <stdexcept>
 #include <vector>
 
+#include "../hip/kernels.hpp"
 #include "pe/device.hpp"
 
 #define PE_NCCL_CHECK(expr)                                                                             \
@@ -102,6 +103,30 @@ class RcclComm final : public DeviceComm {
   double* scratch_ = nullptr;
 };
 
+// Timing-only test transport: every exchange / allreduce is a stream-ordered
+// busy wait of a fixed duration (no data moves).  Lets one GPU measure how
+// much of a given communication latency the halo/interior overlap hides.
+class DelayComm final : public DeviceComm {
+ public:
+  DelayComm(int size, double exchange_us, double allreduce_us)
+      : size_(size), ex_us_(exchange_us), ar_us_(allreduce_us) {}
+  int rank() const override { return 0; }
+  int size() const override { return size_; }
+  void allreduce_sum(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
+  void allreduce_max(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
+  void exchange(const std::vector<Exchange>& ex, hipStream_t s) override {
+    if (!ex.empty()) dev::launch_delay(ex_us_, s);
+  }
+  void host_max(double*, int, hipStream_t) override {}
+  void barrier(hipStream_t) override {}
+  bool capturable() const override { return true; }
+  std::string name() const override { return "delay"; }
+
+ private:
+  int size_;
+  double ex_us_, ar_us_;
+};
+
 class HostStagedComm final : public DeviceComm {
  public:
   HostStagedComm(int rank, int size, CallbackHostComm::ReduceFn r, CallbackHostComm::ExchangeFn e,
@@ -149,6 +174,10 @@ class HostStagedComm final : public DeviceComm {
 };
 
 }  // namespace
+
+std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us) {
+  return std::make_unique<DelayComm>(size, exchange_us, allreduce_us);
+}
 
 std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
                                                       CallbackHostComm::ExchangeFn exch,

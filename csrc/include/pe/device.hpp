@@ -73,6 +73,8 @@ std::unique_ptr<DeviceComm> make_rccl_comm_from_handle(void* nccl_comm);
 // stage-4 pattern (poisson_mpi_cuda2.cu:331-500).  A test/fallback transport
 // for several ranks sharing one GPU (RCCL refuses duplicate devices); the
 // production transport is RCCL.
+// Timing-only test transport (stream-ordered busy waits; no data moves).
+std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us);
 std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
                                                       CallbackHostComm::ExchangeFn exch,
                                                       CallbackHostComm::BarrierFn barrier);
