@@ -265,38 +265,55 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
   k.p[1] = k.x[1] + plane_;
 }
 
-// Halo/interior overlap (multi-rank single-sweep): the items whose outputs
-// are sent to a neighbour (first / last two owned rows and columns) run in a
-// small launch on a high-priority stream; the exchange starts as soon as
-// that launch is done, while the interior items run on the solver stream.
-// PE_OVERLAP=0 disables.
+// Halo/interior overlap (multi-rank single-sweep).  The sweep walks an item
+// list in which, per XCD shard, the boundary items (outputs sent to a
+// neighbour: first / last two owned rows and columns) come first; each bumps
+// st->sig when stored.  A one-wave kernel on a high-priority halo stream waits
+// for the count, then the exchange runs there while the interior items are
+// still being computed.  The sweep keeps its full persistent grid minus
+// `PE_OV_RESERVE` blocks (default 8) left free for the wait / exchange /
+// unpack kernels.  PE_OVERLAP=0 disables.
 void DeviceSolver::setup_overlap() {
-  const KParams& k = *kp_;
+  KParams& k = *kp_;
   const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = fused_ && comm_->size() > 1 && nb && !(e && std::atoi(e) == 0);
   if (!overlap_) return;
-  std::vector<int> b, in;
-  const int64_t nchunks = (blk_.nx + k.ti - 1) / k.ti;
-  for (int64_t ch = 0; ch < nchunks; ++ch)
-    for (int s = 0; s < k.nstrips; ++s) {
-      const int64_t ib = 1 + ch * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-      const int64_t J = -1 + int64_t(s) * dev::kFSW;
-      const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
-      const bool bnd = (blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
-                       (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1);
-      (bnd ? b : in).push_back(int(ch * k.nstrips + s));
-    }
-  nlist_b_ = int(b.size());
-  nlist_i_ = int(in.size());
-  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int) * std::max<size_t>(1, b.size() + in.size())));
-  if (!b.empty()) PE_HIP_CHECK(hipMemcpy(ilist_, b.data(), sizeof(int) * b.size(), hipMemcpyHostToDevice));
-  if (!in.empty())
-    PE_HIP_CHECK(hipMemcpy(ilist_ + b.size(), in.data(), sizeof(int) * in.size(), hipMemcpyHostToDevice));
+  ov_reserve_ = 8;
+  // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
+  // order (no boundary-first list)
+  if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
+  if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
+  const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - ov_reserve_);
+  const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
+  const int nchunks = int((blk_.nx + k.ti - 1) / k.ti);
+  std::vector<int> all;
+  ov_nb_ = 0;
+  ov_lnsh_ = nsh;
+  for (int x = 0; x < nsh; ++x) {
+    std::vector<int> b, in;
+    for (int ch = x * nchunks / nsh; ch < (x + 1) * nchunks / nsh; ++ch)
+      for (int s = 0; s < k.nstrips; ++s) {
+        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+        const int64_t J = -1 + int64_t(s) * dev::kFSW;
+        const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
+        const bool bnd = (blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
+                         (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1);
+        (bnd && !(ov_debug_ & 4) ? b : in).push_back(ch * k.nstrips + s);
+      }
+    ov_lbase_[x] = int(all.size());
+    ov_lnb_[x] = int(b.size());
+    ov_nb_ += int(b.size());
+    all.insert(all.end(), b.begin(), b.end());
+    all.insert(all.end(), in.begin(), in.end());
+  }
+  ov_lbase_[nsh] = int(all.size());
+  if (int(all.size()) != k.nitems) throw std::logic_error("overlap item list does not cover the block");
+  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int) * all.size()));
+  PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int) * all.size(), hipMemcpyHostToDevice));
   int least = 0, greatest = 0;
   PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));
-  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_start_, hipEventDisableTiming));
   PE_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
 }
 
@@ -400,7 +417,6 @@ DeviceSolver::~DeviceSolver() {
   if (hist_) (void)hipFree(hist_);
   if (ilist_) (void)hipFree(ilist_);
   if (hs_) (void)hipStreamDestroy(hs_);
-  if (ev_start_) (void)hipEventDestroy(ev_start_);
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   (void)hipFree(st_);
   (void)hipHostFree(hst_);
@@ -474,6 +490,7 @@ void DeviceSolver::enqueue_init() {
   }
   PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * hsize_ * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
+  ov_epoch_ = 0;
   dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
   PE_HIP_CHECK(hipGetLastError());
 }
@@ -487,29 +504,28 @@ void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 
 void DeviceSolver::enqueue_iteration(int par) {
   if (fused_ && overlap_) {
-    KParams kb = *kp_, ki = *kp_;
-    kb.ilist = ilist_;
-    kb.nilist = nlist_b_;
-    kb.list_role = 1;
-    kb.nblocks = kb.nblocks0 = std::max(1, std::min(kp_->nblocks, (nlist_b_ + dev::kWPB - 1) / dev::kWPB));
-    kb.pb_off = ki.pb_off = std::max(kp_->nblocks, kp_->nblocks0);  // after the interior partials
-    kb.pb_n = ki.pb_n = kb.nblocks;
-    ki.ilist = ilist_ + nlist_b_;
-    ki.nilist = nlist_i_;
-    ki.list_role = 2;
-    // the interior grid leaves the boundary launch's slots free, so both run
-    // at once whichever the dispatcher starts first
-    ki.nblocks = std::max(1, kp_->nblocks - kb.nblocks);
-    ki.nblocks0 = std::max(1, kp_->nblocks0 - kb.nblocks);
-    PE_HIP_CHECK(hipEventRecord(ev_start_, stream_));
-    PE_HIP_CHECK(hipStreamWaitEvent(hs_, ev_start_, 0));
-    dev::launch_S(kb, par, hs_);  // boundary items first, on the high-priority stream
+    KParams ko = *kp_;
+    ko.ilist = ilist_;
+    ko.lnsh = ov_lnsh_;
+    for (int x = 0; x <= 8; ++x) ko.lbase[x] = ov_lbase_[x];
+    for (int x = 0; x < 8; ++x) ko.lnb[x] = ov_lnb_[x];
+    ko.nblocks = std::max(ov_lnsh_, kp_->nblocks - ov_reserve_);
+    ko.nblocks0 = std::max(ov_lnsh_, kp_->nblocks0 - ov_reserve_);
+    ov_epoch_ += 1;
+    const unsigned long long target = ov_epoch_ * (unsigned long long)(ov_nb_);
+    dev::launch_S(ko, par, stream_);  // boundary items first in every shard
+    if (ov_debug_ & 2) {
+      dev::launch_wait_sig(ko, target, stream_);
+      enqueue_exchange(par);
+      comm_->allreduce_sum(st_->fs[par], 7, stream_);
+      return;
+    }
+    dev::launch_wait_sig(ko, target, hs_);  // the exchange starts once they are stored
     for (const HaloPhase& ph : halo_phases(par)) {
       comm_->exchange(ph.ex, hs_);
       if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
     }
     PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
-    dev::launch_S(ki, par, stream_);  // interior items (finalizes the sweep), overlapping the exchange
     PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
     comm_->allreduce_sum(st_->fs[par], 7, stream_);
     return;
@@ -548,7 +564,9 @@ void DeviceSolver::enqueue_chunk(int iters) {
   // The captured graph starts at parity 0 and has an even length; iterations
   // that would break the p / x ping-pong parity run eagerly.
   int it = 0;
-  if (opt_.use_graph && comm_->capturable() && par_ == 0 && iters >= 2) {
+  // (overlap: a graph may serialise the two streams' branches in any order,
+  // and the halo branch waits on the sweep — always eager)
+  if (opt_.use_graph && comm_->capturable() && !overlap_ && par_ == 0 && iters >= 2) {
     const int n = iters - (iters & 1);
     graph_ready(n);
     PE_HIP_CHECK(hipGraphLaunch(graph_, stream_));
@@ -660,6 +678,8 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
   load(halo_, size_t(h.halo_bytes));
   std::fclose(f);
   par_ = h.par;
+  PE_HIP_CHECK(hipMemset(&st_->sig, 0, sizeof(st_->sig)));  // overlap targets restart
+  ov_epoch_ = 0;
 }
 
 void DeviceSolver::wait_event(hipEvent_t ev) {

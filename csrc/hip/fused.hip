@@ -197,8 +197,6 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
   if (!first) {
     const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
-    const bool last = bad || fabs(sc.den) < 1e-15 || (WM == 0 && ((k.check_tol && diff < k.tol) || kiter >= k.max_iter));
-    if (last && k.list_role == 2) return;  // the boundary launch of this sweep handles it
     if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
       if (WM == 2 && st->wpend && !bad) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
       if (blockIdx.x == 0 && threadIdx.x == 0) {
@@ -252,7 +250,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   // re-read from its L2).  order 2: the same ranges dealt statically; 0/1:
   // static global chunk-major / strip-major.
   const int nchunks = (nx + k.ti - 1) / k.ti;
-  const int nsh = min(8, int(gridDim.x));  // shards (every shard must own blocks)
+  const bool listed = k.ilist != nullptr;
+  const int nsh = listed ? k.lnsh : min(8, int(gridDim.x));  // shards (every shard must own blocks)
   const int xs = int(blockIdx.x) % nsh;
   int it0, istride, ilimit, chunk0;
   unsigned* head = &st->qhead[xs][0];
@@ -269,17 +268,22 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     ilimit = k.nitems;
     chunk0 = 0;
   }
-  // Explicit item list (halo/interior overlap): a static walk over it.  The
-  // boundary launch publishes its block partials; the interior launch's last
-  // block waits for them and reduces both sets in a fixed order.
-  const bool listed = k.ilist != nullptr;
+  // Item list (halo/interior overlap): shard x walks its own list segment
+  // (statically, or pulling from its queue under order 3), boundary items
+  // first, so the items whose outputs feed the exchange finish in the first
+  // round of pulls; the exchange waits for them on st->sig, not for the sweep.
+  const int* lst = nullptr;
+  int lnb = 0;
   if (listed) {
-    it0 = blockIdx.x * kWPB + wid;
-    istride = gridDim.x * kWPB;
-    ilimit = k.nilist;
+    const int nbx = (int(gridDim.x) - xs + nsh - 1) / nsh;
+    it0 = (int(blockIdx.x) / nsh) * kWPB + wid;
+    istride = nbx * kWPB;
+    lst = k.ilist + k.lbase[xs];
+    ilimit = k.lbase[xs + 1] - k.lbase[xs];
+    lnb = k.lnb[xs];
     chunk0 = 0;
   }
-  const bool dyn = k.order == 3 && !listed;
+  const bool dyn = k.order == 3;
   const bool persum = dyn;
   auto pull = [&]() -> int {
     unsigned v = 0;
@@ -290,7 +294,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   while (item < ilimit) {
     unsigned nxt_v = 0;  // next item, requested now, read after this one
     if (dyn && lane == 0) nxt_v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int gitem = listed ? cload(k.ilist + item) : item;
+    const int gitem = listed ? cload(lst + item) : item;
     const int s = (k.order == 1 && !listed) ? gitem / nchunks : gitem % k.nstrips;
     const int ch = chunk0 + ((k.order == 1 && !listed) ? gitem % nchunks : gitem / k.nstrips);
     const int J = -1 + s * FSW;
@@ -505,53 +509,27 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       }
       sg = sd = se = sps = szz = szp = spp = 0.0;
     }
+    if (item < lnb) {
+      // boundary item: once its stores (send strips included) have reached L2,
+      // count it.  No agent-scope release here — that is an L2 writeback per
+      // item (≈15 µs per 8-rank sweep); kWaitSig writes each XCD's L2 back once.
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      if (lane == 0) __hip_atomic_fetch_add(&st->sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
     item = dyn ? __builtin_amdgcn_readfirstlane(int(nxt_v)) : item + istride;
   }
   if (persum) return;  // kRed reduces the item sums and finalizes
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   block_reduce<7, false>(v, sm);
-  // boundary launch (role 1): partials after the interior ones, own ticket
-  double* part = k.partial + (k.list_role == 1 ? 7 * size_t(k.pb_off) : 0);
-  unsigned* ticket = &st->ticket[k.list_role == 1 ? 2 : 0];
   if (threadIdx.x == 0)
 #pragma unroll
-    for (int n = 0; n < 7; ++n) part[7 * size_t(blockIdx.x) + n] = v[n];
-  if (arrive_last(ticket, gridDim.x, &sflag)) {
-    if (k.list_role == 1) {  // publish: every boundary partial is visible to this block
-      if (threadIdx.x == 0) {
-        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        __hip_atomic_store(&st->bflag, kiter, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      return;
-    }
+    for (int n = 0; n < 7; ++n) k.partial[7 * size_t(blockIdx.x) + n] = v[n];
+  if (arrive_last(&st->ticket[0], gridDim.x, &sflag)) {
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
-    if (k.list_role == 2) {
-      // wait for the boundary launch of this sweep (it owns reserved slots, so
-      // it always runs; bounded spin as a safety net)
-      if (threadIdx.x == 0) {
-        long long spins = 0;
-        while (__hip_atomic_load(&st->bflag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != kiter &&
-               ++spins < (1ll << 28))
-          __builtin_amdgcn_s_sleep(2);
-        sflag = spins < (1ll << 28);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-      }
-      __syncthreads();
-      const int ok = sflag;
-      double tb[7];
-      reduce_partials<7>(k.partial + 7 * size_t(k.pb_off), unsigned(k.pb_n), tb, sm);
-#pragma unroll
-      for (int n = 0; n < 7; ++n) t[n] = t[n] + tb[n];
-      if (threadIdx.x == 0 && !ok) {  // never observed: report instead of hanging
-        st->status = 5;
-        st->done = 1;
-      }
-    }
     if (threadIdx.x == 0) {
-      if (!st->done) sweep_finalize<WM>(k, st, par, sc, t);
+      sweep_finalize<WM>(k, st, par, sc, t);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -606,6 +584,21 @@ __global__ void kWFlush(KParams k) {
   }
 }
 __global__ void kWFlushDone(KParams k) { k.st->wpend = 0; }
+
+// Overlap: hold the halo stream until every boundary item of the running
+// sweep is in L2 (kS counts them into sig), or the solve has ended (the sweep
+// then stores nothing), then make those stores visible device-wide: L2s are
+// per XCD and not coherent with each other, so each block — launched on 8
+// consecutive workgroups, which the dispatcher deals to the 8 XCDs — writes
+// its XCD's L2 back (agent-scope release).  Targets are cumulative per solve.
+__global__ void kWaitSig(DevState* st, unsigned long long target) {
+  if (threadIdx.x == 0) {
+    while (__hip_atomic_load(&st->sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
+           !__hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+      __builtin_amdgcn_s_sleep(4);
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
+  }
+}
 
 // y-direction halo strips of buffer b (one thread per owned row).
 __global__ void kPack(KParams k, int b) {
@@ -684,7 +677,7 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(k, go);
   else with_kS<2>(k, go);
-  if (k.order == 3 && !k.ilist) launch_red(k, par, s);
+  if (k.order == 3) launch_red(k, par, s);
 }
 
 void launch_red(const KParams& k, int par, hipStream_t s) {
@@ -695,6 +688,10 @@ void launch_red(const KParams& k, int par, hipStream_t s) {
     if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
     else hipLaunchKernelGGL(kRed<2>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
   }
+}
+
+void launch_wait_sig(const KParams& k, unsigned long long target, hipStream_t s) {
+  hipLaunchKernelGGL(kWaitSig, dim3(8), dim3(64), 0, s, k.st, target);
 }
 
 void launch_wflush(const KParams& k, hipStream_t s) {

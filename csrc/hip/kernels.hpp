@@ -46,7 +46,7 @@ struct DevState {
   int wpar;          // buffer x[wpar] holding that p_k
   int pad2;
   unsigned qhead[8][16];  // single-sweep work queue heads, one 64-B line per XCD shard
-  long long bflag;        // overlap: iteration whose boundary-launch partials are published
+  unsigned long long sig;  // overlap: boundary items stored, cumulative over the solve's sweeps
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -94,13 +94,14 @@ struct KParams {
   long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
   double* hist;                  // keep_history: ‖Δw‖ of iteration k at hist[k-1] (k ≤ hist_n)
   long long hist_n;
-  // Halo/interior overlap: this launch walks only the listed items (global
-  // chunk-major indices); role 1 = boundary launch (owns the last-sweep /
-  // breakdown paths), 2 = interior launch (returns on them).
+  // Halo/interior overlap: the sweep walks an item list (global chunk-major
+  // indices) split into lnsh shards; shard x owns ilist[lbase[x] .. lbase[x+1])
+  // and its first lnb[x] entries are boundary items (outputs sent to a
+  // neighbour), each of which bumps st->sig once its stores are visible.
   const int* ilist;
-  int nilist;
-  int list_role;
-  int pb_off, pb_n;              // boundary launch: its partials at partial[7*pb_off ...], pb_n blocks
+  int lnsh;
+  int lbase[9];
+  int lnb[8];
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
@@ -125,6 +126,10 @@ void launch_pack(const KParams& k, int b, hipStream_t s);
 // Add a pending deferred w term (no-op when none is pending).
 void launch_wflush(const KParams& k, hipStream_t s);
 void launch_unpack(const KParams& k, int b, hipStream_t s);
+// Overlap: spin until st->sig reaches `target` (every boundary item of the
+// running sweep is in L2) or the solve is done, then write every XCD's L2
+// back.  Put on the halo stream ahead of the exchange.
+void launch_wait_sig(const KParams& k, unsigned long long target, hipStream_t s);
 // Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);
 // Debug/test ops (single-shot, no convergence logic).

@@ -178,10 +178,12 @@ class DeviceSolver {
   double* hist_ = nullptr;
   // halo/interior overlap (multi-rank single-sweep)
   bool overlap_ = false;
-  int* ilist_ = nullptr;  // boundary items, then interior items
-  int nlist_b_ = 0, nlist_i_ = 0;
+  int* ilist_ = nullptr;  // per shard: boundary items, then interior items
+  int ov_lnsh_ = 1, ov_nb_ = 0, ov_reserve_ = 8, ov_debug_ = 0;
+  int ov_lbase_[9] = {}, ov_lnb_[8] = {};
+  unsigned long long ov_epoch_ = 0;  // overlapped sweeps since the state was last cleared (sig targets)
   hipStream_t hs_ = nullptr;
-  hipEvent_t ev_start_ = nullptr, ev_halo_ = nullptr;
+  hipEvent_t ev_halo_ = nullptr;
   dev::DevState* st_ = nullptr;
   dev::DevState* hst_ = nullptr;  // pinned, 2 slots
   std::unique_ptr<dev::KParams> kp_;

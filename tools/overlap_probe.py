@@ -1,7 +1,8 @@
 """How much communication latency does the halo/interior overlap hide?
 One GPU runs the block of one rank of a multi-GPU decomposition with a
 timing-only transport (stream-ordered busy waits of fixed length stand in
-for the RCCL exchange and allreduce), with PE_OVERLAP=0 and 1.
+for the RCCL exchange and allreduce), with PE_OVERLAP=0 and 1
+(PROBE_OV=0,1:8,1:32:1 → overlap:reserved blocks[:PE_OV_DEBUG]).
 
     python tools/overlap_probe.py [exchange_us allreduce_us]"""
 import os
@@ -24,8 +25,10 @@ for P, spec in configs:
     rank = P // 2
     blk = nat.decompose(8192, 8192, g, rank)
     for delays in [(0.0, 0.0), (ex_us, ar_us)]:
-        for ov in ("0", "1"):
-            os.environ["PE_OVERLAP"] = ov
+        for ov in os.environ.get("PROBE_OV", "0,1:8").split(","):
+            os.environ["PE_OVERLAP"] = ov.split(":")[0]
+            os.environ["PE_OV_RESERVE"] = ov.split(":")[1] if ":" in ov else "8"
+            os.environ["PE_OV_DEBUG"] = ov.split(":")[2] if ov.count(":") > 1 else "0"
             opt = nat.SolveOptions()
             opt.check_tol = False
             comm = nat.make_delay_comm(P, delays[0], delays[1])
