@@ -107,6 +107,8 @@ int main(int argc, char** argv) {
   } else {
     std::unique_ptr<DeviceComm> comm;
     if (size > 1) comm = make_rccl_comm(exchange_uid(rank, size), rank, size);
+    if (comm && std::getenv("PE_ALLREDUCE") && std::string(std::getenv("PE_ALLREDUCE")) == "p2p")
+      comm = make_p2p_allreduce_comm(std::move(comm));
     const ProcessGrid pg = process_grid_from_spec(decomp, size, P.M, P.N);
     const Block blk = decompose(P.M, P.N, pg, rank);
     DeviceSolver solver(P, blk, comm.get(), opt);

@@ -261,7 +261,36 @@ PYBIND11_MODULE(_native, m) {
   py::class_<CommHandle>(m, "DeviceComm")
       .def_property_readonly("rank", [](const CommHandle& h) { return h.comm->rank(); })
       .def_property_readonly("size", [](const CommHandle& h) { return h.comm->size(); })
-      .def_property_readonly("name", [](const CommHandle& h) { return h.comm->name(); });
+      .def_property_readonly("name", [](const CommHandle& h) { return h.comm->name(); })
+      .def(
+          "bench_allreduce",
+          [](CommHandle& h, int n, int iters) {
+            // stream-ordered latency of the in-place sum of n doubles (collective)
+            py::gil_scoped_release nogil;
+            double* d = nullptr;
+            hipStream_t s = nullptr;
+            hipEvent_t e0, e1;
+            PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+            PE_HIP_CHECK(hipMalloc(&d, sizeof(double) * std::max(1, n)));
+            PE_HIP_CHECK(hipMemsetAsync(d, 0, sizeof(double) * std::max(1, n), s));
+            PE_HIP_CHECK(hipEventCreate(&e0));
+            PE_HIP_CHECK(hipEventCreate(&e1));
+            for (int i = 0; i < 5; ++i) h.comm->allreduce_sum(d, n, s);
+            h.comm->barrier(s);
+            PE_HIP_CHECK(hipEventRecord(e0, s));
+            for (int i = 0; i < iters; ++i) h.comm->allreduce_sum(d, n, s);
+            PE_HIP_CHECK(hipEventRecord(e1, s));
+            PE_HIP_CHECK(hipEventSynchronize(e1));
+            float ms = 0.f;
+            PE_HIP_CHECK(hipEventElapsedTime(&ms, e0, e1));
+            (void)hipEventDestroy(e0);
+            (void)hipEventDestroy(e1);
+            (void)hipFree(d);
+            (void)hipStreamDestroy(s);
+            return 1e3 * double(ms) / std::max(1, iters);
+          },
+          py::arg("n") = 7, py::arg("iters") = 1000,
+          "Microseconds per in-place allreduce_sum of n doubles (call on every rank).");
   m.def(
       "make_rccl_comm",
       [](py::bytes uid, int rank, int size) {
@@ -307,6 +336,15 @@ PYBIND11_MODULE(_native, m) {
         return h;
       },
       py::arg("rank"), py::arg("size"), py::arg("reduce_fn"), py::arg("exchange_fn"), py::arg("barrier_fn"));
+  m.def(
+      "use_p2p_allreduce",
+      [](CommHandle& h) {
+        py::gil_scoped_release nogil;
+        h.comm = make_p2p_allreduce_comm(std::move(h.comm));
+      },
+      py::arg("comm"),
+      "Switch the per-iteration sums of this communicator to the one-shot P2P allreduce (collective: call on "
+      "every rank).");
   m.def(
       "make_rccl_comm_from_handle",
       [](uintptr_t handle) {

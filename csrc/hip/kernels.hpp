@@ -130,6 +130,12 @@ void launch_unpack(const KParams& k, int b, hipStream_t s);
 // running sweep is in L2) or the solve is done, then write every XCD's L2
 // back.  Put on the halo stream ahead of the exchange.
 void launch_wait_sig(const KParams& k, unsigned long long target, hipStream_t s);
+// One-shot P2P allreduce (p2p.hip): every rank's receive buffer holds
+// 2 × P slots of kP2PSlot doubles (n ≤ kP2PSlot-1 values + a sequence flag);
+// peers[r] = rank r's buffer mapped into this process.  P ≤ 64.
+constexpr int kP2PSlot = 16;
+void launch_p2p_sum(double* d, int n, double* const* peers, int me, int P, unsigned long long seq, double timeout_s,
+                    hipStream_t s);
 // Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);
 // Debug/test ops (single-shot, no convergence logic).

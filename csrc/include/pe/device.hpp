@@ -75,6 +75,9 @@ std::unique_ptr<DeviceComm> make_rccl_comm_from_handle(void* nccl_comm);
 // production transport is RCCL.
 // Timing-only test transport (stream-ordered busy waits; no data moves).
 std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us);
+// One-shot P2P allreduce (IPC-mapped receive buffers, p2p.hip) for the
+// per-iteration sums; everything else through `base` (PE_ALLREDUCE=p2p).
+std::unique_ptr<DeviceComm> make_p2p_allreduce_comm(std::unique_ptr<DeviceComm> base);
 std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
                                                       CallbackHostComm::ExchangeFn exch,
                                                       CallbackHostComm::BarrierFn barrier);

@@ -85,7 +85,8 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
     Default: RCCL over xGMI, unique id via the torch store.  PE_COMM=host
     selects the host-staged gloo transport (several ranks on one GPU — RCCL
     refuses duplicate devices — for testing the multi-process path on a
-    single-GPU box)."""
+    single-GPU box).  PE_ALLREDUCE=p2p runs the per-iteration sums as a
+    one-shot peer-to-peer kernel over IPC-mapped buffers instead."""
     nat = native()
     nat.set_device(ctx.local_rank % max(1, nat.device_count()))
     if ctx.world == 1:
@@ -94,15 +95,19 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
         global _GLOO
         if _GLOO is None:
             _GLOO = dist.new_group(backend="gloo")
-        return nat.make_host_staged_comm(ctx.rank, ctx.world, *gloo_callbacks(_GLOO))
-    store = _store()
-    key = f"{tag}/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
-    if ctx.rank == 0:
-        uid = nat.rccl_unique_id()
-        store.set(key, uid)
+        comm = nat.make_host_staged_comm(ctx.rank, ctx.world, *gloo_callbacks(_GLOO))
     else:
-        uid = store.get(key)
-    return nat.make_rccl_comm(bytes(uid), ctx.rank, ctx.world)
+        store = _store()
+        key = f"{tag}/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
+        if ctx.rank == 0:
+            uid = nat.rccl_unique_id()
+            store.set(key, uid)
+        else:
+            uid = store.get(key)
+        comm = nat.make_rccl_comm(bytes(uid), ctx.rank, ctx.world)
+    if os.environ.get("PE_ALLREDUCE", "rccl") == "p2p":
+        nat.use_p2p_allreduce(comm)  # one-shot xGMI allreduce of the per-iteration sums
+    return comm
 
 
 # ---------------------------------------------------------------------------

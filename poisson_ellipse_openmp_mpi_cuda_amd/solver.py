@@ -55,6 +55,7 @@ class SolveReport:
     algo: str = ""
     nonfinite: bool = False
     history: Optional[list] = None  # ‖Δw‖ per iteration (keep_history=True)
+    comm: str = ""  # device transport of a multi-rank HIP run (e.g. "rccl", "p2p-allreduce+rccl")
 
     @property
     def iters_per_s(self) -> float:
@@ -183,4 +184,6 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
             w = wl
         else:
             w = _dist.gather_blocks(_dist.init(), prob, blk, wl)
-    return _report("hip", prob, res, world, 1, init, w, rank)
+    rep = _report("hip", prob, res, world, 1, init, w, rank)
+    rep.comm = comm.name if comm is not None else "self"
+    return rep

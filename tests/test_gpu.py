@@ -292,16 +292,20 @@ def test_two_process_device_path_host_staged(gpu):
     assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
 
 
-@pytest.mark.parametrize("nproc,decomp,overlap", [(4, "aspect", "1"), (3, "aspect", "1"), (4, "aspect", "0")])
-def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap):
+@pytest.mark.parametrize("nproc,decomp,overlap,allreduce", [(4, "aspect", "1", "rccl"), (3, "aspect", "1", "rccl"),
+                                                        (4, "aspect", "0", "rccl"), (4, "aspect", "1", "p2p"),
+                                                        (2, "aspect", "0", "p2p")])
+def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
     rows through the x phase of the single-sweep halo) — and 3×1 — match the
     single-process solution (gathered w); with and without the boundary /
-    interior overlap on two streams."""
+    interior overlap on two streams; with the per-iteration sums through the
+    host-staged transport or the one-shot P2P allreduce kernel (IPC-mapped
+    buffers of the other processes)."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap)
-    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}.npy")
+    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="60")
+    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}_{allreduce}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
@@ -310,6 +314,7 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap):
     assert out.returncode == 0, out.stderr[-3000:]
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
+    assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce == "p2p" else "host-staged")
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
