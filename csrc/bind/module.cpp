@@ -413,6 +413,17 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)
       .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
+      .def_property_readonly("order", [](DeviceSolver& s) { return s.params().order; })
+      .def_property_readonly("nitems", [](DeviceSolver& s) { return s.params().nslots; })
+      .def("stamps",
+           [](DeviceSolver& s) {
+             std::vector<unsigned long long> v = s.stamps();
+             py::array_t<unsigned long long> a(py::ssize_t(v.size()));
+             if (!v.empty()) std::memcpy(a.mutable_data(), v.data(), sizeof(unsigned long long) * v.size());
+             return a;
+           },
+           "PE_STAMPS=1 diagnostic timeline of the last sweep (tools/stamp_probe.py).")
+      .def("clear_stamps", &DeviceSolver::clear_stamps)
       .def_property_readonly("blocks", [](DeviceSolver& s) { return dev::grid_blocks(s.params()); })
       .def_property_readonly("block", &DeviceSolver::block);
 

@@ -230,7 +230,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
   // block partials: interior grid, then (overlap) the boundary grid after it
   const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
-  PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + (fused_ ? 8 * int64_t(k.nitems) : 0))));
+  // item-sum slots: one per item, more when setup_items splits tail items
+  nslot_cap_ = fused_ ? 2 * k.nitems + 64 : 0;
+  k.nslots = k.nitems;
+  PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + 8 * int64_t(nslot_cap_))));
   k.partial = partial_;
   k.itemsum = fused_ ? partial_ + npart : nullptr;
   k.ih1sq = 1.0 / k.h1sq;
@@ -240,8 +243,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
+  if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
+    nstamps_ = 4 * size_t(nslot_cap_) + 2 * size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
+    PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
+    PE_HIP_CHECK(hipMemset(stamps_, 0, sizeof(unsigned long long) * nstamps_));
+    k.stamps = stamps_;
+  }
   if (fused_) choose_placement();
-  setup_overlap();
+  setup_items();
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -273,44 +282,126 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
 // still being computed.  The sweep keeps its full persistent grid minus
 // `PE_OV_RESERVE` blocks (default 8) left free for the wait / exchange /
 // unpack kernels.  PE_OVERLAP=0 disables.
-void DeviceSolver::setup_overlap() {
+//
+// Every dynamic (order 3) sweep walks such lists, overlap or not.  Item cost
+// estimate (from stamps of the sweep, tools/stamp_probe.py): a row of a
+// strip that contains boundary-band nodes (coefficients evaluated from the
+// chord tables) costs ≈ kGenCost plain rows; an item's rows are its own plus
+// the 4 halo rows it re-reads.  Shards are contiguous chunk ranges of equal
+// estimated cost (consecutive chunks stay on one XCD), and each shard lists
+// its boundary items (overlap) first, then its heavy items in decreasing
+// cost, then the rest chunk-major: the sweep's tail is then made of light
+// items, and waves steal from other shards once their own is empty.
+void DeviceSolver::setup_items() {
   KParams& k = *kp_;
   const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = fused_ && comm_->size() > 1 && nb && !(e && std::atoi(e) == 0);
-  if (!overlap_) return;
-  ov_reserve_ = 8;
-  // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
-  // order (no boundary-first list)
-  if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
-  if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
-  const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - ov_reserve_);
+  if (!fused_ || (k.order != 3 && !overlap_)) return;
+  if (overlap_) {
+    ov_reserve_ = 8;
+    // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
+    // order (no boundary-first list)
+    if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
+    if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
+  }
+  const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - (overlap_ ? ov_reserve_ : 0));
   const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
   const int nchunks = int((blk_.nx + k.ti - 1) / k.ti);
-  std::vector<int> all;
+  double gen_cost = 3.0;
+  if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
+  const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
+  // per-item cost: rows ib-2 .. ie+2, band rows weighted
+  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
+  auto item_cost = [&](int ch, int s) {
+    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+    const int64_t J = -1 + int64_t(s) * dev::kFSW;
+    double c = 0.0;
+    for (int64_t q = ib - 2; q <= ie + 2; ++q) {
+      const int64_t t = q + 1;  // table index of local row q
+      bool gen = false;
+      if (t >= 0 && t < rows_tab) {
+        const int* r = &rowcls_host_[size_t(t) * 4];
+        const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
+        gen = lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
+      }
+      c += gen ? gen_cost : 1.0;
+    }
+    return c;
+  };
+  std::vector<double> cost(size_t(k.nitems));
+  std::vector<double> ccost(size_t(nchunks) + 1, 0.0);  // prefix sums per chunk
+  for (int ch = 0; ch < nchunks; ++ch) {
+    double cc = 0.0;
+    for (int s = 0; s < k.nstrips; ++s) cc += cost[size_t(ch) * k.nstrips + s] = item_cost(ch, s);
+    ccost[size_t(ch) + 1] = ccost[size_t(ch)] + cc;
+  }
+  const double light = double(k.ti + 4);
+  std::vector<int> cut(size_t(nsh) + 1, 0);
+  for (int x = 1; x < nsh; ++x) {
+    const double target = ccost.back() * x / nsh;
+    int c = cut[size_t(x) - 1];
+    while (c < nchunks && ccost[size_t(c) + 1] <= target) ++c;
+    cut[size_t(x)] = c;
+  }
+  cut[size_t(nsh)] = nchunks;
+  // Tail split (dynamic sweeps): the last PE_TAIL_FRAC of every shard's light
+  // items are cut into PE_TAIL_SPLIT shorter items, so the round of items
+  // running when the queues drain is short (the drain is ≈ one item long).
+  double tail_frac = k.order == 3 ? 0.3 : 0.0;
+  int tail_split = 2;
+  if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
+  if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));
+  auto entry = [](int64_t ib, int64_t rows, int s) { return int2{int(ib), s | int(rows << 20)}; };
+  std::vector<int2> all;
   ov_nb_ = 0;
   ov_lnsh_ = nsh;
   for (int x = 0; x < nsh; ++x) {
-    std::vector<int> b, in;
-    for (int ch = x * nchunks / nsh; ch < (x + 1) * nchunks / nsh; ++ch)
+    std::vector<int> b, heavy, in;
+    for (int ch = cut[size_t(x)]; ch < cut[size_t(x) + 1]; ++ch)
       for (int s = 0; s < k.nstrips; ++s) {
+        const int id = ch * k.nstrips + s;
         const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
         const int64_t J = -1 + int64_t(s) * dev::kFSW;
         const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
-        const bool bnd = (blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
-                         (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1);
-        (bnd && !(ov_debug_ & 4) ? b : in).push_back(ch * k.nstrips + s);
+        const bool bnd = overlap_ && !(ov_debug_ & 4) &&
+                         ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
+                          (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1));
+        if (bnd) b.push_back(id);
+        else if (sort_heavy && cost[size_t(id)] > 1.25 * light) heavy.push_back(id);
+        else in.push_back(id);
       }
+    std::stable_sort(heavy.begin(), heavy.end(), [&](int a, int c) { return cost[size_t(a)] > cost[size_t(c)]; });
     ov_lbase_[x] = int(all.size());
     ov_lnb_[x] = int(b.size());
     ov_nb_ += int(b.size());
-    all.insert(all.end(), b.begin(), b.end());
-    all.insert(all.end(), in.begin(), in.end());
+    const size_t nsplit = size_t(tail_frac * double(in.size()) + 0.5);
+    auto push = [&](int id, int parts) {
+      const int ch = id / k.nstrips, s = id % k.nstrips;
+      const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+      const int64_t n = ie - ib + 1;
+      parts = int(std::min<int64_t>(parts, n));
+      for (int q = 0; q < parts; ++q) {
+        const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
+        all.push_back(entry(a0, a1 - a0, s));
+      }
+    };
+    for (int id : b) push(id, 1);
+    for (int id : heavy) push(id, 1);
+    for (size_t i = 0; i < in.size(); ++i) push(in[i], i + nsplit >= in.size() ? tail_split : 1);
   }
   ov_lbase_[nsh] = int(all.size());
-  if (int(all.size()) != k.nitems) throw std::logic_error("overlap item list does not cover the block");
-  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int) * all.size()));
-  PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int) * all.size(), hipMemcpyHostToDevice));
+  if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
+  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+  PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+  // Every dynamic sweep walks the list (the plain one counts no boundary
+  // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).
+  k.ilist = ilist_;
+  k.lnsh = nsh;
+  k.nslots = int(all.size());
+  for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
+  for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+  if (!overlap_) return;
   int least = 0, greatest = 0;
   PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));
@@ -415,6 +506,7 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(halo_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
+  if (stamps_) (void)hipFree(stamps_);
   if (ilist_) (void)hipFree(ilist_);
   if (hs_) (void)hipStreamDestroy(hs_);
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
@@ -425,12 +517,26 @@ DeviceSolver::~DeviceSolver() {
 
 KParams& DeviceSolver::params() { return *kp_; }
 
+void DeviceSolver::clear_stamps() {
+  if (nstamps_) PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
+}
+
+std::vector<unsigned long long> DeviceSolver::stamps() {
+  std::vector<unsigned long long> v(nstamps_);
+  if (nstamps_) {
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    PE_HIP_CHECK(hipMemcpy(v.data(), stamps_, sizeof(unsigned long long) * nstamps_, hipMemcpyDeviceToHost));
+  }
+  return v;
+}
+
 void DeviceSolver::build_tables(int64_t rows_hi, int64_t cols_hi) {
   const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi);
   PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
   const double* col = t.data();
   const double* row = t.data() + (rows_hi + 2) * 4;
-  const std::vector<int> rc = row_classes(col, row, rows_hi, cols_hi);
+  rowcls_host_ = row_classes(col, row, rows_hi, cols_hi);
+  const std::vector<int>& rc = rowcls_host_;
   PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
 }
 

@@ -51,6 +51,11 @@ namespace {
 constexpr int FSW = kFSW;
 
 __device__ __forceinline__ double2 dd(double a, double b) { return make_double2(a, b); }
+// Item-list entry through the constant (scalar) path: one s_load_dwordx2.
+__device__ __forceinline__ int2 cload_i2(const int2* p) {
+  const long long v = cload(reinterpret_cast<const long long*>(p));
+  return make_int2(int(v), int(v >> 32));
+}
 
 // Per-wave LDS copy of the strip's row-table entries (boundary-band rows
 // only read them; LDS reads are counted by lgkmcnt, so they never drain
@@ -182,52 +187,32 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
 // average.  A deferring sweep that is the last one (converged / cap) applies
 // its own term pointwise; a breakdown applies the pending one; the host
 // flushes a pending term (launch_wflush) before w is read.
-template <int OCC, int PF, bool NT, int WM>
+//
+// STAMP — diagnostic build (PE_STAMPS=1, tools/stamp_probe.py): lane 0 of
+// every wave records s_memrealtime at its entry and exit and at the start and
+// end of every item into k.stamps.  Never the production kernel.
+__device__ __forceinline__ unsigned long long rtc() {
+  unsigned long long t;  // one asm statement: never merged or moved by the compiler
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+template <int OCC, int PF, bool NT, int WM, bool STAMP = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
-  if (st->done) return;
+  const unsigned long long t_entry = STAMP ? rtc() : 0ull;
+  // Every state word the sweep needs is loaded up front, together (one
+  // round trip, not a chain behind the `done` test: measured ≈5 µs from
+  // wave entry to the first item with the chain).
+  const int done = st->done, wpend = st->wpend;
+  const double alpha_st = st->alpha;
+  // ---- scalars of this sweep from the previous sweep's global sums ----
+  const Scal sc = sweep_scalars(k, st, par);
+  if (done) return;
   __shared__ double sm[32];
   __shared__ int sflag;
   __shared__ WaveTV tvs[kWPB];
 
-  // ---- scalars of this sweep from the previous sweep's global sums ----
-  const Scal sc = sweep_scalars(k, st, par);
-  const bool first = sc.first;
-  const long long kiter = sc.kiter;
-  const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
-  if (!first) {
-    const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
-    if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
-      if (WM == 2 && st->wpend && !bad) w_pointwise(k, k.x[par ^ 1], st->alpha, 0.0, 0.0, 0.0);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->status = bad ? 4 : 2;
-        st->iter = kiter;
-        st->done = 1;
-        st->wpend = 0;
-      }
-      return;
-    }
-    const bool conv = k.check_tol && diff < k.tol;
-    if (WM == 0 && (conv || kiter >= k.max_iter)) {
-      // last sweep of the solve: only w changes (w += α_k p_k, pointwise)
-      w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->gprev = g;
-        st->rz_cur = g;
-        st->alpha = alpha;
-        st->beta = beta;
-        st->last_diff = diff;
-        if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = diff;
-        st->iter = kiter;
-        st->status = conv ? 1 : 3;
-        st->done = 1;
-        st->wpend = 0;
-      }
-      return;
-    }
-  }
-  // α of the pending term left by the previous (deferring) sweep
-  const double alpha_prev = (WM == 2 && st->wpend) ? st->alpha : 0.0;
 
   // Row pointers at column -1 (uniform, SGPR) + lane offset (unsigned VGPR).
   const double* __restrict__ Xm = k.x[par ^ 1] - 1;
@@ -240,6 +225,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
 
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   WaveTV& tvw = tvs[wid];
+  const int gwave = int(blockIdx.x) * kWPB + wid;
+  if constexpr (STAMP) {
+    if (lane == 0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave] = t_entry;
+  }
   // Item walk.  order 3 (default): dynamic — the chunks (row bands) are
   // split into 8 contiguous ranges, one per XCD shard (blocks are dealt
   // round-robin to the 8 XCDs), and the waves of shard x pull (strip, chunk)
@@ -272,7 +261,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   // (statically, or pulling from its queue under order 3), boundary items
   // first, so the items whose outputs feed the exchange finish in the first
   // round of pulls; the exchange waits for them on st->sig, not for the sweep.
-  const int* lst = nullptr;
+  const int2* lst = nullptr;
   int lnb = 0;
   if (listed) {
     const int nbx = (int(gridDim.x) - xs + nsh - 1) / nsh;
@@ -290,15 +279,102 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     if (lane == 0) v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     return __builtin_amdgcn_readfirstlane(int(v));
   };
-  int item = dyn ? pull() : it0;
-  while (item < ilimit) {
-    unsigned nxt_v = 0;  // next item, requested now, read after this one
+  // Dynamic listed walk: a wave whose shard queue is exhausted steals from
+  // the next shards' queues (each item's sums go to its own slot, so the
+  // reduction does not depend on who computed it): no XCD idles while
+  // another still holds items.  The host orders every shard's list
+  // boundary items (overlap), then heavy items, then the rest chunk-major,
+  // and cuts the shards at equal estimated cost (setup_items).
+  int sh = xs, visited = 1;
+  auto next_shard = [&]() -> bool {
+    if (!(dyn && listed) || visited >= nsh) return false;
+    sh = sh + 1 == nsh ? 0 : sh + 1;
+    ++visited;
+    lst = k.ilist + k.lbase[sh];
+    ilimit = k.lbase[sh + 1] - k.lbase[sh];
+    lnb = k.lnb[sh];
+    head = &st->qhead[sh][0];
+    return true;
+  };
+  // Every wave's first item is static (its index within the shard); the
+  // queue hands out the items after the first round, so a pull returns v and
+  // the item is v + (waves of that shard).  The next item is requested when
+  // an item starts and its list entry is fetched right after the item's
+  // prologue (the atomic has returned by then), so an item boundary waits on
+  // neither.
+  auto shard_waves = [&](int x) { return ((int(gridDim.x) - x + nsh - 1) / nsh) * kWPB; };
+  int item = it0;
+  // prefetched list entry of `item` (have_next: valid); the first one is
+  // requested before the scalar checks below wait for the state loads
+  bool have_next = listed && it0 < ilimit;
+  int2 enext = have_next ? cload_i2(lst + it0) : make_int2(0, 0);
+
+  const bool first = sc.first;
+  const long long kiter = sc.kiter;
+  const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
+  if (!first) {
+    const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
+    if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
+      if (WM == 2 && wpend && !bad) w_pointwise(k, k.x[par ^ 1], alpha_st, 0.0, 0.0, 0.0);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->status = bad ? 4 : 2;
+        st->iter = kiter;
+        st->done = 1;
+        st->wpend = 0;
+      }
+      return;
+    }
+    const bool conv = k.check_tol && diff < k.tol;
+    if (WM == 0 && (conv || kiter >= k.max_iter)) {
+      // last sweep of the solve: only w changes (w += α_k p_k, pointwise)
+      w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
+      if (blockIdx.x == 0 && threadIdx.x == 0) {
+        st->gprev = g;
+        st->rz_cur = g;
+        st->alpha = alpha;
+        st->beta = beta;
+        st->last_diff = diff;
+        if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = diff;
+        st->iter = kiter;
+        st->status = conv ? 1 : 3;
+        st->done = 1;
+        st->wpend = 0;
+      }
+      return;
+    }
+  }
+  // α of the pending term left by the previous (deferring) sweep
+  const double alpha_prev = (WM == 2 && wpend) ? alpha_st : 0.0;
+  for (;;) {
+    if (item >= ilimit) {
+      if (!next_shard()) break;
+      item = pull() + shard_waves(sh);
+      have_next = false;
+      continue;
+    }
+    unsigned nxt_v = 0;  // next item, requested now, read after the prologue
     if (dyn && lane == 0) nxt_v = __hip_atomic_fetch_add(head, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const int gitem = listed ? cload(lst + item) : item;
-    const int s = (k.order == 1 && !listed) ? gitem / nchunks : gitem % k.nstrips;
-    const int ch = chunk0 + ((k.order == 1 && !listed) ? gitem % nchunks : gitem / k.nstrips);
+    // Item geometry: a list entry is {first row, strip | rows << 20} (items
+    // of any height; its sums go to slot = list position), otherwise the
+    // item index is (strip, ti-row chunk) and the slot is chunk-major.
+    int s, ib, ie;
+    int64_t slot;
+    if (listed) {
+      const int2 e = have_next ? enext : cload_i2(lst + item);
+      s = e.y & 0xFFFFF;
+      ib = e.x;
+      ie = min(ib + (e.y >> 20) - 1, nx);
+      slot = int64_t(k.lbase[sh]) + item;
+    } else {
+      const int gitem = item;
+      s = k.order == 1 ? gitem / nchunks : gitem % k.nstrips;
+      const int ch = chunk0 + (k.order == 1 ? gitem % nchunks : gitem / k.nstrips);
+      ib = 1 + ch * k.ti;
+      ie = min(ib + k.ti - 1, nx);
+      slot = int64_t(ch) * k.nstrips + s;
+    }
+    const unsigned long long t_item = STAMP ? rtc() : 0ull;
     const int J = -1 + s * FSW;
-    const int ib = 1 + ch * k.ti, ie = min(ib + k.ti - 1, nx);
     const int c0 = J + 2 * lane;               // odd → 16-byte aligned pair (c0, c0+1)
     const unsigned off = unsigned(c0 + 1);     // element offset from column -1
     const int64_t g0 = k.gj0 + c0;
@@ -308,7 +384,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     const bool o0 = inner && c0 >= 1 && c0 <= ny;
     const bool o1 = inner && c0 + 1 <= ny;
     const int jl0 = 2 * lane;
-    {  // strip chord entries → LDS (band rows only)
+    // Strip chord entries → LDS, read by boundary-band rows only: staged only
+    // when the item has band rows in this strip (a few % of items).
+    bool tv_ok = false;
+    auto stage_tv = [&]() {
       const double* t0 = k.rowT + (c0 + 1) * 4;
       const double4 a = *reinterpret_cast<const double4*>(t0);
       const double4 b = *reinterpret_cast<const double4*>(t0 + 4);
@@ -322,19 +401,30 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    }
+      tv_ok = true;
+    };
     // Row classes of a 64-row segment, lane l ↔ row segbase+l; band rows as
-    // a scalar bit mask.  Reloaded every FSEG rows (items may be long).
+    // a scalar bit mask.  Reloaded every FSEG rows (items may be long).  The
+    // load is issued before the prologue's row loads and waited for after
+    // them (loads complete in order: waiting for it leaves the rows in flight).
     int segbase = 0;
     int4 rcv;
     unsigned long long genmask = 0;
-    auto load_seg = [&](int base) {
+    auto issue_seg = [&](int base) {
       segbase = base;
       const int nr = ie + 3 - base;
       rcv = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
-      genmask = __ballot(lane < nr && has_gen(RowCls{rcv.x, rcv.y, rcv.z, rcv.w}, J, J + 127));
     };
-    load_seg(ib - 2);
+    auto finish_seg = [&]() {
+      const int nr = ie + 3 - segbase;
+      genmask = __ballot(lane < nr && has_gen(RowCls{rcv.x, rcv.y, rcv.z, rcv.w}, J, J + 127));
+      if (genmask != 0 && !tv_ok) stage_tv();
+    };
+    auto load_seg = [&](int base) {
+      issue_seg(base);
+      finish_seg();
+    };
+    issue_seg(ib - 2);
     auto rinfo = [&](int t) {
       RowI r;
       r.t = t;
@@ -388,6 +478,17 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       pq[q] = ld2(xr + poff + off);
       if constexpr (WM == 2) wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
       else wq[q] = dd(0.0, 0.0);
+    }
+    finish_seg();
+    // next item: the pull (older than the prologue loads) has returned
+    int nxt_item = ilimit;
+    have_next = false;
+    if (dyn) {
+      nxt_item = __builtin_amdgcn_readfirstlane(int(nxt_v)) + shard_waves(sh);
+      if (listed && nxt_item < ilimit) {
+        enext = cload_i2(lst + nxt_item);
+        have_next = true;
+      }
     }
     RowI R0 = rinfo(ib - 2), R1 = rinfo(ib - 1);
     double2 pa, pb;  // p_k rows i, i+1 at step i
@@ -503,7 +604,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
 #pragma unroll
         for (int n = 0; n < 7; ++n) v[n] += __shfl_xor(v[n], o, 64);
       if (lane == 0) {
-        double* dst = k.itemsum + 8 * (int64_t(ch) * k.nstrips + s);
+        double* dst = k.itemsum + 8 * slot;
 #pragma unroll
         for (int n = 0; n < 7; ++n) dst[n] = v[n];
       }
@@ -516,7 +617,19 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       if (lane == 0) __hip_atomic_fetch_add(&st->sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
-    item = dyn ? __builtin_amdgcn_readfirstlane(int(nxt_v)) : item + istride;
+    if constexpr (STAMP) {
+      if (lane == 0) {
+        unsigned long long* d = k.stamps + 4 * slot;
+        d[0] = t_item;
+        d[1] = rtc();
+        d[2] = (unsigned long long)gwave | ((unsigned long long)s << 32);
+        d[3] = (unsigned long long)ib | ((unsigned long long)(ie - ib + 1) << 32) | ((unsigned long long)(genmask != 0) << 48);
+      }
+    }
+    item = dyn ? nxt_item : item + istride;
+  }
+  if constexpr (STAMP) {
+    if (lane == 0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc();
   }
   if (persum) return;  // kRed reduces the item sums and finalizes
 
@@ -544,7 +657,7 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
   __shared__ double sm[32];
   __shared__ int sflag;
   const Scal sc = sweep_scalars(k, st, par);
-  const int64_t n = k.nitems, lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
+  const int64_t n = k.nslots, lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   for (int64_t i = lo + threadIdx.x; i < hi; i += TJ) {
     const double4* src = reinterpret_cast<const double4*>(k.itemsum + 8 * i);
@@ -568,6 +681,70 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
       sweep_finalize<WM>(k, st, par, sc, t);
       __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
+  }
+}
+
+// Single-workgroup variant for blocks of few items (multi-rank blocks): no
+// partials, no release/acquire ticket — the multi-block form spends most of
+// its ≈10 µs in that fan-in.  Thread t sums items t, t+1024, … (4 loads in
+// flight), then a fixed wave → workgroup tree: deterministic.
+constexpr int kRed1Threads = 1024;
+template <int WM>
+__global__ __launch_bounds__(kRed1Threads) void kRed1(KParams k, int par) {
+  DevState* st = k.st;
+  const int done = st->done;
+  const Scal sc = sweep_scalars(k, st, par);
+  if (done) return;
+  __shared__ double sm[7][kRed1Threads / 64];
+  const int64_t n = k.nslots;
+  double v[7] = {0, 0, 0, 0, 0, 0, 0};
+  const double4* src = reinterpret_cast<const double4*>(k.itemsum);
+  int64_t i = threadIdx.x;
+  for (; i + 3 * kRed1Threads < n; i += 4 * kRed1Threads) {
+    double4 a[4], b[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      a[u] = src[2 * (i + u * kRed1Threads)];
+      b[u] = src[2 * (i + u * kRed1Threads) + 1];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      v[0] += a[u].x;
+      v[1] += a[u].y;
+      v[2] += a[u].z;
+      v[3] += a[u].w;
+      v[4] += b[u].x;
+      v[5] += b[u].y;
+      v[6] += b[u].z;
+    }
+  }
+  for (; i < n; i += kRed1Threads) {
+    const double4 a = src[2 * i], b = src[2 * i + 1];
+    v[0] += a.x;
+    v[1] += a.y;
+    v[2] += a.z;
+    v[3] += a.w;
+    v[4] += b.x;
+    v[5] += b.y;
+    v[6] += b.z;
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) v[q] += __shfl_xor(v[q], o, 64);
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (lane == 0)
+#pragma unroll
+    for (int q = 0; q < 7; ++q) sm[q][wid] = v[q];
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t[7];
+#pragma unroll
+    for (int q = 0; q < 7; ++q) {
+      t[q] = 0.0;
+      for (int w = 0; w < kRed1Threads / 64; ++w) t[q] += sm[q][w];
+    }
+    sweep_finalize<WM>(k, st, par, sc, t);
   }
 }
 
@@ -657,11 +834,15 @@ static int s_cfg() {
 }
 
 template <int WM, class F>
-static auto with_kS(const KParams&, F&& f) {
+static auto with_kS(const KParams& k, F&& f) {
+  if (k.stamps) return f(kS<0, 4, true, WM, true>);
   switch (s_cfg()) {
     case 1: return f(kS<0, 2, false, WM>);
     case 2: return f(kS<0, 3, true, WM>);
     case 3: return f(kS<0, 5, true, WM>);
+    case 4:  // deferring sweep capped at 3 waves per SIMD (168 VGPRs, a few spills), applying one as default
+      if constexpr (WM == 0) return f(kS<3, 4, true, 0>);
+      else return f(kS<0, 4, true, WM>);
     default: return f(kS<0, 4, true, WM>);
   }
 }
@@ -681,10 +862,19 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
 }
 
 void launch_red(const KParams& k, int par, hipStream_t s) {
+  static const int red1_max = [] {
+    const char* e = std::getenv("PE_RED1_MAX");
+    return e ? std::atoi(e) : 20000;
+  }();
+  if (k.nslots <= red1_max) {
+    if (par == 0) hipLaunchKernelGGL(kRed1<0>, dim3(1), dim3(kRed1Threads), 0, s, k, par);
+    else hipLaunchKernelGGL(kRed1<2>, dim3(1), dim3(kRed1Threads), 0, s, k, par);
+    return;
+  }
   {
     int rb = 16;  // few arrivals on the ticket: the fan-in, not the 2 MB, sets the time
     if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
-    rb = std::max(1, std::min(rb, (k.nitems + 255) / 256));
+    rb = std::max(1, std::min(rb, (k.nslots + 255) / 256));
     if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
     else hipLaunchKernelGGL(kRed<2>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
   }

@@ -90,18 +90,25 @@ struct KParams {
   int64_t wpitch;
   int64_t poff;
   double* x[2];
-  double* itemsum;               // dynamic single-sweep: per-item sums [nitems][8]
+  double* itemsum;               // dynamic single-sweep: per-item sums [nslots][8]
+  int nslots;                    // item-sum slots: list entries (listed walk) or nitems
   long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
   double* hist;                  // keep_history: ‖Δw‖ of iteration k at hist[k-1] (k ≤ hist_n)
   long long hist_n;
-  // Halo/interior overlap: the sweep walks an item list (global chunk-major
-  // indices) split into lnsh shards; shard x owns ilist[lbase[x] .. lbase[x+1])
-  // and its first lnb[x] entries are boundary items (outputs sent to a
-  // neighbour), each of which bumps st->sig once its stores are visible.
-  const int* ilist;
+  // Item lists (dynamic sweeps, setup_items): entries {first row, strip |
+  // rows << 20}, split into lnsh shards; shard x owns ilist[lbase[x] ..
+  // lbase[x+1]) and (halo/interior overlap) its first lnb[x] entries are
+  // boundary items (outputs sent to a neighbour), each of which bumps st->sig
+  // once its stores are visible.
+  const int2* ilist;
   int lnsh;
   int lbase[9];
   int lnb[8];
+  // Diagnostic timeline (PE_STAMPS=1, single-sweep only; null otherwise;
+  // a separate kernel build records it): per item {start, end, wave, block}
+  // in s_memrealtime ticks (100 MHz), then per wave {entry, exit}.
+  // Overwritten by every sweep.
+  unsigned long long* stamps;
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)

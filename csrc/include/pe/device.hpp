@@ -149,11 +149,15 @@ class DeviceSolver {
   const Problem& problem() const { return prob_; }
   int chunk() const { return chunk_; }
   dev::KParams& params();
+  // PE_STAMPS=1 diagnostic timeline of the last sweep (see KParams::stamps);
+  // empty when off.
+  std::vector<unsigned long long> stamps();
+  void clear_stamps();  // stream-ordered: the next sweep's stamps only
 
  private:
   void build_tables(int64_t rows_hi, int64_t cols_hi);
   void set_fused_fields(double* x0, double* x1, double* w);
-  void setup_overlap();
+  void setup_items();  // dynamic item lists per XCD shard (+ halo/interior overlap)
   void choose_placement();
   void enqueue_iteration(int par);
   void enqueue_exchange(int buf);
@@ -175,13 +179,17 @@ class DeviceSolver {
   int64_t xsize_ = 0, wsize_ = 0, plane_ = 0;
   double* tables_ = nullptr;
   int* rowcls_ = nullptr;
+  std::vector<int> rowcls_host_;  // host copy of the row classes (item cost estimates)
   double* halo_ = nullptr;    // send_dn, send_up, recv_dn, recv_up (nx each; ×4 single-sweep)
   int64_t hsize_ = 0;
   double* partial_ = nullptr;
   double* hist_ = nullptr;
+  unsigned long long* stamps_ = nullptr;
+  size_t nstamps_ = 0;
   // halo/interior overlap (multi-rank single-sweep)
   bool overlap_ = false;
-  int* ilist_ = nullptr;  // per shard: boundary items, then interior items
+  int2* ilist_ = nullptr;  // per shard: boundary items, heavy items, the rest (dev::KParams::ilist)
+  int nslot_cap_ = 0;      // item-sum slots allocated
   int ov_lnsh_ = 1, ov_nb_ = 0, ov_reserve_ = 8, ov_debug_ = 0;
   int ov_lbase_[9] = {}, ov_lnb_[8] = {};
   unsigned long long ov_epoch_ = 0;  // overlapped sweeps since the state was last cleared (sig targets)

@@ -1,0 +1,123 @@
+"""Sweep timeline of the single-sweep kernel from in-kernel stamps.
+
+One GPU runs the block of one rank of a P-rank decomposition of 8192²
+(timing-only transport, zero delays, overlap off), with PE_STAMPS=1: a
+diagnostic build of the sweep writes, per work item, s_memrealtime at its
+start and end (100 MHz) and, per wave, its entry and exit.  The last sweep's
+stamps are read back and summarised: kernel span, wave entry spread, first
+item latency, item duration distribution, gaps between a wave's items, and
+the tail (how long the chip runs partly idle at the end).  The stamped
+build's own run time is not a measurement of the real kernel: read shares.
+
+    PROBE_CFG=8:aspect,1:aspect PROBE_ENV="PE_TI=8;PE_TI=16" python tools/stamp_probe.py
+"""
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ["PE_STAMPS"] = "1"
+os.environ["PE_OVERLAP"] = "0"
+
+import poisson_ellipse_openmp_mpi_cuda_amd as pe  # noqa: E402
+from poisson_ellipse_openmp_mpi_cuda_amd._loader import native  # noqa: E402
+from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D  # noqa: E402
+
+
+def pct(a, q):
+    return float(np.percentile(a, q)) if len(a) else float("nan")
+
+
+def summarise(st: np.ndarray, nitems: int) -> str:
+    it = st[: 4 * nitems].reshape(nitems, 4).astype(np.int64)
+    geo = it[:, 3].copy()
+    strip = it[:, 2] >> 32
+    it[:, 2] &= 0xFFFFFFFF  # wave id
+    wv_all = st[4 * nitems :].reshape(-1, 2).astype(np.int64)
+    live = wv_all[:, 0] > 0
+    wv = wv_all[live]
+    t0 = wv[:, 0].min()
+    us = lambda x: x / 100.0  # 100 MHz ticks → µs  # noqa: E731
+    end = max(wv[:, 1].max(), it[:, 1].max())
+    span = us(end - t0)
+    dur = us(it[:, 1] - it[:, 0])
+    out = [f"  span {span:7.1f} us  waves {len(wv)}  items {nitems}  items/wave {nitems / len(wv):.1f}"]
+    ent = us(wv[:, 0] - t0)
+    out.append(f"  wave entry after the first: median {np.median(ent):6.1f}  p99 {pct(ent, 99):6.1f}  max {ent.max():6.1f} us")
+    ex = us(wv[:, 1] - t0)
+    out.append(f"  wave exit: min {ex.min():6.1f}  p10 {pct(ex, 10):6.1f}  median {np.median(ex):6.1f}  max {ex.max():6.1f} us"
+               f"  -> tail (max - median) {ex.max() - np.median(ex):5.1f} us")
+    med = np.median(dur)
+    out.append(f"  item duration: p10 {pct(dur, 10):6.2f}  median {med:6.2f}  p90 {pct(dur, 90):6.2f}"
+               f"  p99 {pct(dur, 99):6.2f}  max {dur.max():6.2f} us")
+    slow = dur > 1.5 * med
+    out.append(f"  items > 1.5x median: {slow.sum()} ({100 * slow.mean():.1f} %), {100 * dur[slow].sum() / dur.sum():.1f} % of item time")
+    order = np.lexsort((it[:, 0], it[:, 2]))
+    first_lat, gaps = [], []
+    prev_w, prev_end = -1, 0
+    for s0, s1, w, _b in it[order]:
+        if w != prev_w:
+            if 0 <= w < len(wv_all) and wv_all[w, 0] > 0:
+                first_lat.append(us(s0 - wv_all[w, 0]))
+            prev_w = w
+        else:
+            gaps.append(us(s0 - prev_end))
+        prev_end = s1
+    out.append(f"  first item start after wave entry: median {np.median(first_lat):6.2f}  p90 {pct(first_lat, 90):6.2f} us")
+    if gaps:
+        out.append(f"  gap between a wave's items: median {np.median(gaps):6.3f}  p90 {pct(gaps, 90):6.3f} us")
+    # time profile of busy waves (10 bins)
+    edges = np.linspace(t0, end, 11)
+    prof = []
+    for a, b in zip(edges[:-1], edges[1:]):
+        ov = np.clip(np.minimum(it[:, 1], b) - np.maximum(it[:, 0], a), 0, None).sum()
+        prof.append(ov / ((b - a) * len(wv)))
+    out.append("  busy waves per tenth of the span: " + " ".join(f"{p:4.2f}" for p in prof))
+    out.append(f"  busy fraction (item time / waves x span) {dur.sum() / (len(wv) * span):5.3f}")
+    late = np.argsort(it[:, 1])[-8:]
+    for i in late:
+        out.append(f"    late item: start {us(it[i, 0] - t0):6.1f} end {us(it[i, 1] - t0):6.1f} us  rows {geo[i] & 0xFFFFFFFF}"
+                   f"+{(geo[i] >> 32) & 0xFFFF}  strip {strip[i]}  band {geo[i] >> 48}  wave {it[i, 2]}")
+    band = (geo >> 48) == 1
+    if band.any():
+        out.append(f"  band items: {band.sum()}  duration median {np.median(dur[band]):6.2f} us; others {np.median(dur[~band]):6.2f} us")
+    return "\n".join(out)
+
+
+def main():
+    nat = native()
+    configs = [(int(c.split(":")[0]), c.split(":")[1]) for c in os.environ.get("PROBE_CFG", "8:aspect,1:aspect").split(",")]
+    envs = [e.strip() for e in os.environ.get("PROBE_ENV", "").split(";")]
+    prob = pe.EllipseProblem(8192, 8192)
+    for P, spec in configs:
+        g = D.grid(P, 8192, 8192, spec)
+        blk = nat.decompose(8192, 8192, g, P // 2)
+        for env in envs:
+            kv = dict(x.split("=") for x in env.split()) if env else {}
+            saved = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
+            opt = nat.SolveOptions()
+            opt.check_tol = False
+            comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
+            s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
+            s.reset()
+            dt = s.time_iterations(40, False)
+            print(f"P={P} {g.Px}x{g.Py} block {blk.nx}x{blk.ny} [{env or 'default'}] ti={s.ti} order={s.order}: "
+                  f"{dt / 40 * 1e6:.1f} us/iter (stamped build)", flush=True)
+            for sweep in ("deferring", "applying"):  # iterations alternate the two sweep variants
+                s.clear_stamps()
+                s.run_iterations(1, False)
+                st = np.asarray(s.stamps())
+                print(f" one {sweep}-parity sweep:")
+                print(summarise(st, s.nitems), flush=True)
+            del s, comm
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+
+
+if __name__ == "__main__":
+    main()
