@@ -157,6 +157,8 @@ def main() -> int:
             "parallelism": f"2d-decomp {blk.Px}x{blk.Py} (RCCL)" if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
             "algo": "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else "classic (2 kernels, 2 allreduces / iter)",
+            "transport": comm.name if comm is not None else "none",
+            "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
         },
         "valid": valid,
     }

@@ -414,6 +414,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("order", [](DeviceSolver& s) { return s.params().order; })
+      .def_property_readonly("xr", [](DeviceSolver& s) { return s.params().xr.peers != nullptr; },
+                             "True when the sweep sums its scalars over ranks itself (P2P transport)")
       .def_property_readonly("nitems", [](DeviceSolver& s) { return s.params().nslots; })
       .def("stamps",
            [](DeviceSolver& s) {

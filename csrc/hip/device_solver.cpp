@@ -251,6 +251,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
   if (fused_) choose_placement();
   setup_items();
+  // In-sweep cross-rank reduction (after the placement search, whose sweeps
+  // are local and differ in number between ranks).  PE_XR=0 keeps the
+  // separate allreduce launch.
+  if (fused_ && comm_->size() > 1 && comm_->peer_sum()) {
+    const char* e = std::getenv("PE_XR");
+    if (!(e && std::atoi(e) == 0)) k.xr = *comm_->peer_sum();
+  }
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -608,6 +615,12 @@ void DeviceSolver::enqueue_pack(int buf) { dev::launch_pack(*kp_, buf, stream_);
 void DeviceSolver::enqueue_unpack(int buf) { dev::launch_unpack(*kp_, buf, stream_); }
 void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 
+// Cross-rank sum of sweep `par`'s 7 sums: nothing to enqueue when the sweep
+// sums them over ranks itself (k.xr, P2P transport).
+void DeviceSolver::enqueue_fs_reduce(int par) {
+  if (!kp_->xr.peers) comm_->allreduce_sum(st_->fs[par], 7, stream_);
+}
+
 void DeviceSolver::enqueue_iteration(int par) {
   if (fused_ && overlap_) {
     KParams ko = *kp_;
@@ -623,7 +636,7 @@ void DeviceSolver::enqueue_iteration(int par) {
     if (ov_debug_ & 2) {
       dev::launch_wait_sig(ko, target, stream_);
       enqueue_exchange(par);
-      comm_->allreduce_sum(st_->fs[par], 7, stream_);
+      enqueue_fs_reduce(par);
       return;
     }
     dev::launch_wait_sig(ko, target, hs_);  // the exchange starts once they are stored
@@ -633,13 +646,13 @@ void DeviceSolver::enqueue_iteration(int par) {
     }
     PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
     PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
-    comm_->allreduce_sum(st_->fs[par], 7, stream_);
+    enqueue_fs_reduce(par);
     return;
   }
   if (fused_) {
     dev::launch_S(*kp_, par, stream_);
     enqueue_exchange(par);
-    comm_->allreduce_sum(st_->fs[par], 7, stream_);
+    enqueue_fs_reduce(par);
     return;
   }
   dev::launch_F(*kp_, par, opt_.variant, stream_);
@@ -825,7 +838,7 @@ void DeviceSolver::reset() {
     enqueue_exchange(0);
     dev::launch_S(*kp_, 1, stream_);
     enqueue_exchange(1);
-    comm_->allreduce_sum(st_->fs[1], 7, stream_);
+    enqueue_fs_reduce(1);
     return;
   }
   comm_->exchange(halo_plan(), stream_);
@@ -895,7 +908,7 @@ SolveResult DeviceSolver::solve() {
         PE_HIP_CHECK(hipEventRecord(ev[1], stream_));
         enqueue_exchange(par);
         PE_HIP_CHECK(hipEventRecord(ev[2], stream_));
-        comm_->allreduce_sum(st_->fs[par], 7, stream_);
+        enqueue_fs_reduce(par);
         PE_HIP_CHECK(hipEventRecord(ev[3], stream_));
         PE_HIP_CHECK(hipEventSynchronize(ev[3]));
         float t[3];

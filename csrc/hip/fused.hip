@@ -37,6 +37,7 @@
 #include <cstdlib>
 
 #include "kcommon.hpp"
+#include "peer_sum.hpp"
 
 // The single-sweep formulation does not reproduce the reference rounding
 // anyway: let the compiler contract a*b+c into v_fma_f64.
@@ -173,6 +174,28 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
   }
 #pragma unroll
   for (int x = 0; x < 8; ++x) __hip_atomic_store(&st->qhead[x][0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// The final reduction block of a sweep (every thread calls it; the local
+// sums t are valid in thread 0): with a P2P transport (k.xr) the 7 sums are
+// summed over ranks right here (peer_sum.hpp) — the iteration then needs no
+// allreduce launch — then thread 0 updates the state.
+template <int WM>
+__device__ __forceinline__ void finalize_block(const KParams& k, DevState* st, int par, const Scal& sc,
+                                               double (&t)[7]) {
+  __shared__ double v[8];
+  __shared__ unsigned long long sseq;
+  __shared__ int sok;
+  if (k.xr.peers) {
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int n = 0; n < 7; ++n) v[n] = t[n];
+    peer_sum_block(k.xr, v, 7, &sseq, &sok);
+    if (threadIdx.x == 0)
+#pragma unroll
+      for (int n = 0; n < 7; ++n) t[n] = v[n];
+  }
+  if (threadIdx.x == 0) sweep_finalize<WM>(k, st, par, sc, t);
 }
 
 // OCC > 0 caps registers for OCC waves per SIMD (amdgpu_waves_per_eu); PF =
@@ -641,10 +664,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   if (arrive_last(&st->ticket[0], gridDim.x, &sflag)) {
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
-    if (threadIdx.x == 0) {
-      sweep_finalize<WM>(k, st, par, sc, t);
-      __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    finalize_block<WM>(k, st, par, sc, t);
+    if (threadIdx.x == 0) __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -677,10 +698,8 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
   if (arrive_last(&st->ticket[1], gridDim.x, &sflag)) {
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
-    if (threadIdx.x == 0) {
-      sweep_finalize<WM>(k, st, par, sc, t);
-      __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    finalize_block<WM>(k, st, par, sc, t);
+    if (threadIdx.x == 0) __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -737,15 +756,15 @@ __global__ __launch_bounds__(kRed1Threads) void kRed1(KParams k, int par) {
 #pragma unroll
     for (int q = 0; q < 7; ++q) sm[q][wid] = v[q];
   __syncthreads();
+  double t[7];
   if (threadIdx.x == 0) {
-    double t[7];
 #pragma unroll
     for (int q = 0; q < 7; ++q) {
       t[q] = 0.0;
       for (int w = 0; w < kRed1Threads / 64; ++w) t[q] += sm[q][w];
     }
-    sweep_finalize<WM>(k, st, par, sc, t);
   }
+  finalize_block<WM>(k, st, par, sc, t);
 }
 
 // Apply a pending α_k p_k (p_k = p-plane of x[wpar]) before w is read.
@@ -840,9 +859,6 @@ static auto with_kS(const KParams& k, F&& f) {
     case 1: return f(kS<0, 2, false, WM>);
     case 2: return f(kS<0, 3, true, WM>);
     case 3: return f(kS<0, 5, true, WM>);
-    case 4:  // deferring sweep capped at 3 waves per SIMD (168 VGPRs, a few spills), applying one as default
-      if constexpr (WM == 0) return f(kS<3, 4, true, 0>);
-      else return f(kS<0, 4, true, WM>);
     default: return f(kS<0, 4, true, WM>);
   }
 }

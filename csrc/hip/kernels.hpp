@@ -49,6 +49,18 @@ struct DevState {
   unsigned long long sig;  // overlap: boundary items stored, cumulative over the solve's sweeps
 };
 
+// One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
+// peers[r] = rank r's buffer (2 × P slots of kP2PSlot doubles: n ≤ kP2PSlot-1
+// values + a sequence flag) mapped into this process, seq = this rank's
+// reduction counter (device), timeout in s_memrealtime ticks (100 MHz).
+constexpr int kP2PSlot = 16;
+struct PeerSum {
+  double* const* peers;
+  unsigned long long* seq;
+  int me, P;
+  long long timeout_ticks;
+};
+
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
 // lj ∈ [0, ny+1], element = base + li*pitch + lj.
 struct KParams {
@@ -109,6 +121,10 @@ struct KParams {
   // in s_memrealtime ticks (100 MHz), then per wave {entry, exit}.
   // Overwritten by every sweep.
   unsigned long long* stamps;
+  // Cross-rank reduction inside the sweep (PE_XR, with a P2P comm): the final
+  // reduction block sums the 7 sums over ranks itself (xr.peers == null: the
+  // host enqueues the comm's allreduce instead).
+  PeerSum xr;
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
@@ -137,12 +153,8 @@ void launch_unpack(const KParams& k, int b, hipStream_t s);
 // running sweep is in L2) or the solve is done, then write every XCD's L2
 // back.  Put on the halo stream ahead of the exchange.
 void launch_wait_sig(const KParams& k, unsigned long long target, hipStream_t s);
-// One-shot P2P allreduce (p2p.hip): every rank's receive buffer holds
-// 2 × P slots of kP2PSlot doubles (n ≤ kP2PSlot-1 values + a sequence flag);
-// peers[r] = rank r's buffer mapped into this process.  P ≤ 64.
-constexpr int kP2PSlot = 16;
-void launch_p2p_sum(double* d, int n, double* const* peers, int me, int P, unsigned long long seq, double timeout_s,
-                    hipStream_t s);
+// One-shot P2P allreduce kernel (p2p.hip) of n ≤ kP2PSlot-1 doubles, in place.  P ≤ 64.
+void launch_p2p_sum(double* d, int n, const PeerSum& ps, hipStream_t s);
 // Group-comm helper: out[i] = Σ_r in_r[i] (or max), written to every rank's buffer.
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s);
 // Debug/test ops (single-shot, no convergence logic).

@@ -22,6 +22,10 @@
 
 namespace pe {
 
+namespace dev {
+struct PeerSum;
+}  // namespace dev
+
 [[noreturn]] void hip_fail(hipError_t e, const char* expr, const char* file, int line);
 int device_count();
 void set_device(int dev);
@@ -45,6 +49,9 @@ class DeviceComm {
   // abort the communicator so peers blocked in it fail instead of hanging.
   virtual void check_async() {}
   virtual void abort() {}
+  // One-shot P2P sum tables (P2P transport only): the single-sweep solver
+  // then sums its per-iteration scalars over ranks inside the sweep.
+  virtual const dev::PeerSum* peer_sum() const { return nullptr; }
 };
 
 class SelfDeviceComm final : public DeviceComm {
@@ -160,6 +167,7 @@ class DeviceSolver {
   void setup_items();  // dynamic item lists per XCD shard (+ halo/interior overlap)
   void choose_placement();
   void enqueue_iteration(int par);
+  void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
   void enqueue_exchange(int buf);
   void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
   void enqueue_chunk(int iters);

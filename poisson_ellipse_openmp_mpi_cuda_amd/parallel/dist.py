@@ -85,8 +85,14 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
     Default: RCCL over xGMI, unique id via the torch store.  PE_COMM=host
     selects the host-staged gloo transport (several ranks on one GPU — RCCL
     refuses duplicate devices — for testing the multi-process path on a
-    single-GPU box).  PE_ALLREDUCE=p2p runs the per-iteration sums as a
-    one-shot peer-to-peer kernel over IPC-mapped buffers instead."""
+    single-GPU box).
+
+    Per-iteration sums (PE_ALLREDUCE): "p2p" (default on RCCL jobs) maps
+    every peer's receive buffer over xGMI (IPC) and lets the solver's sweep
+    sum its scalars over ranks inside its final reduction block — no
+    allreduce launch per iteration (PE_XR=0: a one-shot P2P kernel instead).
+    The set-up self-tests and every rank falls back to RCCL's allreduce if
+    any rank cannot use it.  "rccl": ncclAllReduce on the device scalars."""
     nat = native()
     nat.set_device(ctx.local_rank % max(1, nat.device_count()))
     if ctx.world == 1:
@@ -105,7 +111,8 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
         else:
             uid = store.get(key)
         comm = nat.make_rccl_comm(bytes(uid), ctx.rank, ctx.world)
-    if os.environ.get("PE_ALLREDUCE", "rccl") == "p2p":
+    default = "rccl" if os.environ.get("PE_COMM", "rccl") == "host" else "p2p"
+    if os.environ.get("PE_ALLREDUCE", default) == "p2p":
         nat.use_p2p_allreduce(comm)  # one-shot xGMI allreduce of the per-iteration sums
     return comm
 

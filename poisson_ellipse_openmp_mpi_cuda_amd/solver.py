@@ -56,6 +56,7 @@ class SolveReport:
     nonfinite: bool = False
     history: Optional[list] = None  # ‖Δw‖ per iteration (keep_history=True)
     comm: str = ""  # device transport of a multi-rank HIP run (e.g. "rccl", "p2p-allreduce+rccl")
+    xr: bool = False  # the sweep sums its scalars over ranks itself (P2P transport, no allreduce launch)
 
     @property
     def iters_per_s(self) -> float:
@@ -186,4 +187,5 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
             w = _dist.gather_blocks(_dist.init(), prob, blk, wl)
     rep = _report("hip", prob, res, world, 1, init, w, rank)
     rep.comm = comm.name if comm is not None else "self"
+    rep.xr = bool(solver.xr)
     return rep

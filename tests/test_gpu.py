@@ -294,17 +294,21 @@ def test_two_process_device_path_host_staged(gpu):
 
 @pytest.mark.parametrize("nproc,decomp,overlap,allreduce", [(4, "aspect", "1", "rccl"), (3, "aspect", "1", "rccl"),
                                                         (4, "aspect", "0", "rccl"), (4, "aspect", "1", "p2p"),
-                                                        (2, "aspect", "0", "p2p")])
+                                                        (2, "aspect", "0", "p2p"), (4, "aspect", "1", "p2p-kernel"),
+                                                        (3, "rows", "0", "p2p")])
 def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
     rows through the x phase of the single-sweep halo) — and 3×1 — match the
     single-process solution (gathered w); with and without the boundary /
     interior overlap on two streams; with the per-iteration sums through the
-    host-staged transport or the one-shot P2P allreduce kernel (IPC-mapped
-    buffers of the other processes)."""
+    host-staged transport, through the P2P transport (IPC-mapped buffers of
+    the other processes) summed inside the sweep's final reduction block
+    ("p2p"), or through the standalone one-shot P2P kernel ("p2p-kernel",
+    PE_XR=0)."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="60")
+    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce.split("-")[0],
+               PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1")
     outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}_{allreduce}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -314,7 +318,8 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     assert out.returncode == 0, out.stderr[-3000:]
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
-    assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce == "p2p" else "host-staged")
+    assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
+    assert d["xr"] == (allreduce == "p2p")
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
