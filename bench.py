@@ -48,7 +48,7 @@ def main() -> int:
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--grid", type=int, nargs="+", default=[8192, 8192])
-    ap.add_argument("--decomp", default="aspect", help="aspect | reference | rows | cols | <Px>x<Py>")
+    ap.add_argument("--decomp", default="device", help="device | aspect | reference | rows | cols | <Px>x<Py>")
     ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solve")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused"))

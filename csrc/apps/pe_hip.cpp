@@ -1,7 +1,7 @@
 // pe_hip — the stage-4 executable (MPI + CUDA in the reference) rebuilt for
 // MI355X: one process per GPU, RCCL over xGMI, device-resident PCG.
 //
-//   pe_hip [--tol 1e-6] [--max-iter K] [--decomp aspect|reference]
+//   pe_hip [--tol 1e-6] [--max-iter K] [--decomp device|aspect|reference|rows|cols|PxxPy]
 //          [--init zero|random] [--seed S] [--variant 0|1] [--algo auto|classic|fused] [--chunk K]
 //          [--no-graph] [--timing] [--vranks P] [--json] [M N]
 //
@@ -84,7 +84,7 @@ int main(int argc, char** argv) {
   opt.checkpoint_every = args.geti("checkpoint-every", 0);
   opt.resume_path = args.get("resume", "");
   opt.log_every = int(args.geti("log-every", 0));
-  const std::string decomp = args.get("decomp", "aspect");
+  const std::string decomp = args.get("decomp", "device");
 
   const int rank = env_int("PE_RANK", "RANK", 0);
   const int size = env_int("PE_WORLD_SIZE", "WORLD_SIZE", 1);

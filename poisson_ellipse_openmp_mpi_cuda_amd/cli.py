@@ -32,8 +32,9 @@ def build_parser():
     ap.add_argument("--backend", choices=BACKENDS, default=os.environ.get("PE_BACKEND", "hip"))
     ap.add_argument("--ranks", type=int, default=1, help="thread-ranks (ranks) or virtual ranks (hip-group)")
     ap.add_argument("--threads", type=int, default=int(os.environ.get("OMP_NUM_THREADS", "1") or 1))
-    ap.add_argument("--decomp", default="aspect",
-                    help="aspect | reference | rows | cols | <Px>x<Py> (e.g. 4x2)")
+    ap.add_argument("--decomp", default=None,
+                    help="aspect | reference | rows | cols | device | <Px>x<Py> (e.g. 4x2); "
+                         "default: device for the GPU backends, aspect otherwise")
     ap.add_argument("--init", choices=("zero", "random"), default="zero")
     ap.add_argument("--seed", type=int, default=1234)
     ap.add_argument("--tol", type=float, default=1e-6)

@@ -9,6 +9,8 @@ is one of
   x-direction rows over strided y-direction columns (8 ranks on 8192² →
   4×2, 2 ranks on 4096² → 2×1, the BASELINE.json configurations),
 * ``rows`` / ``cols`` — P×1 / 1×P slabs,
+* ``device`` — the GPU solver's default: row slabs while every rank keeps
+  ≥ 512 rows (one contiguous halo message per side), else ``aspect``,
 * ``"<Px>x<Py>"`` — an explicit grid (``"4x2"``).
 """
 
@@ -17,6 +19,12 @@ from __future__ import annotations
 from .._loader import native
 
 MODES = ("aspect", "reference", "rows", "cols")
+SPECS = MODES + ("device",)
+
+
+def default_spec(backend: str) -> str:
+    """Decomposition used when none is given: "device" for the GPU backends."""
+    return "device" if backend in ("hip", "hip-group") else "aspect"
 
 
 def mode_enum(mode: str):

@@ -104,7 +104,7 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         history=list(res.history) if len(res.history) else None)
 
 
-def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str = "aspect",
+def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str | None = None,
           init: str = "zero", seed: int = 1234, return_w: bool = False, device: str = "cuda", **kw) -> SolveReport:
     """Solve the fictitious-domain Poisson problem with the chosen backend.
 
@@ -114,6 +114,7 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     """
     if backend not in BACKENDS:
         raise ValueError(f"backend must be one of {BACKENDS}")
+    decomp = decomp or _decomp.default_spec(backend)
     nat = native()
     P = prob.to_native()
     if backend in ("serial", "omp", "ranks"):
