@@ -162,13 +162,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.check_tol = opt_.check_tol ? 1 : 0;
   // Failure-detection hooks: PE_FAULT_INJECT=nan@iter:K poisons
   // the reduced sums after iteration K (the solver must stop with a
-  // non-finite status), PE_FAULT_INJECT=stall makes the host believe the
-  // device never finishes (the watchdog must fire); PE_WATCHDOG_S sets the
+  // non-finite status), PE_FAULT_INJECT=stall (or stall@rank:R, one rank
+  // only) makes the host believe the device never finishes (the watchdog
+  // must fire); PE_WATCHDOG_S sets the
   // no-progress limit of the host loop.
   if (const char* e = std::getenv("PE_FAULT_INJECT")) {
     const std::string f = e;
     if (f.rfind("nan@iter:", 0) == 0) k.fault_iter = std::atoll(f.c_str() + 9);
     if (f == "stall") fault_stall_ = true;
+    // stall@rank:R — only rank R hangs (its watchdog fires and aborts the
+    // communicator; the peers then see the transport fail, not a hang)
+    if (f.rfind("stall@rank:", 0) == 0 && std::atoi(f.c_str() + 11) == blk_.rank) fault_stall_ = true;
   }
   if (const char* e = std::getenv("PE_WATCHDOG_S")) watchdog_s_ = std::atof(e);
   if (opt_.keep_history) {  // per-iteration ‖Δw‖ on the device (capped at 2²⁴ iterations)

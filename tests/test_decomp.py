@@ -105,3 +105,38 @@ def test_device_spec_falls_back_to_aspect_for_thin_slabs():
     assert D.process_grid(8, 8192, 8192, "device") == (8, 1)
     assert D.process_grid(16, 4096, 4096, "device") == D.process_grid(16, 4096, 4096, "aspect")
     assert D.default_spec("hip") == "device" and D.default_spec("ranks") == "aspect"
+
+
+# property test over P = 1..64 and random grids — coverage,
+# disjointness, sizes within 1, remainder to low coordinates, neighbour
+# symmetry, for every process-grid spec the solvers accept.
+from hypothesis import given, settings, strategies as st  # noqa: E402
+
+
+@settings(max_examples=150, deadline=None)
+@given(P=st.integers(1, 64), M=st.integers(3, 400), N=st.integers(3, 400),
+       mode=st.sampled_from(["reference", "aspect", "device", "rows", "cols"]))
+def test_partition_properties_random(P, M, N, mode):
+    blks = D.blocks(M, N, P, mode)
+    assert len(blks) == P
+    Px, Py = blks[0].Px, blks[0].Py
+    cover = np.zeros((M - 1, N - 1), dtype=np.int32)
+    for b in blks:
+        # empty blocks only when a direction has more ranks than interior
+        # lines (the reference runs them too: its loops are just empty)
+        assert b.nx >= 1 or Px > M - 1
+        assert b.ny >= 1 or Py > N - 1
+        cover[b.i0 - 1:b.i1, b.j0 - 1:b.j1] += 1
+    assert (cover == 1).all()
+    Px, Py = blks[0].Px, blks[0].Py
+    assert Px * Py == P
+    nx = [next(b.nx for b in blks if b.px == x) for x in range(Px)]
+    ny = [next(b.ny for b in blks if b.py == y) for y in range(Py)]
+    assert max(nx) - min(nx) <= 1 and max(ny) - min(ny) <= 1
+    assert nx == sorted(nx, reverse=True) and ny == sorted(ny, reverse=True)
+    opp = {0: 1, 1: 0, 2: 3, 3: 2}
+    for b in blks:
+        assert b.rank == b.px + b.py * Px  # x-fastest rank order (reference :97-133)
+        for d, n in enumerate(b.nbr):
+            if n >= 0:
+                assert blks[n].nbr[opp[d]] == b.rank

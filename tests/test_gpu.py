@@ -341,6 +341,31 @@ def test_watchdog_fires_on_stall(gpu, monkeypatch):
         solve(EllipseProblem(200, 300), backend="hip")
 
 
+def test_one_rank_stall_fails_the_job(gpu):
+    """PE_FAULT_INJECT=stall@rank:1 (SURVEY §5 hang@rank hook): rank 1's host
+    loop never sees the device finish, its watchdog fires, the process exits
+    non-zero and torchrun tears the job down — the job fails, it does not
+    hang (the process group is killed if it ever did)."""
+    import signal
+
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_FAULT_INJECT="stall@rank:1", PE_WATCHDOG_S="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+           "poisson_ellipse_openmp_mpi_cuda_amd", "--quiet", "200", "300"]
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=90)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        pytest.fail("a stalled rank hung the job instead of failing it")
+    assert p.returncode != 0
+    assert "watchdog" in err, err[-3000:]
+
+
 @pytest.mark.parametrize("algo", ["fused", "classic"])
 def test_checkpoint_resume_bitwise(gpu, algo, tmp_path):
     prob = EllipseProblem(400, 600)
