@@ -31,7 +31,7 @@ int main(int argc, char** argv) {
   if (args.flag("help")) {
     std::puts("usage: pe_cpu [--backend serial|omp|ranks] [--ranks P] [--threads T] [--threads-sweep L]\n"
               "              [--norm weighted|unweighted] [--decomp reference|aspect] [--init zero|random]\n"
-              "              [--seed S] [--tol D] [--max-iter K] [--stage stage0..3] [--json] [M N]");
+              "              [--seed S] [--tol D] [--max-iter K] [--stage stage0..3] [--grids 10,20,40] [--json] [M N]");
     return 0;
   }
   Problem P;
@@ -42,8 +42,13 @@ int main(int argc, char** argv) {
   }
   P.tol = args.getd("tol", 1e-6);
   P.max_iter = args.geti("max-iter", -1);
-  P.norm = args.get("norm", "weighted") == "unweighted" ? Norm::Unweighted : Norm::Weighted;
   const std::string backend = args.get("backend", "serial");
+  std::string stage = args.get("stage", "");
+  // stage0 (Withoutopenmp1.cpp:106-196) stops on the unweighted ‖Δw‖ and, run
+  // without M N, loops over the grids {10, 20, 40}² (:177)
+  P.norm = args.get("norm", stage == "stage0" ? "unweighted" : "weighted") == "unweighted" ? Norm::Unweighted
+                                                                                          : Norm::Weighted;
+  std::vector<int> grids = parse_list(args.get("grids", (stage == "stage0" && pos.size() < 2) ? "10,20,40" : ""));
   int ranks = int(args.geti("ranks", 1));
   int threads = int(args.geti("threads", backend == "omp" ? 4 : 1));
   const std::string decomp = args.get("decomp", "reference");
@@ -51,7 +56,7 @@ int main(int argc, char** argv) {
   opt.init = args.get("init", "zero") == "random" ? Init::Random : Init::Zero;
   opt.seed = uint64_t(args.geti("seed", 1234));
   opt.log_every = int(args.geti("log-every", 0));
-  std::string stage = args.get("stage", backend == "serial" ? "stage2" : backend == "omp" ? "stage2" : (threads > 1 ? "stage3" : "stage2"));
+  if (stage.empty()) stage = (backend != "serial" && backend != "omp" && threads > 1) ? "stage3" : "stage2";
 
   std::vector<int> sweep = parse_list(args.get("threads-sweep", ""));
   if (sweep.empty()) sweep.push_back(threads);
@@ -60,7 +65,13 @@ int main(int argc, char** argv) {
   if (ranks > 1 || backend == "ranks")
     std::cout << (threads > 1 ? "MPI/OpenMP run with " : "Pure MPI 2D run with ") << ranks
               << (threads > 1 ? " MPI processes; " : " processes; ") << "M=" << P.M << ", N=" << P.N << std::endl;
+  std::vector<std::pair<int, int>> sizes;
+  for (int g : grids) sizes.emplace_back(g, g);
+  if (sizes.empty()) sizes.emplace_back(P.M, P.N);
+  for (const auto& mn : sizes)
   for (int t : sweep) {
+    P.M = mn.first;
+    P.N = mn.second;
     opt.threads = t;
     SolveResult r = cpu_pcg_threads(P, process_grid_from_spec(decomp, ranks, P.M, P.N), opt);
     if (args.flag("json")) {

@@ -77,6 +77,19 @@ def test_native_cpu_app():
     assert out.count("Threads =") == 2
 
 
+def test_native_stage0_grid_loop():
+    """`pe_cpu --stage stage0` = the stage0 program (Withoutopenmp1.cpp:176-196):
+    grids {10, 20, 40}², unweighted stop rule → 17 / 31 / 61 iterations."""
+    import re
+
+    exe = os.path.join(ROOT, "bin", "pe_cpu")
+    if not os.path.exists(exe):
+        pytest.skip("bin/pe_cpu not built")
+    out = subprocess.run([exe, "--stage", "stage0"], capture_output=True, text=True, check=True).stdout
+    got = [tuple(map(int, m)) for m in re.findall(r"M=(\d+), N=(\d+) \| Iter=(\d+) \| Time=\d+\.\d{4} s", out)]
+    assert got == [(10, 10, 17), (20, 20, 31), (40, 40, 61)]
+
+
 def test_dump_roundtrip(tmp_path):
     w = np.random.default_rng(0).random((5, 7))
     dump.save(tmp_path / "x.npy", w, EllipseProblem(6, 8))
