@@ -893,7 +893,9 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
 void launch_red(const KParams& k, int par, hipStream_t s) {
   static const int red1_max = [] {
     const char* e = std::getenv("PE_RED1_MAX");
-    return e ? std::atoi(e) : 20000;
+    // one workgroup streams ≈1.5 µs per 1000 slots (8192²'s 44 k slots: 71 µs
+    // vs 10 µs for 64 blocks, tools/jobs/red_trace.sh): only tiny lists
+    return e ? std::atoi(e) : 4000;
   }();
   if (k.nslots <= red1_max) {
     if (par == 0) hipLaunchKernelGGL(kRed1<0>, dim3(1), dim3(kRed1Threads), 0, s, k, par);
@@ -901,7 +903,9 @@ void launch_red(const KParams& k, int par, hipStream_t s) {
     return;
   }
   {
-    int rb = 16;  // few arrivals on the ticket: the fan-in, not the 2 MB, sets the time
+    // 8192² (44 k slots, 2.8 MB): 4 / 16 / 64 / 128 / 512 blocks = 26.7 / 13.5 /
+    // 10.1 / 10.8 / 11.6 µs — load parallelism first, then the ticket fan-in
+    int rb = 64;
     if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
     rb = std::max(1, std::min(rb, (k.nslots + 255) / 256));
     if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
