@@ -417,6 +417,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("xr", [](DeviceSolver& s) { return s.params().xr.peers != nullptr; },
                              "True when the sweep sums its scalars over ranks itself (P2P transport)")
       .def_property_readonly("nitems", [](DeviceSolver& s) { return s.params().nslots; })
+      .def_property_readonly("stamp_waves",
+                             [](DeviceSolver& s) { return dev::kWPB * std::max(s.params().nblocks, s.params().nblocks0); })
       .def("stamps",
            [](DeviceSolver& s) {
              std::vector<unsigned long long> v = s.stamps();

@@ -19,6 +19,7 @@
 #include <cstdio>
 #include <cstring>
 #include <deque>
+#include <queue>
 #include <limits>
 #include <thread>
 
@@ -198,7 +199,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // rows per item and item order first: they select the sweep kernel variant
   // whose occupancy sizes the grid
   const bool big = double(nx) * double(ny) >= double(1 << 24);
-  if (fused_ && ti_env == 0) ti = big ? 16 : 8;  // sweeps: 8192² dynamic 16 rows; ≤ 4096² static 8
+  // sweeps: 8192² dynamic 18 rows (= 5 unrolled groups of 4 row steps, 3.29 s
+  // vs 3.31-3.74 at 16); smaller blocks static 10 (1600×2400 /
+  // 2400×3200 / 4096² / the 8-rank 8192² block: 3-8 % faster than 8 or 6 rows,
+  // profiles/r2_tune.txt)
+  if (fused_ && ti_env == 0) ti = big ? 18 : 10;
   // Single-sweep item order: the per-XCD dynamic queue (order 3) when the
   // block is large (8192²: +8 % — boundary-band strips cost more, a static
   // deal leaves waves idle), static chunk-major otherwise (small blocks: the
@@ -221,21 +226,25 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.ti = ti;
   k.nstrips = int(strips);
   k.nitems = int(strips * ((nx + ti - 1) / ti));
-  auto grid_for = [&](int cap) {
-    const int per = (k.nitems + cap - 1) / cap;
-    const int waves = (k.nitems + per - 1) / per;
+  // fewest waves that keep every wave's share of the n items equal
+  auto grid_for = [&](int cap, int n) {
+    const int per = (n + cap - 1) / cap;
+    const int waves = (n + per - 1) / per;
     return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
   };
-  k.nblocks = grid_for(wave_cap);
-  k.nblocks0 = k.nblocks;
+  int wave_cap0 = wave_cap;
   if (fused_ && !std::getenv("PE_WAVES")) {
     const int per0 = dev::resident_blocks_S(k, 0);
-    if (per0 > 0) k.nblocks0 = grid_for(cus * per0 * dev::kWPB);
+    if (per0 > 0) wave_cap0 = cus * per0 * dev::kWPB;
   }
+  k.nblocks = grid_for(wave_cap, k.nitems);
+  k.nblocks0 = grid_for(wave_cap0, k.nitems);
+  wave_cap_ = std::min(wave_cap, wave_cap0);
   // block partials: interior grid, then (overlap) the boundary grid after it
   const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
   // item-sum slots: one per item, more when setup_items splits tail items
-  nslot_cap_ = fused_ ? 2 * k.nitems + 64 : 0;
+  // (static sweeps split heavy items into up to ti pieces: setup_items)
+  nslot_cap_ = fused_ ? (k.order == 0 ? ti + 1 : 2) * k.nitems + 64 : 0;
   k.nslots = k.nitems;
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + 8 * int64_t(nslot_cap_))));
   k.partial = partial_;
@@ -247,14 +256,21 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
+  if (fused_) choose_placement();
+  setup_items();
+  if (static_waves_ > 0) {
+    // static list walk: the grid is the one the list was laid out for (plus
+    // the blocks the overlap keeps free for the halo stream)
+    k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
+  }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
-    nstamps_ = 4 * size_t(nslot_cap_) + 2 * size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
+    const size_t nw = size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
+    nstamps_ = 4 * size_t(nslot_cap_) + 2 * nw + 32 * nw;
     PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
     PE_HIP_CHECK(hipMemset(stamps_, 0, sizeof(unsigned long long) * nstamps_));
     k.stamps = stamps_;
+    k.stamps2 = stamps_ + nstamps_ - 32 * nw;  // the last 32 × waves entries
   }
-  if (fused_) choose_placement();
-  setup_items();
   // In-sweep cross-rank reduction (after the placement search, whose sweeps
   // are local and differ in number between ranks).  PE_XR=0 keeps the
   // separate allreduce launch.
@@ -308,7 +324,10 @@ void DeviceSolver::setup_items() {
   const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = fused_ && comm_->size() > 1 && nb && !(e && std::atoi(e) == 0);
-  if (!fused_ || (k.order != 3 && !overlap_)) return;
+  // Lists: dynamic sweeps (order 3), static chunk-major sweeps (order 0:
+  // heavy items split, below) and the overlap; orders 1 / 2 are plain
+  // tuning walks.
+  if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
   if (overlap_) {
     ov_reserve_ = 8;
     // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
@@ -322,24 +341,147 @@ void DeviceSolver::setup_items() {
   double gen_cost = 3.0;
   if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
   const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
+  const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
   // per-item cost: rows ib-2 .. ie+2, band rows weighted
   const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
-  auto item_cost = [&](int ch, int s) {
-    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+  // Does local row q have a boundary-band node in strip s's 128 loaded
+  // columns?  (The kernel's has_gen on the same row-class table.)
+  auto row_gen = [&](int64_t q, int s) {
     const int64_t J = -1 + int64_t(s) * dev::kFSW;
+    const int64_t t = q + 1;  // table index of local row q
+    if (t < 0 || t >= rows_tab) return false;
+    const int* r = &rowcls_host_[size_t(t) * 4];
+    const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
+    return lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
+  };
+  auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
     double c = 0.0;
-    for (int64_t q = ib - 2; q <= ie + 2; ++q) {
-      const int64_t t = q + 1;  // table index of local row q
-      bool gen = false;
-      if (t >= 0 && t < rows_tab) {
-        const int* r = &rowcls_host_[size_t(t) * 4];
-        const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
-        gen = lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
-      }
-      c += gen ? gen_cost : 1.0;
-    }
+    for (int64_t q = ib - 2; q <= ie + 2; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
     return c;
   };
+  auto rows_band = [&](int64_t ib, int64_t ie, int s) {
+    for (int64_t q = ib - 2; q <= ie + 2; ++q)
+      if (row_gen(q, s)) return true;
+    return false;
+  };
+  auto item_cost = [&](int ch, int s) {
+    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+    return rows_cost(ib, ie, s);
+  };
+  // {first row | band flag, strip | rows << 20}; the band flag selects the
+  // kernel's coefficient path (rows ib-2 .. ie+2 include a boundary-band row)
+  auto entry = [&](int64_t ib, int64_t rows, int s) {
+    const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
+    return int2{int(ib) | flag, s | int(rows << 20)};
+  };
+  auto is_boundary = [&](int64_t ib, int64_t ie, int s) {  // outputs a neighbour needs (overlap)
+    const int64_t J = -1 + int64_t(s) * dev::kFSW;
+    const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
+    return overlap_ && !(ov_debug_ & 4) &&
+           ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
+            (blk_.has(UP) && jhi >= blk_.ny - 1));
+  };
+
+  if (k.order == 0) {
+    // ---- Static sweeps: a longest-processing-time-first layout ----
+    // Every wave walks list positions w, w + W, w + 2W, … (W = the grid's
+    // waves), so the host decides who does what: items are cut where one
+    // would exceed a wave's fair share (band items cost ≈2-3× a plain one;
+    // on small blocks, where each wave gets about one item, the band items
+    // alone were the sweep's tail — profiles/r2_small_before.txt), then
+    // assigned heaviest first to the least-loaded wave, and a wave's k-th
+    // item goes to position k·W + w (empty entries fill the gaps).  Equal
+    // costs keep chunk-major order, so each round of positions still covers
+    // a compact window of rows.  Overlap: boundary items take the first
+    // positions (they run in the first round).
+    struct Piece {
+      int64_t ib, rows;
+      int s;
+      double cost;
+      bool bnd;
+    };
+    const double overhead = 3.0;  // per-item prologue / epilogue, in row steps (stamps)
+    int waves_avail = std::max(dev::kWPB, wave_cap_ - (overlap_ ? ov_reserve_ * dev::kWPB : 0));
+    if (const char* w = std::getenv("PE_WAVES")) waves_avail = std::max(dev::kWPB, std::atoi(w));
+    double total = 0.0;
+    for (int id = 0; id < k.nitems; ++id) total += item_cost(id / k.nstrips, id % k.nstrips) + overhead;
+    // cut only when there are fewer items than waves (small blocks): with
+    // more items than waves the layout balances them, and every cut re-reads
+    // 4 more halo rows (2048²: 96 vs 91 µs per iteration with cuts)
+    const int W0 = std::max(1, std::min(waves_avail, k.nitems));
+    const double share = k.nitems >= waves_avail ? 1e300 : std::max(total / W0, (double(k.ti + 4) + overhead) * 1.15);
+    std::vector<Piece> pcs;
+    for (int ch = 0; ch < nchunks; ++ch)
+      for (int s = 0; s < k.nstrips; ++s) {
+        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+        const int64_t n = ie - ib + 1;
+        const bool bnd = is_boundary(ib, ie, s);
+        int parts = 1;
+        if (split_heavy && !bnd) {
+          for (; 2 * (parts + 1) <= n; ++parts) {  // pieces of >= 2 rows
+            double worst = 0.0;
+            for (int q = 0; q < parts; ++q)
+              worst = std::max(worst, rows_cost(ib + n * q / parts, ib + n * (q + 1) / parts - 1, s) + overhead);
+            if (worst <= share) break;
+          }
+        }
+        for (int q = 0; q < parts; ++q) {
+          const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
+          pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
+        }
+      }
+    const int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
+    std::vector<std::vector<int>> per(static_cast<size_t>(W));
+    std::vector<double> load(static_cast<size_t>(W), 0.0);
+    std::vector<int> order;
+    int nbnd = 0;
+    for (int i = 0; i < int(pcs.size()); ++i) {
+      if (pcs[size_t(i)].bnd) {  // boundary pieces: positions 0, 1, … in order
+        per[size_t(nbnd % W)].push_back(i);
+        load[size_t(nbnd % W)] += pcs[size_t(i)].cost;
+        ++nbnd;
+      } else {
+        order.push_back(i);
+      }
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return pcs[size_t(a)].cost > pcs[size_t(b)].cost; });
+    using LW = std::pair<double, int>;
+    std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
+    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
+    for (int i : order) {
+      const LW t = heap.top();
+      heap.pop();
+      per[size_t(t.second)].push_back(i);
+      heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
+    }
+    size_t rounds = 0;
+    for (const auto& v : per) rounds = std::max(rounds, v.size());
+    std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)
+    for (int w = 0; w < W; ++w)
+      for (size_t r = 0; r < per[size_t(w)].size(); ++r) {
+        const Piece& p = pcs[size_t(per[size_t(w)][r])];
+        all[r * size_t(W) + size_t(w)] = entry(p.ib, p.rows, p.s);
+      }
+    static_waves_ = W;
+    nslot_cap_ = std::max<int>(nslot_cap_, int(all.size()));
+    ov_nb_ = nbnd;
+    ov_lnsh_ = 1;
+    ov_lbase_[0] = 0;
+    for (int x = 1; x <= 8; ++x) ov_lbase_[x] = int(all.size());
+    ov_lnb_[0] = nbnd;
+    for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
+    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+    PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+    k.ilist = ilist_;
+    k.lnsh = 1;
+    k.lwaves = W;
+    k.nslots = int(all.size());
+    for (int x = 0; x <= 8; ++x) k.lbase[x] = ov_lbase_[x];
+    for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+    if (overlap_) create_halo_stream();
+    return;
+  }
   std::vector<double> cost(size_t(k.nitems));
   std::vector<double> ccost(size_t(nchunks) + 1, 0.0);  // prefix sums per chunk
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -363,7 +505,6 @@ void DeviceSolver::setup_items() {
   int tail_split = 2;
   if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
   if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));
-  auto entry = [](int64_t ib, int64_t rows, int s) { return int2{int(ib), s | int(rows << 20)}; };
   std::vector<int2> all;
   ov_nb_ = 0;
   ov_lnsh_ = nsh;
@@ -373,12 +514,7 @@ void DeviceSolver::setup_items() {
       for (int s = 0; s < k.nstrips; ++s) {
         const int id = ch * k.nstrips + s;
         const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-        const int64_t J = -1 + int64_t(s) * dev::kFSW;
-        const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
-        const bool bnd = overlap_ && !(ov_debug_ & 4) &&
-                         ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) ||
-                          (blk_.has(DOWN) && jlo <= 2) || (blk_.has(UP) && jhi >= blk_.ny - 1));
-        if (bnd) b.push_back(id);
+        if (is_boundary(ib, ie, s)) b.push_back(id);
         else if (sort_heavy && cost[size_t(id)] > 1.25 * light) heavy.push_back(id);
         else in.push_back(id);
       }
@@ -412,7 +548,10 @@ void DeviceSolver::setup_items() {
   k.nslots = int(all.size());
   for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
   for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
-  if (!overlap_) return;
+  if (overlap_) create_halo_stream();
+}
+
+void DeviceSolver::create_halo_stream() {
   int least = 0, greatest = 0;
   PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));

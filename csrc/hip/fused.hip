@@ -65,6 +65,32 @@ struct WaveTV {
   double sA[128], eA[128], hB[130];
 };
 
+// Per-wave LDS ring of boundary-band coefficients.  A band row's face
+// coefficients and 1/D (chord lengths, four face fits and a division per
+// node) are evaluated ONCE, when the row enters the pipeline at the p_k
+// stage, and re-read by the s = A p and q = A z stages of the next two row
+// steps.  Evaluating them at each of the three stages made a band item cost
+// ≈3.4× a plain one (800×1200: 31 vs 9 µs; the band items were the sweep's
+// critical path, profiles/r2_small_before.txt).  Each lane reads back only
+// its own two columns: no cross-lane synchronisation.
+// [slot][field a0 a1 b0 b1 d][lane], one (column c0, c0+1) pair per entry.
+struct BandRing {
+  double2 v[3][5][64];
+};
+__device__ __forceinline__ void ring_put(BandRing& r, int slot, int lane, const CS& x0, const CS& x1) {
+  r.v[slot][0][lane] = make_double2(x0.a0, x1.a0);
+  r.v[slot][1][lane] = make_double2(x0.a1, x1.a1);
+  r.v[slot][2][lane] = make_double2(x0.b0, x1.b0);
+  r.v[slot][3][lane] = make_double2(x0.b1, x1.b1);
+  r.v[slot][4][lane] = make_double2(x0.d, x1.d);
+}
+__device__ __forceinline__ void ring_get(const BandRing& r, int slot, int lane, CS& x0, CS& x1) {
+  const double2 a0 = r.v[slot][0][lane], a1 = r.v[slot][1][lane], b0 = r.v[slot][2][lane], b1 = r.v[slot][3][lane],
+                d = r.v[slot][4][lane];
+  x0 = CS{a0.x, a1.x, b0.x, b1.x, d.x};
+  x1 = CS{a0.y, a1.y, b0.y, b1.y, d.y};
+}
+
 // Row descriptor carried through the 3-row pipeline: lane-resident interior
 // flags of the lane's two columns, and whether the strip has a boundary-band
 // node in this row (uniform).
@@ -72,7 +98,6 @@ struct RowI {
   bool in0, in1, gen;
   int t;  // local row
 };
-constexpr int FSEG = 60;  // rows per row-class segment: rows s0-2 .. s0+61 live one per lane
 
 // Select-only coefficients of a band-free row: f = 1 inside, 1/eps outside;
 // d = 1/D accordingly.
@@ -82,9 +107,9 @@ __device__ __forceinline__ double lapf(const KParams& k, double f, double pm, do
                                        double pr) {
   return f * (((p0 - pm) - (pn - p0)) * k.ih1sq + ((p0 - pl) - (pr - p0)) * k.ih2sq);
 }
-__device__ __forceinline__ CS cs_gen(const KParams& k, const RowCls& rc, int q, int lj, const WaveTV& tv, int jl) {
+__device__ __forceinline__ CS cs_gen(const KParams& k, const RowCls& rc, const CT& ct, int lj, const WaveTV& tv, int jl) {
   const TV t{tv.sA[jl], tv.eA[jl], tv.hB[jl], tv.hB[jl + 1]};
-  return cset_rc(k, rc, q, lj, t);
+  return cset_rc(k, rc, ct, lj, t);
 }
 
 typedef double v2d __attribute__((ext_vector_type(2)));
@@ -143,6 +168,46 @@ __device__ __forceinline__ Scal sweep_scalars(const KParams& k, const DevState* 
     c.zc = 1.0;
   }
   return c;
+}
+
+// Does this sweep end the solve before its own work?  brk: breakdown /
+// non-finite scalars (stop before this sweep's w term, reference :413);
+// last: a deferring sweep (WM = 0) that converged or hit the cap — it only
+// adds its own α_k p_k to w.  A pure function of the scalars, so every block
+// of the sweep and of its reduction kernel decides the same.
+struct Term {
+  bool brk, bad, last, conv;
+};
+template <int WM>
+__device__ __forceinline__ Term sweep_term(const KParams& k, const Scal& c) {
+  Term t{false, false, false, false};
+  if (c.first) return t;
+  t.bad = !isfinite(c.den) || !isfinite(c.g) || !isfinite(c.diff);
+  t.brk = t.bad || fabs(c.den) < 1e-15;
+  t.conv = k.check_tol && c.diff < k.tol;
+  t.last = !t.brk && WM == 0 && (t.conv || c.kiter >= k.max_iter);
+  return t;
+}
+
+// Terminal state write (one thread, in the block that arrives last — never
+// while another block of the grid may still be reading the state it read at
+// entry: the ticket orders every block's reads before this write).
+__device__ __forceinline__ void sweep_terminal(const KParams& k, DevState* st, const Scal& c, const Term& t) {
+  if (t.brk) {
+    st->status = t.bad ? 4 : 2;
+    st->iter = c.kiter;
+  } else {
+    st->gprev = c.g;
+    st->rz_cur = c.g;
+    st->alpha = c.alpha;
+    st->beta = c.beta;
+    st->last_diff = c.diff;
+    if (k.hist && c.kiter <= k.hist_n) k.hist[c.kiter - 1] = c.diff;
+    st->iter = c.kiter;
+    st->status = t.conv ? 1 : 3;
+  }
+  st->done = 1;
+  st->wpend = 0;
 }
 
 // State update after a sweep's sums t[7] are known (one thread).
@@ -224,17 +289,19 @@ template <int OCC, int PF, bool NT, int WM, bool STAMP = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   const unsigned long long t_entry = STAMP ? rtc() : 0ull;
-  // Every state word the sweep needs is loaded up front, together (one
-  // round trip, not a chain behind the `done` test: measured ≈5 µs from
-  // wave entry to the first item with the chain).
+  // Every state word the sweep needs is loaded up front, together, and
+  // nothing waits for them until the wave's first item has issued its
+  // prologue row loads (`leave` below): the state round trip after the
+  // kernel boundary (≈3 µs from wave entry to the first item when waited for
+  // first, profiles/r2_small_before.txt) overlaps the row loads' own.
   const int done = st->done, wpend = st->wpend;
   const double alpha_st = st->alpha;
   // ---- scalars of this sweep from the previous sweep's global sums ----
   const Scal sc = sweep_scalars(k, st, par);
-  if (done) return;
   __shared__ double sm[32];
   __shared__ int sflag;
   __shared__ WaveTV tvs[kWPB];
+  __shared__ BandRing rings[kWPB];
 
 
   // Row pointers at column -1 (uniform, SGPR) + lane offset (unsigned VGPR).
@@ -248,6 +315,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
 
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   WaveTV& tvw = tvs[wid];
+  BandRing& rg = rings[wid];
   const int gwave = int(blockIdx.x) * kWPB + wid;
   if constexpr (STAMP) {
     if (lane == 0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave] = t_entry;
@@ -294,6 +362,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     ilimit = k.lbase[xs + 1] - k.lbase[xs];
     lnb = k.lnb[xs];
     chunk0 = 0;
+    if (!(k.order == 3) && k.lwaves > 0) {  // static layout for exactly lwaves waves
+      istride = k.lwaves;
+      if (it0 >= k.lwaves) it0 = ilimit;
+    }
   }
   const bool dyn = k.order == 3;
   const bool persum = dyn;
@@ -327,45 +399,43 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   // neither.
   auto shard_waves = [&](int x) { return ((int(gridDim.x) - x + nsh - 1) / nsh) * kWPB; };
   int item = it0;
+  bool first_item = true;  // STAMP: the step timeline covers the wave's first item
+  auto sstamp = [&](int n) {
+    if constexpr (STAMP) {
+      if (first_item && lane == 0) k.stamps2[int64_t(gwave) * 32 + n] = rtc();
+    }
+  };
   // prefetched list entry of `item` (have_next: valid); the first one is
   // requested before the scalar checks below wait for the state loads
   bool have_next = listed && it0 < ilimit;
   int2 enext = have_next ? cload_i2(lst + it0) : make_int2(0, 0);
 
-  const bool first = sc.first;
-  const long long kiter = sc.kiter;
-  const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc, g = sc.g, diff = sc.diff;
-  if (!first) {
-    const bool bad = !isfinite(sc.den) || !isfinite(sc.g) || !isfinite(sc.diff);
-    if (bad || fabs(sc.den) < 1e-15) {  // breakdown / non-finite: stop before this sweep's w term (reference :413)
-      if (WM == 2 && wpend && !bad) w_pointwise(k, k.x[par ^ 1], alpha_st, 0.0, 0.0, 0.0);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->status = bad ? 4 : 2;
-        st->iter = kiter;
-        st->done = 1;
-        st->wpend = 0;
+  const double alpha = sc.alpha, beta = sc.beta, zc = sc.zc;
+  // Once per wave, after its first prologue loads (or after the walk when it
+  // gets no item): true → the wave leaves (solve done, or a terminal sweep).
+  bool state_ok = false;
+  auto leave = [&]() -> bool {
+    state_ok = true;
+    if (done) return true;
+    const Term tm = sweep_term<WM>(k, sc);
+    if (tm.brk || tm.last) {
+      // breakdown: apply only the pending term; last sweep of the solve: only
+      // w changes (w += α_k p_k, pointwise).  The state is written by the
+      // last-arriving block here (static sweeps) or by the reduction kernel
+      // that follows (dynamic sweeps) — never while blocks may still read it.
+      if (tm.brk) {
+        if (WM == 2 && wpend && !tm.bad) w_pointwise(k, k.x[par ^ 1], alpha_st, 0.0, 0.0, 0.0);
+      } else {
+        w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
       }
-      return;
-    }
-    const bool conv = k.check_tol && diff < k.tol;
-    if (WM == 0 && (conv || kiter >= k.max_iter)) {
-      // last sweep of the solve: only w changes (w += α_k p_k, pointwise)
-      w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
-      if (blockIdx.x == 0 && threadIdx.x == 0) {
-        st->gprev = g;
-        st->rz_cur = g;
-        st->alpha = alpha;
-        st->beta = beta;
-        st->last_diff = diff;
-        if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = diff;
-        st->iter = kiter;
-        st->status = conv ? 1 : 3;
-        st->done = 1;
-        st->wpend = 0;
+      if (!persum && arrive_last(&st->ticket[0], gridDim.x, &sflag) && threadIdx.x == 0) {
+        sweep_terminal(k, st, sc, tm);
+        __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
-      return;
+      return true;
     }
-  }
+    return false;
+  };
   // α of the pending term left by the previous (deferring) sweep
   const double alpha_prev = (WM == 2 && wpend) ? alpha_st : 0.0;
   for (;;) {
@@ -382,11 +452,17 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     // item index is (strip, ti-row chunk) and the slot is chunk-major.
     int s, ib, ie;
     int64_t slot;
+    bool band = true;  // the item has boundary-band rows (general march); lists say which do not
     if (listed) {
       const int2 e = have_next ? enext : cload_i2(lst + item);
       s = e.y & 0xFFFFF;
-      ib = e.x;
+      ib = e.x & kRowMask;
+      band = (e.x & kBandBit) != 0;
       ie = min(ib + (e.y >> 20) - 1, nx);
+      if (ie < ib) {  // empty position of a static layout
+        item += istride;
+        continue;
+      }
       slot = int64_t(k.lbase[sh]) + item;
     } else {
       const int gitem = item;
@@ -397,6 +473,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       slot = int64_t(ch) * k.nstrips + s;
     }
     const unsigned long long t_item = STAMP ? rtc() : 0ull;
+    sstamp(0);
     const int J = -1 + s * FSW;
     const int c0 = J + 2 * lane;               // odd → 16-byte aligned pair (c0, c0+1)
     const unsigned off = unsigned(c0 + 1);     // element offset from column -1
@@ -407,6 +484,27 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     const bool o0 = inner && c0 >= 1 && c0 <= ny;
     const bool o1 = inner && c0 + 1 <= ny;
     const int jl0 = 2 * lane;
+    // y-direction halo strips (columns 1,2 and ny-1,ny) of output row i → send buffers
+    auto send_strips = [&](int i, const double2& rkI, const double2& pa) {
+      if (k.has[DOWN] && o0 && c0 == 1) {
+        double* sb = k.send_dn + int64_t(i - 1) * 4;
+        sb[0] = rkI.x;
+        sb[1] = rkI.y;
+        sb[2] = pa.x;
+        sb[3] = pa.y;
+      }
+      if (k.has[UP]) {
+        double* sb = k.send_up + int64_t(i - 1) * 4;
+        if (o0 && c0 >= ny - 1) {
+          sb[c0 - (ny - 1)] = rkI.x;
+          sb[c0 - (ny - 1) + 2] = pa.x;
+        }
+        if (o1 && c0 + 1 >= ny - 1) {
+          sb[c0 + 1 - (ny - 1)] = rkI.y;
+          sb[c0 + 1 - (ny - 1) + 2] = pa.y;
+        }
+      }
+    };
     // Strip chord entries → LDS, read by boundary-band rows only: staged only
     // when the item has band rows in this strip (a few % of items).
     bool tv_ok = false;
@@ -427,18 +525,26 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       tv_ok = true;
     };
     // Row classes of a 64-row segment, lane l ↔ row segbase+l; band rows as
-    // a scalar bit mask.  Reloaded every FSEG rows (items may be long).  The
+    // a scalar bit mask.  Reloaded every 60 rows (items may be long).  The
     // load is issued before the prologue's row loads and waited for after
     // them (loads complete in order: waiting for it leaves the rows in flight).
     int segbase = 0;
     int4 rcv;
+    double2 ctv;  // column table of row segbase+lane: {half-width, sB}
+    double cte;   // ... eB
     unsigned long long genmask = 0;
     auto issue_seg = [&](int base) {
       segbase = base;
       const int nr = ie + 3 - base;
       rcv = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+      if (band) {
+        const double* ctr = k.colT + (min(base + lane, ie + 3) + 1) * 4;  // rows base .. ie+3
+        ctv = *reinterpret_cast<const double2*>(ctr);
+        cte = ctr[2];
+      }
     };
     auto finish_seg = [&]() {
+      if (!band) return;  // plain items: the row classes are waited for at their first use
       const int nr = ie + 3 - segbase;
       genmask = __ballot(lane < nr && has_gen(RowCls{rcv.x, rcv.y, rcv.z, rcv.w}, J, J + 127));
       if (genmask != 0 && !tv_ok) stage_tv();
@@ -458,18 +564,24 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       r.gen = (genmask >> l) & 1ull;
       return r;
     };
-    auto dval = [&](const RowI& R, int t, double& d0, double& d1) {
+    // Row t enters the pipeline (its p_k stage): 1/D of both columns; a
+    // band row evaluates its coefficients here, once, into ring slot `slot`.
+    auto enter = [&](const RowI& R, int t, int slot, double& d0, double& d1) {
       if (!R.gen) {
         d0 = dsel(k, R.in0);
         d1 = dsel(k, R.in1);
       } else {
-        const RowCls rc = rcl_read(rcv, R.t - segbase);
-        d0 = cs_gen(k, rc, t, c0, tvw, jl0).d;
-        d1 = cs_gen(k, rc, t, c0 + 1, tvw, jl0 + 1).d;
+        const int l = R.t - segbase;
+        const RowCls rc = rcl_read(rcv, l);
+        const CT ct{readlane(ctv.x, l), readlane(ctv.x, l + 1), readlane(ctv.y, l), readlane(cte, l)};
+        const CS x0 = cs_gen(k, rc, ct, c0, tvw, jl0), x1 = cs_gen(k, rc, ct, c0 + 1, tvw, jl0 + 1);
+        ring_put(rg, slot, lane, x0, x1);
+        d0 = x0.d;
+        d1 = x1.d;
       }
     };
     // (A u)(row t) for both columns; d0/d1 = 1/D of row t.
-    auto apply = [&](const RowI& R, int t, const double2& um, const double2& u0, const double2& un, double ul,
+    auto apply = [&](const RowI& R, int slot, const double2& um, const double2& u0, const double2& un, double ul,
                      double ur, double& a0, double& a1, double& d0, double& d1) {
       if (!R.gen) {
         const double f0 = fsel(k, R.in0), f1 = fsel(k, R.in1);
@@ -478,8 +590,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         d0 = dsel(k, R.in0);
         d1 = dsel(k, R.in1);
       } else {
-        const RowCls rc = rcl_read(rcv, R.t - segbase);
-        const CS x0 = cs_gen(k, rc, t, c0, tvw, jl0), x1 = cs_gen(k, rc, t, c0 + 1, tvw, jl0 + 1);
+        CS x0, x1;
+        ring_get(rg, slot, lane, x0, x1);
         a0 = stencil<false>(k, x0, um.x, u0.x, un.x, ul, u0.y);
         a1 = stencil<false>(k, x1, um.y, u0.y, un.y, u0.x, ur);
         d0 = x0.d;
@@ -502,7 +614,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       if constexpr (WM == 2) wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
       else wq[q] = dd(0.0, 0.0);
     }
+    if (!state_ok && leave()) return;
+    sstamp(1);
     finish_seg();
+    sstamp(2);
     // next item: the pull (older than the prologue loads) has returned
     int nxt_item = ilimit;
     have_next = false;
@@ -513,109 +628,115 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         have_next = true;
       }
     }
-    RowI R0 = rinfo(ib - 2), R1 = rinfo(ib - 1);
-    double2 pa, pb;  // p_k rows i, i+1 at step i
+    // ---- the row march ----
+    // Row t's values live in slot (t - t0) & 3 of 4-entry register arrays and
+    // the row loop is unrolled by 4 (= the prefetch depth), so every slot
+    // index is a compile-time constant and nothing rotates (a rolled loop
+    // spent ≈70 v_mov_b64 per row step moving its window; a row step is
+    // instruction-issue-bound when a sweep gives each SIMD about one wave —
+    // small blocks: 0.84 µs per step at 800×1200, profiles/r2_steps_before.txt).
+    // The last group stops at row ie (a uniform early exit).
+    // Boundary-band rows (items with the band flag only; a scalar test per
+    // row) take the coefficient path: evaluated once when the row enters
+    // (ring slot (t - t0) mod 3), re-read by its two stencil stages.
+    static_assert(PF == 4, "row march: prefetch depth = unroll factor");
+    const int t0 = ib - 2;
+    double2 RQ[4], PQ[4], WQ[4], P[4], Z[4], Q[4], RIN[2], S[2], RK[2];
+    RowI RW[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      RQ[(q + 2) & 3] = rq[q];  // x rows ib+q = t0+2+q
+      PQ[(q + 2) & 3] = pq[q];
+      WQ[q] = wq[q];  // w rows t0+q
+      Z[q] = dd(0.0, 0.0);
+      Q[q] = dd(0.0, 0.0);
+      P[q] = dd(0.0, 0.0);
+      RW[q] = RowI{false, false, false, 0};
+    }
+    RW[0] = rinfo(t0);
+    RW[1] = rinfo(t0 + 1);
     {
       double d0, d1;
-      dval(R0, ib - 2, d0, d1);
-      pa = dd(zc * (rA.x * d0) + beta * pA.x, zc * (rA.y * d1) + beta * pA.y);
-      dval(R1, ib - 1, d0, d1);
-      pb = dd(zc * (rin1.x * d0) + beta * pB.x, zc * (rin1.y * d1) + beta * pB.y);
+      enter(RW[0], t0, 0, d0, d1);
+      P[0] = dd(zc * (rA.x * d0) + beta * pA.x, zc * (rA.y * d1) + beta * pA.y);
+      enter(RW[1], t0 + 1, 1, d0, d1);
+      P[1] = dd(zc * (rin1.x * d0) + beta * pB.x, zc * (rin1.y * d1) + beta * pB.y);
     }
-    double2 sI = dd(0.0, 0.0), rkI = dd(0.0, 0.0), zM = dd(0.0, 0.0), zI = dd(0.0, 0.0);
-    double2 qa = pA, qb = pB;  // p_{k-1} rows i, i+1 (WM == 2: the pending term)
-
-    for (int i = ib - 2; i <= ie; ++i) {
-      if (i > ib && (i - ib) % FSEG == 0) load_seg(i - 2);  // rows i-2 .. i+61
-      // ---- prefetch x row i+2+PF and w row i+PF, clamped to the rows this
-      // item reads (a clamped re-read hits L2; no predicated loads) ----
-      const double* xn = Xm + int64_t(min(i + 2 + PF, ie + 2)) * pitch;
-      const double2 rN = ld2(xn + off), pN = ld2(xn + poff + off);
-      double2 wN = dd(0.0, 0.0);
-      if constexpr (WM == 2) wN = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
-      const double2 rQ0 = rq[0], pQ0 = pq[0], wQ0 = wq[0];
-
-      // p_k(i+2) = z_{k-1} + β p_{k-1}
-      const RowI R2 = rinfo(i + 2);
-      double d20, d21;
-      dval(R2, i + 2, d20, d21);
-      const double2 pc = dd(zc * (rQ0.x * d20) + beta * pQ0.x, zc * (rQ0.y * d21) + beta * pQ0.y);
-
-      // s(i+1) = A p_k, r_k(i+1), z_k(i+1)
-      double s0, s1, d10, d11;
-      apply(R1, i + 1, pa, pb, pc, dpp_shr1(pb.y), dpp_shl1(pb.x), s0, s1, d10, d11);
-      const double rk0 = rin1.x - alpha * s0, rk1 = rin1.y - alpha * s1;
-      const int64_t gr = k.gi0 + i + 1;
-      const bool rl = gr >= 1 && gr <= k.M - 1;
-      const double zn0 = (rl && lv0) ? rk0 * d10 : 0.0;
-      const double zn1 = (rl && lv1) ? rk1 * d11 : 0.0;
-
-      if (i >= ib) {
-        // q(i) = A z_k, the 7 sums, the row-i outputs
-        double q0, q1, e0, e1;
-        apply(R0, i, zM, zI, dd(zn0, zn1), dpp_shr1(zI.y), dpp_shl1(zI.x), q0, q1, e0, e1);
-        const double zo0 = o0 ? zI.x : 0.0, po0 = o0 ? pa.x : 0.0;
-        const double zo1 = o1 ? zI.y : 0.0, po1 = o1 ? pa.y : 0.0;
-        sg += rkI.x * zo0 + rkI.y * zo1;
-        sd += zo0 * q0 + zo1 * q1;
-        se += zo0 * sI.x + zo1 * sI.y;
-        sps += po0 * sI.x + po1 * sI.y;
-        szz += zo0 * zo0 + zo1 * zo1;
-        szp += zo0 * po0 + zo1 * po1;
-        spp += po0 * po0 + po1 * po1;
-        double* yr = Ym + int64_t(i) * pitch + off;
-        double* wd = Wm + int64_t(i) * wp + off;
-        const double2 wv = dd(wQ0.x + alpha_prev * qa.x + alpha * pa.x, wQ0.y + alpha_prev * qa.y + alpha * pa.y);
-        if (o1) {
-          st2<NT>(yr, rkI);
-          st2<NT>(yr + poff, pa);
-          if constexpr (WM == 2) st2<NT>(wd, wv);
-        } else if (o0) {
-          yr[0] = rkI.x;
-          yr[poff] = pa.x;
-          if constexpr (WM == 2) wd[0] = wv.x;
-        }
-        // y-direction halo strips (columns 1,2 and ny-1,ny) → send buffers
-        if (k.has[DOWN] && o0 && c0 == 1) {
-          double* sb = k.send_dn + int64_t(i - 1) * 4;
-          sb[0] = rkI.x;
-          sb[1] = rkI.y;
-          sb[2] = pa.x;
-          sb[3] = pa.y;
-        }
-        if (k.has[UP]) {
-          double* sb = k.send_up + int64_t(i - 1) * 4;
-          if (o0 && c0 >= ny - 1) {
-            sb[c0 - (ny - 1)] = rkI.x;
-            sb[c0 - (ny - 1) + 2] = pa.x;
-          }
-          if (o1 && c0 + 1 >= ny - 1) {
-            sb[c0 + 1 - (ny - 1)] = rkI.y;
-            sb[c0 + 1 - (ny - 1) + 2] = pa.y;
-          }
-        }
-      }
-      // ---- shift the register window ----
-      R0 = R1;
-      R1 = R2;
-      zM = zI;
-      zI = dd(zn0, zn1);
-      sI = dd(s0, s1);
-      rkI = dd(rk0, rk1);
-      pa = pb;
-      pb = pc;
-      qa = qb;
-      qb = pQ0;
-      rin1 = rQ0;
+    Q[0] = pA;
+    Q[1] = pB;
+    RIN[0] = rin1;
+    RIN[1] = S[0] = S[1] = RK[0] = RK[1] = dd(0.0, 0.0);
+    sstamp(3);
+    const int nsteps = ie - t0 + 1;
+    int sl = 0;  // ring slot of row i at step i ((i - t0) mod 3)
+    for (int g = 0; 4 * g < nsteps; ++g) {
+      if (g > 0 && g % 15 == 0) load_seg(t0 + 4 * g + 2);  // rows i+2 .. i+65 of this group's i
 #pragma unroll
-      for (int q = 0; q + 1 < PF; ++q) {
-        rq[q] = rq[q + 1];
-        pq[q] = pq[q + 1];
-        wq[q] = wq[q + 1];
+      for (int jj = 0; jj < 4; ++jj) {
+        const int i = t0 + 4 * g + jj;
+        if (i > ie) break;
+        const int a = jj, b = (jj + 1) & 3, c = (jj + 2) & 3, m = (jj + 3) & 3;  // rows i, i+1, i+2, i-1
+        const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl == 0 ? 2 : sl - 1;  // ring slots of rows i+1, i+2
+        const double2 rQ0 = RQ[c], pQ0 = PQ[c], wQ0 = WQ[a];
+        {  // prefetch x row i+6 and w row i+4 into the slots just consumed
+          const double* xn = Xm + int64_t(min(i + 2 + PF, ie + 2)) * pitch;
+          RQ[c] = ld2(xn + off);
+          PQ[c] = ld2(xn + poff + off);
+          if constexpr (WM == 2) WQ[a] = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
+        }
+        // p_k(i+2) = z_{k-1} + β p_{k-1}
+        RW[c] = rinfo(i + 2);
+        {
+          double d0, d1;
+          enter(RW[c], i + 2, sl2, d0, d1);
+          P[c] = dd(zc * (rQ0.x * d0) + beta * pQ0.x, zc * (rQ0.y * d1) + beta * pQ0.y);
+        }
+        if constexpr (WM == 2) Q[c] = pQ0;
+        // s(i+1) = A p_k, r_k(i+1), z_k(i+1)
+        double s0, s1, d10, d11;
+        apply(RW[b], sl1, P[a], P[b], P[c], dpp_shr1(P[b].y), dpp_shl1(P[b].x), s0, s1, d10, d11);
+        const double2 rin = RIN[jj & 1];
+        const double rk0 = rin.x - alpha * s0, rk1 = rin.y - alpha * s1;
+        const int64_t gr = k.gi0 + i + 1;
+        const bool rl = gr >= 1 && gr <= k.M - 1;
+        const double zn0 = (rl && lv0) ? rk0 * d10 : 0.0;
+        const double zn1 = (rl && lv1) ? rk1 * d11 : 0.0;
+        if (i >= ib) {
+          // q(i) = A z_k, the 7 sums, the row-i outputs
+          const double2 zI = Z[a], pa = P[a], sI = S[jj & 1], rkI = RK[jj & 1];
+          double q0, q1, e0, e1;
+          apply(RW[a], sl, Z[m], zI, dd(zn0, zn1), dpp_shr1(zI.y), dpp_shl1(zI.x), q0, q1, e0, e1);
+          const double zo0 = o0 ? zI.x : 0.0, po0 = o0 ? pa.x : 0.0;
+          const double zo1 = o1 ? zI.y : 0.0, po1 = o1 ? pa.y : 0.0;
+          sg += rkI.x * zo0 + rkI.y * zo1;
+          sd += zo0 * q0 + zo1 * q1;
+          se += zo0 * sI.x + zo1 * sI.y;
+          sps += po0 * sI.x + po1 * sI.y;
+          szz += zo0 * zo0 + zo1 * zo1;
+          szp += zo0 * po0 + zo1 * po1;
+          spp += po0 * po0 + po1 * po1;
+          double* yr = Ym + int64_t(i) * pitch + off;
+          double* wd = Wm + int64_t(i) * wp + off;
+          const double2 qa = Q[a];
+          const double2 wv = dd(wQ0.x + alpha_prev * qa.x + alpha * pa.x, wQ0.y + alpha_prev * qa.y + alpha * pa.y);
+          if (o1) {
+            st2<NT>(yr, rkI);
+            st2<NT>(yr + poff, pa);
+            if constexpr (WM == 2) st2<NT>(wd, wv);
+          } else if (o0) {
+            yr[0] = rkI.x;
+            yr[poff] = pa.x;
+            if constexpr (WM == 2) wd[0] = wv.x;
+          }
+          send_strips(i, rkI, pa);
+        }
+        Z[b] = dd(zn0, zn1);
+        S[(jj + 1) & 1] = dd(s0, s1);
+        RK[(jj + 1) & 1] = dd(rk0, rk1);
+        RIN[(jj + 1) & 1] = rQ0;
+        sl = sl1;
+        if (i - ib + 6 < 30) sstamp(i - ib + 6);  // after row step i: slots 4 ..
       }
-      rq[PF - 1] = rN;
-      pq[PF - 1] = pN;
-      wq[PF - 1] = wN;
     }
     if (persum) {
       // per-item sums (wave-reduced) in a fixed slot: the reduction kernel
@@ -646,22 +767,22 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         d[0] = t_item;
         d[1] = rtc();
         d[2] = (unsigned long long)gwave | ((unsigned long long)s << 32);
-        d[3] = (unsigned long long)ib | ((unsigned long long)(ie - ib + 1) << 32) | ((unsigned long long)(genmask != 0) << 48);
+        d[3] = (unsigned long long)ib | ((unsigned long long)(ie - ib + 1) << 32) | ((unsigned long long)(band ? 1 : 0) << 48);
       }
     }
+    sstamp(31);
+    first_item = false;
     item = dyn ? nxt_item : item + istride;
   }
   if constexpr (STAMP) {
     if (lane == 0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc();
   }
+  if (!state_ok && leave()) return;
   if (persum) return;  // kRed reduces the item sums and finalizes
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   block_reduce<7, false>(v, sm);
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int n = 0; n < 7; ++n) k.partial[7 * size_t(blockIdx.x) + n] = v[n];
-  if (arrive_last(&st->ticket[0], gridDim.x, &sflag)) {
+  if (publish_last<7>(k.partial + 7 * size_t(blockIdx.x), v, &st->ticket[0], gridDim.x, &sflag)) {
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
     finalize_block<WM>(k, st, par, sc, t);
@@ -678,6 +799,16 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
   __shared__ double sm[32];
   __shared__ int sflag;
   const Scal sc = sweep_scalars(k, st, par);
+  {
+    const Term tm = sweep_term<WM>(k, sc);
+    if (tm.brk || tm.last) {  // the sweep stopped early (kS): only the terminal state is left to write
+      if (arrive_last(&st->ticket[1], gridDim.x, &sflag) && threadIdx.x == 0) {
+        sweep_terminal(k, st, sc, tm);
+        __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      return;
+    }
+  }
   const int64_t n = k.nslots, lo = n * blockIdx.x / gridDim.x, hi = n * (blockIdx.x + 1) / gridDim.x;
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
   // RU items per thread in flight: all loads of a batch are issued before the
@@ -710,10 +841,7 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
     }
   }
   block_reduce<7, false>(v, sm);
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int q = 0; q < 7; ++q) k.partial[7 * size_t(blockIdx.x) + q] = v[q];
-  if (arrive_last(&st->ticket[1], gridDim.x, &sflag)) {
+  if (publish_last<7>(k.partial + 7 * size_t(blockIdx.x), v, &st->ticket[1], gridDim.x, &sflag)) {
     double t[7];
     reduce_partials<7>(k.partial, gridDim.x, t, sm);
     finalize_block<WM>(k, st, par, sc, t);
@@ -732,6 +860,13 @@ __global__ __launch_bounds__(kRed1Threads) void kRed1(KParams k, int par) {
   const int done = st->done;
   const Scal sc = sweep_scalars(k, st, par);
   if (done) return;
+  {
+    const Term tm = sweep_term<WM>(k, sc);
+    if (tm.brk || tm.last) {  // the sweep stopped early (kS): only the terminal state is left to write
+      if (threadIdx.x == 0) sweep_terminal(k, st, sc, tm);
+      return;
+    }
+  }
   __shared__ double sm[7][kRed1Threads / 64];
   const int64_t n = k.nslots;
   double v[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -855,8 +990,9 @@ __global__ void kUnpack(KParams k, int b) {
 // Kernel configuration (PE_SKERNEL, for tuning sweeps): 0 default = 4 rows
 // of loads in flight per wave + non-temporal w/output streams (8192² sweep:
 // 1373 it/s vs 1119 for 2 rows / temporal at 3 waves per SIMD — the sweep is
-// bound by HBM latency per wave, not by occupancy), 1 = 2 rows temporal,
-// 2 = 3 rows non-temporal, 3 = 5 rows non-temporal.
+// bound by HBM latency per wave, not by occupancy); 1 = temporal streams.
+// (Round 1 also measured 2 / 3 / 5 rows in flight: 4 won, and the plain
+// march's unroll is tied to it.)
 static int s_cfg() {
   static const int v = [] {
     const char* e = std::getenv("PE_SKERNEL");
@@ -867,12 +1003,10 @@ static int s_cfg() {
 
 template <int WM, class F>
 static auto with_kS(const KParams& k, F&& f) {
-  if (k.stamps) return f(kS<0, 4, true, WM, true>);
+  if (k.stamps) return f(kS<2, 4, true, WM, true>);
   switch (s_cfg()) {
-    case 1: return f(kS<0, 2, false, WM>);
-    case 2: return f(kS<0, 3, true, WM>);
-    case 3: return f(kS<0, 5, true, WM>);
-    default: return f(kS<0, 4, true, WM>);
+    case 1: return f(kS<2, 4, false, WM>);
+    default: return f(kS<2, 4, true, WM>);
   }
 }
 

@@ -188,6 +188,30 @@ __device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, 
   return *sflag != 0;
 }
 
+// Write-through form of arrive_last for a block's N partial sums (thread 0
+// holds them): stored `sc1` (relaxed agent-scope atomic stores), drained,
+// then the ticket — no per-block L2 write-back (`buffer_wbl2`, ≈1.7-6.5 µs
+// on a dirty L2, paid by every block of the grid); the last arriver does
+// the agent acquire before reading (MI355X_MICROARCH.md, visibility recipe R1).
+template <int N>
+__device__ __forceinline__ bool publish_last(double* dst, const double (&v)[N], unsigned* ticket, unsigned nblocks,
+                                             int* sflag) {
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int n = 0; n < N; ++n) __hip_atomic_store(dst + n, v[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = (t == nblocks - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    *sflag = last;
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
 // Sum N-tuples of partials [nblocks][N] in block order (deterministic).
 template <int N>
 __device__ __forceinline__ void reduce_partials(const double* partial, unsigned nblocks, double (&v)[N], double* sm) {
@@ -247,8 +271,28 @@ __device__ __forceinline__ double fcoef_fast(double l, double h, double inv_h, d
   return t + (1.0 - t) * inv_eps;
 }
 
+// 1/x for the band diagonal (x = a sum of positive face terms ≥ 2/h², far
+// from denormal / overflow): hardware reciprocal + two Newton steps, ≤ 1 ulp
+// from the IEEE quotient — 5 instructions instead of the ≈10 of the scaled
+// IEEE division sequence.
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  double e = fma(-x, r, 1.0);
+  r = fma(r, e, r);
+  e = fma(-x, r, 1.0);
+  return fma(r, e, r);
+}
+
+// Column-table values of one row q: chord half-width at the faces left of
+// rows q and q+1 (vertical faces), and the y-range of the row's horizontal
+// faces.  The single-sweep kernel reads them from lanes (one row per lane,
+// loaded with the row classes), never through scalar loads in the loop.
+struct CT {
+  double half0, half1, sB, eB;
+};
+
 // cset with the row class already in SGPRs (fast arithmetic).
-__device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, int64_t q, int64_t lj, const TV& t) {
+__device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, const CT& ct, int64_t lj, const TV& t) {
   CS x;
   if (lj >= c.in_lo && lj <= c.in_hi) {
     x.a0 = x.a1 = x.b0 = x.b1 = 1.0;
@@ -258,13 +302,11 @@ __device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, int64_t
     x.d = k.dinv_out;
   } else {
     const double ih1 = -k.nih1, ih2 = -k.nih2;
-    const double* ct = k.colT + (q + 1) * 4;
-    const double half0 = cload(ct), half1 = cload(ct + 4), sB = cload(ct + 1), eB = cload(ct + 2);
-    x.a0 = fcoef_fast(chord_len(half0, t.sA, t.eA), k.h2, ih2, k.inv_eps);
-    x.a1 = fcoef_fast(chord_len(half1, t.sA, t.eA), k.h2, ih2, k.inv_eps);
-    x.b0 = fcoef_fast(chord_len(t.hB, sB, eB), k.h1, ih1, k.inv_eps);
-    x.b1 = fcoef_fast(chord_len(t.hB1, sB, eB), k.h1, ih1, k.inv_eps);
-    x.d = 1.0 / ((x.a1 + x.a0) * k.ih1sq + (x.b1 + x.b0) * k.ih2sq);
+    x.a0 = fcoef_fast(chord_len(ct.half0, t.sA, t.eA), k.h2, ih2, k.inv_eps);
+    x.a1 = fcoef_fast(chord_len(ct.half1, t.sA, t.eA), k.h2, ih2, k.inv_eps);
+    x.b0 = fcoef_fast(chord_len(t.hB, ct.sB, ct.eB), k.h1, ih1, k.inv_eps);
+    x.b1 = fcoef_fast(chord_len(t.hB1, ct.sB, ct.eB), k.h1, ih1, k.inv_eps);
+    x.d = rcp_nr((x.a1 + x.a0) * k.ih1sq + (x.b1 + x.b0) * k.ih2sq);
   }
   return x;
 }

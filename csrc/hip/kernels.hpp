@@ -114,6 +114,7 @@ struct KParams {
   // once its stores are visible.
   const int2* ilist;
   int lnsh;
+  int lwaves;                    // static list layout: wave w walks positions w, w + lwaves, … (0: the grid's waves)
   int lbase[9];
   int lnb[8];
   // Diagnostic timeline (PE_STAMPS=1, single-sweep only; null otherwise;
@@ -121,6 +122,7 @@ struct KParams {
   // in s_memrealtime ticks (100 MHz), then per wave {entry, exit}.
   // Overwritten by every sweep.
   unsigned long long* stamps;
+  unsigned long long* stamps2;   // per wave, 32 stamps along its FIRST item (start, prologue, row steps)
   // Cross-rank reduction inside the sweep (PE_XR, with a P2P comm): the final
   // reduction block sums the 7 sums over ranks itself (xr.peers == null: the
   // host enqueues the comm's allreduce instead).
@@ -131,6 +133,11 @@ constexpr int kTJ = 256;         // threads per block (4 wave64s)
 constexpr int kWPB = 4;          // waves per block
 constexpr int kSW = 128;         // columns per wave strip (2 per lane, 16-B accesses)
 constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live one per lane)
+// Item-list entries {first row | band flag, strip | rows << 20}: kBandBit set
+// when the item's rows ib-2 .. ie+2 contain a boundary-band row in its strip
+// (general march); clear → the plain unrolled march.
+constexpr int kBandBit = 1 << 30;
+constexpr int kRowMask = kBandBit - 1;
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
 
 void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,

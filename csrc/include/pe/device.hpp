@@ -164,7 +164,8 @@ class DeviceSolver {
  private:
   void build_tables(int64_t rows_hi, int64_t cols_hi);
   void set_fused_fields(double* x0, double* x1, double* w);
-  void setup_items();  // dynamic item lists per XCD shard (+ halo/interior overlap)
+  void setup_items();  // item lists: static LPT layout or dynamic per-XCD shards (+ halo/interior overlap)
+  void create_halo_stream();
   void choose_placement();
   void enqueue_iteration(int par);
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
@@ -199,6 +200,8 @@ class DeviceSolver {
   int2* ilist_ = nullptr;  // per shard: boundary items, heavy items, the rest (dev::KParams::ilist)
   int nslot_cap_ = 0;      // item-sum slots allocated
   int ov_lnsh_ = 1, ov_nb_ = 0, ov_reserve_ = 8, ov_debug_ = 0;
+  int wave_cap_ = 0;     // resident waves of the sweep grid (occupancy)
+  int static_waves_ = 0; // static list walk: waves the list is laid out for (0: no static list)
   int ov_lbase_[9] = {}, ov_lnb_[8] = {};
   unsigned long long ov_epoch_ = 0;  // overlapped sweeps since the state was last cleared (sig targets)
   hipStream_t hs_ = nullptr;

@@ -17,12 +17,13 @@ nat = native()
 configs = [(int(c.split(":")[0]), c.split(":")[1]) for c in os.environ.get("PROBE_CFG", "8:aspect").split(",")]
 envs = [e.strip() for e in os.environ.get("PROBE_ENV", "").split(";")]
 iters = int(os.environ.get("PROBE_ITERS", "400"))
-prob = pe.EllipseProblem(8192, 8192)
+GM, GN = (int(v) for v in os.environ.get("PROBE_GRID", "8192x8192").split("x"))
+prob = pe.EllipseProblem(GM, GN)
 os.environ["PE_OVERLAP"] = "0"
 for P, spec in configs:
-    g = D.grid(P, 8192, 8192, spec)
+    g = D.grid(P, GM, GN, spec)
     rank = P // 2
-    blk = nat.decompose(8192, 8192, g, rank)
+    blk = nat.decompose(GM, GN, g, rank)
     for env in envs:
         kv = dict(x.split("=") for x in env.split()) if env else {}
         saved = {k: os.environ.get(k) for k in kv}

@@ -29,12 +29,35 @@ def pct(a, q):
     return float(np.percentile(a, q)) if len(a) else float("nan")
 
 
-def summarise(st: np.ndarray, nitems: int) -> str:
-    it = st[: 4 * nitems].reshape(nitems, 4).astype(np.int64)
+def step_timeline(steps: np.ndarray) -> str:
+    """Median time (µs) from a wave's first item start to each stamped point of that item."""
+    s = steps.reshape(-1, 32).astype(np.int64)
+    s = s[s[:, 0] > 0]
+    if not len(s):
+        return "  (no step stamps)"
+    names = {1: "prologue issued", 2: "row classes in", 3: "prologue rows in", 31: "item end"}
+    out = ["  first-item timeline (median us after item start, n waves):"]
+    for c in range(1, 32):
+        v = s[:, c]
+        ok = v > 0
+        if ok.sum() < max(1, len(s) // 4):
+            continue
+        d = (v[ok] - s[ok, 0]) / 100.0
+        out.append(f"    {names.get(c, f'after row step {c - 6:+d}'):22s} {np.median(d):7.2f}  (n {ok.sum()})")
+    return "\n".join(out)
+
+
+def summarise(st: np.ndarray, nitems: int, nw: int) -> str:
+    steps = st[len(st) - 32 * nw:]
+    st = st[: len(st) - 32 * nw]
+    nslots = nitems
+    it = st[: 4 * nslots].reshape(nslots, 4).astype(np.int64)
+    it = it[it[:, 0] > 0]  # static layouts have empty positions
+    nitems = len(it)
     geo = it[:, 3].copy()
     strip = it[:, 2] >> 32
     it[:, 2] &= 0xFFFFFFFF  # wave id
-    wv_all = st[4 * nitems :].reshape(-1, 2).astype(np.int64)
+    wv_all = st[4 * nslots : 4 * nslots + 2 * nw].reshape(-1, 2).astype(np.int64)
     live = wv_all[:, 0] > 0
     wv = wv_all[live]
     t0 = wv[:, 0].min()
@@ -82,6 +105,7 @@ def summarise(st: np.ndarray, nitems: int) -> str:
     band = (geo >> 48) == 1
     if band.any():
         out.append(f"  band items: {band.sum()}  duration median {np.median(dur[band]):6.2f} us; others {np.median(dur[~band]):6.2f} us")
+    out.append(step_timeline(steps))
     return "\n".join(out)
 
 
@@ -89,10 +113,11 @@ def main():
     nat = native()
     configs = [(int(c.split(":")[0]), c.split(":")[1]) for c in os.environ.get("PROBE_CFG", "8:aspect,1:aspect").split(",")]
     envs = [e.strip() for e in os.environ.get("PROBE_ENV", "").split(";")]
-    prob = pe.EllipseProblem(8192, 8192)
+    GM, GN = (int(v) for v in os.environ.get("PROBE_GRID", "8192x8192").split("x"))
+    prob = pe.EllipseProblem(GM, GN)
     for P, spec in configs:
-        g = D.grid(P, 8192, 8192, spec)
-        blk = nat.decompose(8192, 8192, g, P // 2)
+        g = D.grid(P, GM, GN, spec)
+        blk = nat.decompose(GM, GN, g, P // 2)
         for env in envs:
             kv = dict(x.split("=") for x in env.split()) if env else {}
             saved = {k: os.environ.get(k) for k in kv}
@@ -110,7 +135,7 @@ def main():
                 s.run_iterations(1, False)
                 st = np.asarray(s.stamps())
                 print(f" one {sweep}-parity sweep:")
-                print(summarise(st, s.nitems), flush=True)
+                print(summarise(st, s.nitems, s.stamp_waves), flush=True)
             del s, comm
             for k, v in saved.items():
                 if v is None:
