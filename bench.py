@@ -99,11 +99,13 @@ def main() -> int:
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group)
         return float(t[0])
 
-    # warmup: compile graphs / first-touch / RCCL connections
+    # warmup: first-touch / RCCL connections, then instantiate every chunk
+    # graph the timed run will launch (no capture inside the timed region)
     solver.reset()
     if a.warmup > 0:
         solver.run_iterations(a.warmup, True)
     solver.synchronize()
+    solver.prepare_graphs(a.steps)
     solver.reset()  # the timed steps start a fresh solve (w⁰ = 0)
     solver.synchronize()
     torch.cuda.synchronize()
@@ -128,7 +130,9 @@ def main() -> int:
         barrier()
         res = full.solve()
         tm = res.timers
-        extra = dict(t_solver_s=maxval(tm["solver"]), iters_converged=int(res.iters), converged=bool(res.converged),
+        extra = dict(t_solver_s=maxval(tm["solver"]), t_setup_s=maxval(tm["setup"]), t_iterate_s=maxval(tm["iterate"]),
+                     t_breakdown_s={k: maxval(tm[k]) for k in ("gpu", "dot", "halo", "reduce", "copy")},
+                     iters_converged=int(res.iters), converged=bool(res.converged),
                      l2_err=float(res.l2_err), max_err=float(res.max_err),
                      solve_iters_per_s=float(res.iters) / maxval(tm["iterate"]))
         del full
@@ -157,8 +161,17 @@ def main() -> int:
             "parallelism": f"2d-decomp {blk.Px}x{blk.Py} (RCCL)" if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
             "algo": "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else "classic (2 kernels, 2 allreduces / iter)",
+            "decomposition": {"spec": a.decomp, "Px": blk.Px, "Py": blk.Py, "block": [blk.nx, blk.ny]},
             "transport": comm.name if comm is not None else "none",
             "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
+            "overlap": bool(solver.overlap),
+            "exchange_us_measured": round(solver.exchange_us, 2),
+            "item_order": "dynamic per-XCD queue" if solver.order == 3 else "static LPT layout",
+            "rows_per_item": solver.ti,
+            "chunk": solver.chunk,
+            "placement": {"candidates_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
+                          "chosen": solver.placement_choice, "search_s": round(solver.placement_s, 3)},
+            "construct_s": round(solver.construct_s, 3),
         },
         "valid": valid,
     }
@@ -167,6 +180,9 @@ def main() -> int:
         print(json.dumps(out), flush=True)
     if ctx is not None:
         barrier()
+    if not valid or (extra and not extra.get("converged", False)):
+        print(f"[bench] invalid run: status {int(st['status'])}, {int(st['iter'])} of {a.steps} steps", file=sys.stderr)
+        return 3
     return 0
 
 

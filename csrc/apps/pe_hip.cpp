@@ -107,23 +107,35 @@ int main(int argc, char** argv) {
   } else {
     std::unique_ptr<DeviceComm> comm;
     if (size > 1) comm = make_rccl_comm(exchange_uid(rank, size), rank, size);
-    if (comm && std::getenv("PE_ALLREDUCE") && std::string(std::getenv("PE_ALLREDUCE")) == "p2p")
-      comm = make_p2p_allreduce_comm(std::move(comm));
+    // per-iteration sums: the in-sweep P2P sum over xGMI by default (as the
+    // torch.distributed launcher, parallel/dist.py); PE_ALLREDUCE=rccl keeps
+    // ncclAllReduce.  The P2P set-up self-tests and falls back to RCCL.
+    const char* ar = std::getenv("PE_ALLREDUCE");
+    if (comm && !(ar && std::string(ar) == "rccl")) comm = make_p2p_allreduce_comm(std::move(comm));
     const ProcessGrid pg = process_grid_from_spec(decomp, size, P.M, P.N);
     const Block blk = decompose(P.M, P.N, pg, rank);
-    DeviceSolver solver(P, blk, comm.get(), opt);
-    r = solver.solve();
+    // T_solver = construction (allocation, tables, placement search) + solve
+    // (SolveResult) + teardown (the frees), as the reference's time_solver
+    // (poisson_mpi_cuda2.cu:1010-1016)
+    auto solver = std::make_unique<DeviceSolver>(P, blk, comm.get(), opt);
+    r = solver->solve();
+    const auto t_free = std::chrono::steady_clock::now();
+    solver.reset();
+    r.t.solver += std::chrono::duration<double>(std::chrono::steady_clock::now() - t_free).count();
   }
   const double total = std::chrono::duration<double>(std::chrono::steady_clock::now() - t_program).count();
   if (rank == 0) {
     if (args.flag("json")) {
       std::printf("{\"M\": %d, \"N\": %d, \"ranks\": %d, \"Px\": %d, \"Py\": %d, \"iters\": %lld, \"converged\": %s, "
-                  "\"t_solver\": %.6f, \"t_iterate\": %.6f, \"t_gpu\": %.6f, \"t_halo\": %.6f, \"t_reduce\": %.6f, "
+                  "\"t_solver\": %.6f, \"t_setup\": %.6f, \"t_construct\": %.6f, \"t_iterate\": %.6f, "
+                  "\"t_gpu\": %.6f, \"t_dot\": %.6f, \"dot_fused\": %s, \"t_copy\": %.6f, \"t_halo\": %.6f, "
+                  "\"t_reduce\": %.6f, \"timer_samples\": %.0f, "
                   "\"iters_per_s\": %.3f, \"l2_err\": %.6e, \"max_err\": %.6e, \"max_outside\": %.6e, \"total\": %.6f, "
                   "\"algo\": \"%s\"}\n",
                   P.M, P.N, size * vranks, r.Px, r.Py, (long long)r.iters, r.converged ? "true" : "false", r.t.solver,
-                  r.t.iterate, r.t.gpu, r.t.halo, r.t.reduce, r.iters / std::max(1e-12, r.t.iterate), r.l2_err,
-                  r.max_err, r.max_outside, total, r.algo.c_str());
+                  r.t.setup, r.t.construct, r.t.iterate, r.t.gpu, r.t.dot, r.t.dot_fused ? "true" : "false", r.t.copy,
+                  r.t.halo, r.t.reduce, r.t.sampled, r.iters / std::max(1e-12, r.t.iterate), r.l2_err, r.max_err,
+                  r.max_outside, total, r.algo.c_str());
     } else {
       std::cout << format_result_legacy(P, r, size, "stage4");
       std::printf("   Process grid %dx%d | iters/s ~ %.1f | L2 error in D ~ %.6e | max error in D ~ %.6e\n", r.Px, r.Py,

@@ -28,6 +28,9 @@ py::dict timers_dict(const Timers& t) {
   d["setup"] = t.setup;
   d["solver"] = t.solver;
   d["iterate"] = t.iterate;
+  d["construct"] = t.construct;
+  d["sampled"] = t.sampled;
+  d["dot_fused"] = t.dot_fused;
   return d;
 }
 
@@ -376,6 +379,12 @@ PYBIND11_MODULE(_native, m) {
              s.run_iterations(n, g);
            },
            py::arg("iters"), py::arg("use_graph") = true)
+      .def("prepare_graphs",
+           [](DeviceSolver& s, int64_t n) {
+             py::gil_scoped_release nogil;
+             s.prepare_graphs(n);
+           },
+           py::arg("iters"))
       .def("time_iterations",
            [](DeviceSolver& s, int64_t n, bool g) {
              py::gil_scoped_release nogil;
@@ -412,6 +421,10 @@ PYBIND11_MODULE(_native, m) {
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)
       .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
+      .def_property_readonly("placement_choice", &DeviceSolver::placement_choice)
+      .def_property_readonly("placement_s", &DeviceSolver::placement_seconds)
+      .def_property_readonly("construct_s", &DeviceSolver::construct_seconds)
+      .def_property_readonly("exchange_us", &DeviceSolver::exchange_us)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("order", [](DeviceSolver& s) { return s.params().order; })
       .def_property_readonly("xr", [](DeviceSolver& s) { return s.params().xr.peers != nullptr; },

@@ -64,6 +64,7 @@ static bool fused_possible(const Problem& P, const Block& b) {
 
 DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* comm, const SolveOptions& opt)
     : prob_(prob), blk_(blk), comm_(comm), opt_(opt), kp_(std::make_unique<KParams>()) {
+  const auto t_ctor = clk::now();
   if (!comm_) {
     self_ = std::make_unique<SelfDeviceComm>();
     comm_ = self_.get();
@@ -257,6 +258,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
   if (fused_) choose_placement();
+  if (comm_->size() > 1) measure_exchange();
   setup_items();
   if (static_waves_ > 0) {
     // static list walk: the grid is the one the list was laid out for (plus
@@ -286,6 +288,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   c = std::max(8, std::min(128, c));
   c += c & 1;
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
+  PE_HIP_CHECK(hipDeviceSynchronize());
+  ctor_s_ = secs(t_ctor, clk::now());
 }
 
 void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
@@ -299,6 +303,27 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
   k.r = k.x[0];
   k.p[0] = k.x[0] + plane_;
   k.p[1] = k.x[1] + plane_;
+}
+
+// Median time of this rank's halo exchange (every rank runs the same
+// number of collective exchanges here), then the max over ranks.
+void DeviceSolver::measure_exchange() {
+  Range range("pe.measure_exchange");
+  std::vector<float> t;
+  for (int i = 0; i < 9; ++i) {
+    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+    if (fused_) enqueue_exchange(0);
+    else comm_->exchange(halo_plan(), stream_);
+    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+    PE_HIP_CHECK(hipEventSynchronize(t1_));
+    float ms = 0.f;
+    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+    if (i >= 2) t.push_back(ms);  // two warm-up exchanges (connection set-up)
+  }
+  std::sort(t.begin(), t.end());
+  double us[1] = {1e3 * double(t[t.size() / 2])};
+  comm_->host_max(us, 1, stream_);
+  exchange_us_ = us[0];
 }
 
 // Halo/interior overlap (multi-rank single-sweep).  The sweep walks an item
@@ -322,8 +347,24 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
 void DeviceSolver::setup_items() {
   KParams& k = *kp_;
   const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
+  // Overlap only pays when the exchange costs more than what the overlap
+  // itself costs the sweep (boundary-first item order, blocks kept free for
+  // the halo stream: +9-11 µs per iteration on 2-8 ranks with a zero-latency
+  // transport, profiles/r1_overlap_probe_device_decomp.txt).  Auto: measure
+  // the real exchange here (max over ranks, so every rank decides the same)
+  // and overlap when it exceeds PE_OVERLAP_MIN_US (default 12).
+  // PE_OVERLAP=1 / 0 forces it on / off.
   const char* e = std::getenv("PE_OVERLAP");
-  overlap_ = fused_ && comm_->size() > 1 && nb && !(e && std::atoi(e) == 0);
+  overlap_ = false;
+  if (fused_ && comm_->size() > 1 && nb) {
+    if (e) {
+      overlap_ = std::atoi(e) != 0;
+    } else {
+      double min_us = 12.0;
+      if (const char* m = std::getenv("PE_OVERLAP_MIN_US")) min_us = std::atof(m);
+      overlap_ = exchange_us_ > min_us;
+    }
+  }
   // Lists: dynamic sweeps (order 3), static chunk-major sweeps (order 0:
   // heavy items split, below) and the overlap; orders 1 / 2 are plain
   // tuning walks.
@@ -472,7 +513,9 @@ void DeviceSolver::setup_items() {
     ov_lnb_[0] = nbnd;
     for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
     PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+    const auto tc = clk::now();
     PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+    copy_setup_s_ += secs(tc, clk::now());
     k.ilist = ilist_;
     k.lnsh = 1;
     k.lwaves = W;
@@ -540,7 +583,9 @@ void DeviceSolver::setup_items() {
   ov_lbase_[nsh] = int(all.size());
   if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
   PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+  const auto tc = clk::now();
   PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+  copy_setup_s_ += secs(tc, clk::now());
   // Every dynamic sweep walks the list (the plain one counts no boundary
   // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).
   k.ilist = ilist_;
@@ -570,6 +615,11 @@ void DeviceSolver::create_halo_stream() {
 // fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
 void DeviceSolver::choose_placement() {
   Range range("pe.placement_search");
+  struct Clock {
+    double& out;
+    clk::time_point t0 = clk::now();
+    ~Clock() { out = secs(t0, clk::now()); }
+  } clock{placement_s_};
   const double pts = double(blk_.nx) * double(blk_.ny);
   int tries = pts >= double(1 << 22) ? 8 : 1;
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
@@ -638,16 +688,22 @@ void DeviceSolver::choose_placement() {
     }
   for (void* sp : spacers) PE_HIP_CHECK(hipFree(sp));
   set_fused_fields(c[best].x0, c[best].x1, c[best].w);
+  placement_best_ = int(best);
   placement_ms_.clear();
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
 }
 
 DeviceSolver::~DeviceSolver() {
-  if (graph_) (void)hipGraphExecDestroy(graph_);
+  for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
   (void)hipEventDestroy(ev_[0]);
   (void)hipEventDestroy(ev_[1]);
   (void)hipEventDestroy(t0_);
   (void)hipEventDestroy(t1_);
+  for (const PhaseRec& r : recs_) {
+    (void)hipEventDestroy(r.a);
+    (void)hipEventDestroy(r.b);
+  }
+  for (hipEvent_t e : evpool_) (void)hipEventDestroy(e);
   (void)hipFree(fields_);
   if (xalt_) (void)hipFree(xalt_);
   if (walt_) (void)hipFree(walt_);
@@ -682,12 +738,16 @@ std::vector<unsigned long long> DeviceSolver::stamps() {
 
 void DeviceSolver::build_tables(int64_t rows_hi, int64_t cols_hi) {
   const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi);
+  const auto t0 = clk::now();
   PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
+  copy_setup_s_ += secs(t0, clk::now());
   const double* col = t.data();
   const double* row = t.data() + (rows_hi + 2) * 4;
   rowcls_host_ = row_classes(col, row, rows_hi, cols_hi);
   const std::vector<int>& rc = rowcls_host_;
+  const auto t1 = clk::now();
   PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
+  copy_setup_s_ += secs(t1, clk::now());
 }
 
 std::vector<Exchange> DeviceSolver::halo_plan() const {
@@ -764,7 +824,46 @@ void DeviceSolver::enqueue_fs_reduce(int par) {
   if (!kp_->xr.peers) comm_->allreduce_sum(st_->fs[par], 7, stream_);
 }
 
+// Sampled phase timing: event pairs from a pool; a record's events are read
+// (harvest) once the chunk that holds them has been waited for.
+hipEvent_t DeviceSolver::pooled_event() {
+  if (evpool_.empty()) {
+    hipEvent_t e = nullptr;
+    PE_HIP_CHECK(hipEventCreate(&e));
+    return e;
+  }
+  hipEvent_t e = evpool_.back();
+  evpool_.pop_back();
+  return e;
+}
+
+void DeviceSolver::mark_begin(int ph, hipStream_t s) {
+  if (!sampling_) return;
+  PhaseRec r{ph, sample_iter_, pooled_event(), nullptr};
+  PE_HIP_CHECK(hipEventRecord(r.a, s));
+  recs_.push_back(r);
+}
+
+void DeviceSolver::mark_end(hipStream_t s) {
+  if (!sampling_) return;
+  recs_.back().b = pooled_event();
+  PE_HIP_CHECK(hipEventRecord(recs_.back().b, s));
+}
+
+void DeviceSolver::harvest(size_t n) {
+  n = std::min(n, recs_.size());
+  for (size_t i = 0; i < n; ++i) {
+    float ms = 0.f;
+    PE_HIP_CHECK(hipEventElapsedTime(&ms, recs_[i].a, recs_[i].b));
+    samples_.push_back(PhaseSample{recs_[i].ph, recs_[i].iter, ms});
+    evpool_.push_back(recs_[i].a);
+    evpool_.push_back(recs_[i].b);
+  }
+  recs_.erase(recs_.begin(), recs_.begin() + std::ptrdiff_t(n));
+}
+
 void DeviceSolver::enqueue_iteration(int par) {
+  const int ncomm = comm_->size();
   if (fused_ && overlap_) {
     KParams ko = *kp_;
     ko.ilist = ilist_;
@@ -775,70 +874,126 @@ void DeviceSolver::enqueue_iteration(int par) {
     ko.nblocks0 = std::max(ov_lnsh_, kp_->nblocks0 - ov_reserve_);
     ov_epoch_ += 1;
     const unsigned long long target = ov_epoch_ * (unsigned long long)(ov_nb_);
-    dev::launch_S(ko, par, stream_);  // boundary items first in every shard
+    mark_begin(kPhSweep, stream_);
+    dev::launch_S(ko, par, stream_, false);  // boundary items first in every shard
+    mark_end(stream_);
+    if (ko.order == 3) {
+      mark_begin(kPhDot, stream_);
+      dev::launch_red(ko, par, stream_);
+      mark_end(stream_);
+    }
     if (ov_debug_ & 2) {
       dev::launch_wait_sig(ko, target, stream_);
+      mark_begin(kPhHalo, stream_);
       enqueue_exchange(par);
+      mark_end(stream_);
+    } else {
+      dev::launch_wait_sig(ko, target, hs_);  // the exchange starts once they are stored
+      mark_begin(kPhHalo, hs_);
+      for (const HaloPhase& ph : halo_phases(par)) {
+        comm_->exchange(ph.ex, hs_);
+        if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
+      }
+      mark_end(hs_);
+      PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
+      PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
+    }
+    if (!kp_->xr.peers) {
+      mark_begin(kPhReduce, stream_);
       enqueue_fs_reduce(par);
-      return;
+      mark_end(stream_);
     }
-    dev::launch_wait_sig(ko, target, hs_);  // the exchange starts once they are stored
-    for (const HaloPhase& ph : halo_phases(par)) {
-      comm_->exchange(ph.ex, hs_);
-      if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
+  } else if (fused_) {
+    mark_begin(kPhSweep, stream_);
+    dev::launch_S(*kp_, par, stream_, false);
+    mark_end(stream_);
+    if (kp_->order == 3) {
+      mark_begin(kPhDot, stream_);
+      dev::launch_red(*kp_, par, stream_);
+      mark_end(stream_);
     }
-    PE_HIP_CHECK(hipEventRecord(ev_halo_, hs_));
-    PE_HIP_CHECK(hipStreamWaitEvent(stream_, ev_halo_, 0));
-    enqueue_fs_reduce(par);
-    return;
+    if (ncomm > 1) {
+      mark_begin(kPhHalo, stream_);
+      enqueue_exchange(par);
+      mark_end(stream_);
+      if (!kp_->xr.peers) {
+        mark_begin(kPhReduce, stream_);
+        enqueue_fs_reduce(par);
+        mark_end(stream_);
+      }
+    }
+  } else {
+    mark_begin(kPhSweep, stream_);
+    dev::launch_F(*kp_, par, opt_.variant, stream_);
+    mark_end(stream_);
+    if (ncomm > 1) {
+      mark_begin(kPhReduce, stream_);
+      comm_->allreduce_sum(st_->red_F, 2, stream_);
+      mark_end(stream_);
+    }
+    mark_begin(kPhSweep, stream_);
+    dev::launch_G(*kp_, par, opt_.variant, stream_);
+    mark_end(stream_);
+    if (ncomm > 1) {
+      mark_begin(kPhHalo, stream_);
+      comm_->exchange(halo_plan(), stream_);
+      mark_end(stream_);
+      mark_begin(kPhReduce, stream_);
+      comm_->allreduce_sum(st_->red_G, 1, stream_);
+      mark_end(stream_);
+    }
   }
-  if (fused_) {
-    dev::launch_S(*kp_, par, stream_);
-    enqueue_exchange(par);
-    enqueue_fs_reduce(par);
-    return;
-  }
-  dev::launch_F(*kp_, par, opt_.variant, stream_);
-  comm_->allreduce_sum(st_->red_F, 2, stream_);
-  dev::launch_G(*kp_, par, opt_.variant, stream_);
-  comm_->exchange(halo_plan(), stream_);
-  comm_->allreduce_sum(st_->red_G, 1, stream_);
+  if (sampling_) ++sample_iter_;
 }
 
-bool DeviceSolver::graph_ready(int iters) {
-  if (graph_ && graph_iters_ == iters) return true;
+// Chunk graphs are cached per length (a run of n iterations uses the chunk
+// length and its remainder), so alternating lengths never re-capture.
+hipGraphExec_t DeviceSolver::graph_for(int iters) {
+  for (const auto& g : graphs_)
+    if (g.first == iters) return g.second;
   if (iters & 1) throw std::logic_error("graph chunks must have an even length");
-  if (graph_) {
-    PE_HIP_CHECK(hipGraphExecDestroy(graph_));
-    graph_ = nullptr;
-  }
   hipGraph_t g = nullptr;
+  hipGraphExec_t ge = nullptr;
   PE_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
   for (int it = 0; it < iters; ++it) enqueue_iteration(it & 1);
   PE_HIP_CHECK(hipStreamEndCapture(stream_, &g));
-  PE_HIP_CHECK(hipGraphInstantiate(&graph_, g, nullptr, nullptr, 0));
+  PE_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   PE_HIP_CHECK(hipGraphDestroy(g));
-  graph_iters_ = iters;
-  return true;
+  graphs_.emplace_back(iters, ge);
+  return ge;
 }
 
-void DeviceSolver::enqueue_chunk(int iters) {
+// (overlap: a graph may serialise the two streams' branches in any order,
+// and the halo branch waits on the sweep — always eager)
+bool DeviceSolver::graphs_usable() const { return comm_->capturable() && !overlap_; }
+
+void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   // The captured graph starts at parity 0 and has an even length; iterations
-  // that would break the p / x ping-pong parity run eagerly.
+  // that would break the p / x ping-pong parity run eagerly.  A sampled
+  // chunk runs eagerly with event pairs around the phases of its first
+  // `sample_iters` iterations.
   int it = 0;
-  // (overlap: a graph may serialise the two streams' branches in any order,
-  // and the halo branch waits on the sweep — always eager)
-  if (opt_.use_graph && comm_->capturable() && !overlap_ && par_ == 0 && iters >= 2) {
+  if (sample_iters == 0 && opt_.use_graph && graphs_usable() && par_ == 0 && iters >= 2) {
     const int n = iters - (iters & 1);
-    graph_ready(n);
-    PE_HIP_CHECK(hipGraphLaunch(graph_, stream_));
+    PE_HIP_CHECK(hipGraphLaunch(graph_for(n), stream_));
     it = n;
   }
   for (; it < iters; ++it) {
+    sampling_ = it < sample_iters;
     enqueue_iteration(par_);
     par_ ^= 1;
   }
+  sampling_ = false;
   PE_HIP_CHECK(hipGetLastError());
+}
+
+void DeviceSolver::prepare_graphs(int64_t iters) {
+  if (!graphs_usable()) return;
+  // the chunk lengths run_iterations(iters) launches from parity 0
+  const int64_t full = iters / chunk_, rest = iters % chunk_;
+  if (full > 0) graph_for(chunk_);
+  if (rest >= 2) graph_for(int(rest - (rest & 1)));
+  // the capture enqueued nothing: the stream state is unchanged
 }
 
 // ---------------------------------------------------------------------------
@@ -1018,9 +1173,17 @@ SolveResult DeviceSolver::solve() {
   res.algo = fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
+  // T_solver spans construction (allocation, tables, placement search) like
+  // the reference's time_solver (poisson_mpi_cuda2.cu:1010-1016); a second
+  // solve on the same solver reuses it and does not count it again.
+  const double construct = ctor_counted_ ? 0.0 : ctor_s_;
+  ctor_counted_ = true;
+  double copy_s = construct > 0 ? copy_setup_s_ : 0.0;
   int64_t start_iter = 0;
   if (!opt_.resume_path.empty()) {
+    const auto tc = clk::now();
     load_checkpoint(opt_.resume_path + ".r" + std::to_string(blk_.rank));
+    copy_s += secs(tc, clk::now());
     DevState s0;
     read_state(&s0);
     start_iter = s0.iter;
@@ -1028,105 +1191,85 @@ SolveResult DeviceSolver::solve() {
     reset();
   }
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
-  res.t.setup = secs(t_start, clk::now());
+  res.t.construct = construct;
+  res.t.setup = construct + secs(t_start, clk::now());
   const int64_t ck_every = opt_.checkpoint_path.empty() ? 0 : opt_.checkpoint_every;
-  if (opt_.timing && (ck_every > 0 || start_iter > 0))
-    throw std::invalid_argument("checkpoint / resume is not available with per-phase timing");
+
+  // Phase sampling: every `sample_every`-th chunk, its first two iterations
+  // (all of them with opt_.timing); no host sync beyond the per-chunk state
+  // read the loop does anyway.
+  int sample_every = 8, sample_iters = 2;
+  if (const char* e = std::getenv("PE_TIMER_SAMPLE")) sample_every = std::max(0, std::atoi(e));
+  if (opt_.timing) {
+    sample_every = 1;
+    sample_iters = chunk_;
+  }
+  samples_.clear();
+  sample_iter_ = start_iter;
 
   const int64_t cap = prob_.iter_cap();
   const auto t_loop = clk::now();
   roctxRangePushA("pe.iterate");
   PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-  if (opt_.timing) {
-    // Eager, per-phase event timing (host sync per chunk; diagnostic mode).
-    std::vector<hipEvent_t> ev(6);
-    for (auto& e : ev) PE_HIP_CHECK(hipEventCreate(&e));
-    int64_t k = 0;
-    DevState hs;
-    for (;;) {
-      for (int it = 0; it < chunk_ && fused_; ++it, ++k) {
-        const int par = int(k & 1);
-        PE_HIP_CHECK(hipEventRecord(ev[0], stream_));
-        dev::launch_S(*kp_, par, stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[1], stream_));
-        enqueue_exchange(par);
-        PE_HIP_CHECK(hipEventRecord(ev[2], stream_));
-        enqueue_fs_reduce(par);
-        PE_HIP_CHECK(hipEventRecord(ev[3], stream_));
-        PE_HIP_CHECK(hipEventSynchronize(ev[3]));
-        float t[3];
-        for (int q = 0; q < 3; ++q) PE_HIP_CHECK(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
-        res.t.gpu += t[0] * 1e-3;
-        res.t.halo += t[1] * 1e-3;
-        res.t.reduce += t[2] * 1e-3;
-      }
-      for (int it = 0; it < chunk_ && !fused_; ++it, ++k) {
-        const int par = int(k & 1);
-        PE_HIP_CHECK(hipEventRecord(ev[0], stream_));
-        dev::launch_F(*kp_, par, opt_.variant, stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[1], stream_));
-        comm_->allreduce_sum(st_->red_F, 2, stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[2], stream_));
-        dev::launch_G(*kp_, par, opt_.variant, stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[3], stream_));
-        comm_->exchange(halo_plan(), stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[4], stream_));
-        comm_->allreduce_sum(st_->red_G, 1, stream_);
-        PE_HIP_CHECK(hipEventRecord(ev[5], stream_));
-        PE_HIP_CHECK(hipEventSynchronize(ev[5]));
-        float t[5];
-        for (int q = 0; q < 5; ++q) PE_HIP_CHECK(hipEventElapsedTime(&t[q], ev[q], ev[q + 1]));
-        res.t.gpu += (t[0] + t[2]) * 1e-3;
-        res.t.reduce += (t[1] + t[4]) * 1e-3;
-        res.t.halo += t[3] * 1e-3;
-      }
-      read_state(&hs);
-      if (hs.done || k >= cap) break;
+  int64_t enq = start_iter;
+  int64_t next_ck = ck_every > 0 ? (start_iter / ck_every + 1) * ck_every : std::numeric_limits<int64_t>::max();
+  int64_t next_log = opt_.log_every > 0 ? opt_.log_every : 0;
+  int slot = 0;
+  struct Flight {
+    int slot;
+    size_t nrec;  // phase records enqueued up to and including this chunk
+  };
+  std::deque<Flight> inflight;
+  int64_t nchunk = 0;
+  bool stop = false;
+  for (;;) {
+    while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
+      const bool sample = sample_every > 0 && nchunk % sample_every == 0;
+      sample_iter_ = enq;
+      enqueue_chunk(chunk_, sample ? sample_iters : 0);
+      enq += chunk_;
+      sampling_ = sample;
+      sample_iter_ = enq - 1;
+      mark_begin(kPhCopy, stream_);
+      PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+      mark_end(stream_);
+      sampling_ = false;
+      PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
+      inflight.push_back(Flight{slot, recs_.size()});
+      slot ^= 1;
+      ++nchunk;
     }
-    par_ = int(k & 1);
-    for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
-  } else {
-    int64_t enq = start_iter;
-    int64_t next_ck = ck_every > 0 ? (start_iter / ck_every + 1) * ck_every : std::numeric_limits<int64_t>::max();
-    int64_t next_log = opt_.log_every > 0 ? opt_.log_every : 0;
-    int slot = 0;
-    std::deque<int> inflight;
-    bool stop = false;
-    for (;;) {
-      while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
-        enqueue_chunk(chunk_);
-        enq += chunk_;
-        PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
-        PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
-        inflight.push_back(slot);
-        slot ^= 1;
+    if (inflight.empty()) {
+      if (!stop && enq < cap && enq >= next_ck) {  // drained at a checkpoint boundary
+        const auto tc = clk::now();
+        save_checkpoint(opt_.checkpoint_path + ".r" + std::to_string(blk_.rank));
+        copy_s += secs(tc, clk::now());
+        while (next_ck <= enq) next_ck += ck_every;
+        continue;
       }
-      if (inflight.empty()) {
-        if (!stop && enq < cap && enq >= next_ck) {  // drained at a checkpoint boundary
-          save_checkpoint(opt_.checkpoint_path + ".r" + std::to_string(blk_.rank));
-          while (next_ck <= enq) next_ck += ck_every;
-          continue;
-        }
-        break;
-      }
-      const int s = inflight.front();
-      inflight.pop_front();
-      wait_event(ev_[s]);
-      if (hst_[s].done) stop = true;
-      if (opt_.log_every > 0 && blk_.rank == 0 && hst_[s].iter >= next_log) {  // chunk-granular progress log
-        std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[s].iter,
-                     hst_[s].last_diff, hst_[s].rz_cur);
-        while (next_log <= hst_[s].iter) next_log += opt_.log_every;
-      }
+      break;
+    }
+    const Flight f = inflight.front();
+    inflight.pop_front();
+    wait_event(ev_[f.slot]);
+    // this chunk's (and every earlier) phase events have completed
+    const size_t done_recs = std::min(f.nrec, recs_.size());
+    harvest(done_recs);
+    for (Flight& g : inflight) g.nrec -= std::min(g.nrec, done_recs);
+    if (hst_[f.slot].done) stop = true;
+    if (opt_.log_every > 0 && blk_.rank == 0 && hst_[f.slot].iter >= next_log) {  // chunk-granular progress log
+      std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[f.slot].iter,
+                   hst_[f.slot].last_diff, hst_[f.slot].rz_cur);
+      while (next_log <= hst_[f.slot].iter) next_log += opt_.log_every;
     }
   }
   PE_HIP_CHECK(hipEventRecord(t1_, stream_));
   PE_HIP_CHECK(hipEventSynchronize(t1_));
+  harvest(recs_.size());
   float ms = 0;
   PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
   res.t.iterate = secs(t_loop, clk::now());
   roctxRangePop();
-  if (!opt_.timing) res.t.gpu = ms * 1e-3;
 
   DevState hs;
   enqueue_wflush();
@@ -1152,10 +1295,40 @@ SolveResult DeviceSolver::solve() {
     res.max_err = hs.err[1];
     res.max_outside = hs.err[2];
   }
-  res.t.solver = secs(t_start, clk::now());
+  // Per-phase totals: mean per sampled live iteration (samples taken after
+  // the solve had stopped time no-op kernels and are dropped) × iterations
+  // run; the state read per chunk likewise × chunks run.
+  {
+    const int64_t run = std::max<int64_t>(0, hs.iter - start_iter);
+    double sum[kNPhase] = {};
+    std::vector<char> seen(size_t(std::max<int64_t>(1, run)), 0);
+    int64_t nit = 0, ncopy = 0;
+    for (const PhaseSample& x : samples_) {
+      if (x.iter >= hs.iter) continue;
+      sum[x.ph] += x.ms * 1e-3;
+      if (x.ph == kPhCopy) {
+        ++ncopy;
+      } else if (x.iter >= start_iter && !seen[size_t(x.iter - start_iter)]) {
+        seen[size_t(x.iter - start_iter)] = 1;
+        ++nit;
+      }
+    }
+    const double scale = nit > 0 ? double(run) / double(nit) : 0.0;
+    const int64_t chunks_run = (run + chunk_ - 1) / chunk_;
+    res.t.gpu = (sum[kPhSweep] + sum[kPhDot]) * scale;
+    res.t.dot = sum[kPhDot] * scale;
+    res.t.halo = sum[kPhHalo] * scale;
+    res.t.reduce = sum[kPhReduce] * scale;
+    res.t.copy = copy_s + (ncopy > 0 ? sum[kPhCopy] * double(chunks_run) / double(ncopy) : 0.0);
+    res.t.sampled = double(nit);
+    res.t.dot_fused = !(fused_ && kp_->order == 3);
+    if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
+  }
+  res.t.solver = construct + secs(t_start, clk::now());
   // Timers: max over ranks (reference MPI_Reduce(MAX), :962-966).
-  double tv[8] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate, 0};
-  comm_->host_max(tv, 8, stream_);
+  double tv[10] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate,
+                   res.t.dot, res.t.construct, 0};
+  comm_->host_max(tv, 10, stream_);
   res.t.gpu = tv[0];
   res.t.copy = tv[1];
   res.t.halo = tv[2];
@@ -1163,6 +1336,8 @@ SolveResult DeviceSolver::solve() {
   res.t.setup = tv[4];
   res.t.solver = tv[5];
   res.t.iterate = tv[6];
+  res.t.dot = tv[7];
+  res.t.construct = tv[8];
   return res;
 }
 

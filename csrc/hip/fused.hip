@@ -1010,7 +1010,7 @@ static auto with_kS(const KParams& k, F&& f) {
   }
 }
 
-void launch_S(const KParams& k, int par, hipStream_t s) {
+void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
   // each variant runs on its own resident grid (the deferring one needs
   // fewer registers: 3 waves/SIMD instead of 2)
   const int nb = par == 0 ? k.nblocks0 : k.nblocks;
@@ -1021,7 +1021,7 @@ void launch_S(const KParams& k, int par, hipStream_t s) {
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(k, go);
   else with_kS<2>(k, go);
-  if (k.order == 3) launch_red(k, par, s);
+  if (k.order == 3 && with_red) launch_red(k, par, s);
 }
 
 void launch_red(const KParams& k, int par, hipStream_t s) {

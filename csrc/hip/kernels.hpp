@@ -146,7 +146,7 @@ void launch_F(const KParams& k, int par, int variant, hipStream_t s);
 void launch_G(const KParams& k, int par, int variant, hipStream_t s);
 void launch_error(const KParams& k, hipStream_t s);
 // Single-sweep PCG (fused.hip): one kernel + one 7-scalar reduction per iteration.
-void launch_S(const KParams& k, int par, hipStream_t s);
+void launch_S(const KParams& k, int par, hipStream_t s, bool with_red = true);  // with_red: + launch_red (dynamic order)
 // Deterministic reduction of per-item sums + state update (dynamic / listed sweeps).
 void launch_red(const KParams& k, int par, hipStream_t s);
 // y-direction halo strips of buffer b: pack columns {1,2} / {ny-1,ny} of r,p

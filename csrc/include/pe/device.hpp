@@ -107,6 +107,9 @@ class DeviceSolver {
   // iterations (convergence test off when check_tol == false).
   void reset();
   void run_iterations(int64_t iters, bool use_graph);
+  // Capture + instantiate every chunk graph run_iterations(iters, true)
+  // will launch, so a timed run_iterations contains no capture.
+  void prepare_graphs(int64_t iters);
   double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
   void synchronize();
 
@@ -137,6 +140,10 @@ class DeviceSolver {
   bool overlap() const { return overlap_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
+  int placement_choice() const { return placement_best_; }       // index into placement_ms()
+  double placement_seconds() const { return placement_s_; }      // wall time of the search
+  double construct_seconds() const { return ctor_s_; }           // wall time of the constructor
+  double exchange_us() const { return exchange_us_; }            // measured halo exchange (multi-rank)
   hipStream_t stream() const { return stream_; }
 
   // Checkpoint / resume of the full device state of this rank (raw fields,
@@ -167,12 +174,31 @@ class DeviceSolver {
   void setup_items();  // item lists: static LPT layout or dynamic per-XCD shards (+ halo/interior overlap)
   void create_halo_stream();
   void choose_placement();
+  void measure_exchange();  // sets exchange_us_ (collective)
   void enqueue_iteration(int par);
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
   void enqueue_exchange(int buf);
   void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
-  void enqueue_chunk(int iters);
-  bool graph_ready(int iters);
+  void enqueue_chunk(int iters, int sample_iters = 0);
+  // Sampled phase timing (Timers): hipEvent pairs around the phases of the
+  // sampled iterations, read once their chunk has completed.
+  enum Phase { kPhSweep, kPhDot, kPhHalo, kPhReduce, kPhCopy, kNPhase };
+  struct PhaseRec {
+    int ph;
+    int64_t iter;  // iteration index (kPhCopy: the chunk's last), for dropping post-convergence samples
+    hipEvent_t a, b;
+  };
+  struct PhaseSample {
+    int ph;
+    int64_t iter;
+    float ms;
+  };
+  hipEvent_t pooled_event();
+  void mark_begin(int ph, hipStream_t s);
+  void mark_end(hipStream_t s);
+  void harvest(size_t n);  // read the first n records (their events have completed)
+  hipGraphExec_t graph_for(int iters);
+  bool graphs_usable() const;
 
   Problem prob_;
   Block blk_;
@@ -209,14 +235,22 @@ class DeviceSolver {
   dev::DevState* st_ = nullptr;
   dev::DevState* hst_ = nullptr;  // pinned, 2 slots
   std::unique_ptr<dev::KParams> kp_;
-  hipGraphExec_t graph_ = nullptr;
-  int graph_iters_ = 0;
+  std::vector<std::pair<int, hipGraphExec_t>> graphs_;  // instantiated chunk graphs, by length
   int chunk_ = 16;
   int par_ = 0;  // parity of the next iteration (x / p ping-pong)
   double watchdog_s_ = 0;   // PE_WATCHDOG_S: abort if a chunk makes no progress this long (0 = off)
   bool fault_stall_ = false;  // PE_FAULT_INJECT=stall: pretend the device never finishes (watchdog test)
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
+  std::vector<hipEvent_t> evpool_;
+  std::vector<PhaseRec> recs_;
+  std::vector<PhaseSample> samples_;
+  bool sampling_ = false;
+  int64_t sample_iter_ = 0;  // iteration index of the next enqueued iteration (sampled chunks)
+  double ctor_s_ = 0, copy_setup_s_ = 0, placement_s_ = 0;
+  bool ctor_counted_ = false;
+  int placement_best_ = 0;
+  double exchange_us_ = 0;  // measured halo exchange (max over ranks), multi-rank only  // the first solve() carries the construction time
 };
 
 // Per-row coefficient classes from the chord tables (see row_classes.cpp):

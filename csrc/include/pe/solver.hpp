@@ -18,18 +18,36 @@
 namespace pe {
 
 // Stage timers (seconds, this rank).  Categories follow the reference's
-// stage-4 printout (poisson_mpi_cuda2.cu:968-979) with honest semantics:
-//   gpu     — device kernel time (stencil/update kernels, incl. fused prec/dot)
-//   copy    — host<->device copies (≈0: everything is device-resident)
-//   halo    — halo exchange (P2P) time
-//   reduce  — global allreduce time (the reference lumps this into "MPI")
-//   prec    — preconditioner time (separately timed on CPU; fused on GPU)
-//   dot     — local dot-product time (separately timed on CPU; fused on GPU)
-//   setup   — assembly / allocation before the first iteration
-//   solver  — wall time of the whole solve (setup + iterations + teardown)
+// stage-4 printout (poisson_mpi_cuda2.cu:955-979, timers :695-700) with
+// honest semantics:
+//   gpu     — device compute kernels (device solver: the sweep / stencil
+//             kernels plus the reduction kernel; CPU solvers: the loops)
+//   dot     — the dot-product reduction (device: the item-sum reduction
+//             kernel, a subset of gpu — 0 and `dot_fused` when the fan-in
+//             runs inside the sweep kernel itself)
+//   copy    — host<->device copies (set-up tables, the per-chunk state read,
+//             checkpoints; everything else is device-resident)
+//   halo    — halo exchange (RCCL send/recv + unpack); 0 on one rank
+//   reduce  — cross-rank allreduce launches (0 on one rank, or when the
+//             sweep sums its scalars over ranks itself)
+//   prec    — preconditioner (CPU solvers; fused into the device sweep)
+//   setup   — construction (allocation, tables, item lists, placement
+//             search) + initial state, before the first iteration
+//   construct — the construction part of setup (device solver)
+//   solver  — wall time of the whole solve: setup + iterations + error
+//             (the reference's time_solver spans assembly, malloc, H2D, the
+//             loop and free, poisson_mpi_cuda2.cu:1010-1016)
+//   iterate — wall time of the iteration loop only
+// Device solver: the per-phase device times come from hipEvent pairs around
+// the phases of sampled iterations (no host sync in the loop; every
+// PE_TIMER_SAMPLE-th chunk, default 8, its first two iterations; every
+// iteration with SolveOptions::timing), scaled to the iterations run;
+// `sampled` is the number of iterations measured.
 struct Timers {
   double gpu = 0, copy = 0, halo = 0, reduce = 0, prec = 0, dot = 0, setup = 0, solver = 0;
   double iterate = 0;  // wall time of the iteration loop only
+  double construct = 0, sampled = 0;
+  bool dot_fused = false;
 };
 
 struct SolveOptions {
@@ -44,7 +62,7 @@ struct SolveOptions {
   // Device backend knobs.
   int chunk = 0;             // iterations enqueued per host check (0 = auto)
   bool use_graph = true;     // capture a chunk of iterations into a hipGraph
-  bool timing = false;       // per-phase hipEvent timing (adds host sync)
+  bool timing = false;       // time every iteration's phases (default: a sample of them)
   bool check_tol = true;     // false: never stop on ‖Δw‖ (fixed-iteration benchmarking)
   int variant = 0;           // device arithmetic: 0 fast (1/h², 1/D), 1 reference expression trees
   // Device algorithm: 0 auto (single-sweep when the variant / decomposition

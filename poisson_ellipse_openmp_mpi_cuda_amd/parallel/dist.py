@@ -31,6 +31,8 @@ from .._loader import native
 
 
 _GLOO = None
+_COMMS: dict = {}  # one native communicator per (world, transport) for the whole process
+_UID_CALLS = 0
 
 
 @dataclass
@@ -97,24 +99,47 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
     nat.set_device(ctx.local_rank % max(1, nat.device_count()))
     if ctx.world == 1:
         return None
-    if os.environ.get("PE_COMM", "rccl") == "host":
+    transport = os.environ.get("PE_COMM", "rccl")
+    default = "rccl" if transport == "host" else "p2p"
+    allreduce = os.environ.get("PE_ALLREDUCE", default)
+    key = (ctx.world, ctx.rank, transport, allreduce, tag)
+    if key in _COMMS:  # every solve of the job reuses it (one RCCL init, one IPC mapping)
+        return _COMMS[key]
+    if transport == "host":
         global _GLOO
         if _GLOO is None:
             _GLOO = dist.new_group(backend="gloo")
         comm = nat.make_host_staged_comm(ctx.rank, ctx.world, *gloo_callbacks(_GLOO))
     else:
+        # a fresh store key per communicator creation (every rank counts its
+        # calls identically), deleted once every rank has read it
+        global _UID_CALLS
+        _UID_CALLS += 1
         store = _store()
-        key = f"{tag}/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}"
+        skey = f"{tag}/{os.environ.get('TORCHELASTIC_RUN_ID', 'run')}/{_UID_CALLS}"
         if ctx.rank == 0:
             uid = nat.rccl_unique_id()
-            store.set(key, uid)
+            store.set(skey, uid)
         else:
-            uid = store.get(key)
+            uid = store.get(skey)
         comm = nat.make_rccl_comm(bytes(uid), ctx.rank, ctx.world)
-    default = "rccl" if os.environ.get("PE_COMM", "rccl") == "host" else "p2p"
-    if os.environ.get("PE_ALLREDUCE", default) == "p2p":
+        dist.barrier(group=_gloo_group())
+        if ctx.rank == 0:
+            try:
+                store.delete_key(skey)
+            except Exception:  # older stores: the unique key is enough
+                pass
+    if allreduce == "p2p":
         nat.use_p2p_allreduce(comm)  # one-shot xGMI allreduce of the per-iteration sums
+    _COMMS[key] = comm
     return comm
+
+
+def _gloo_group():
+    global _GLOO
+    if _GLOO is None:
+        _GLOO = dist.new_group(backend="gloo")
+    return _GLOO
 
 
 # ---------------------------------------------------------------------------
