@@ -416,6 +416,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
+      .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))

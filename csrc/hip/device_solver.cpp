@@ -260,6 +260,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (fused_) choose_placement();
   if (comm_->size() > 1) measure_exchange();
   setup_items();
+  setup_resident();
   if (static_waves_ > 0) {
     // static list walk: the grid is the one the list was laid out for (plus
     // the blocks the overlap keeps free for the halo stream)
@@ -287,6 +288,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   int c = int(0.5e-3 / t_iter);
   c = std::max(8, std::min(128, c));
   c += c & 1;
+  if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   PE_HIP_CHECK(hipDeviceSynchronize());
   ctor_s_ = secs(t_ctor, clk::now());
@@ -596,6 +598,83 @@ void DeviceSolver::setup_items() {
   if (overlap_) create_halo_stream();
 }
 
+// LDS-resident geometry: tiles of one 124-column strip × R rows (the
+// streaming sweep's strips), one workgroup each, at most one per CU, R ≥ 8
+// where the block allows and ≤ kResMaxRows; the band-coefficient table is
+// sized from the host row classes (the kernel's exact band test).
+void DeviceSolver::setup_resident() {
+  KParams& k = *kp_;
+  resident_ = false;
+  const char* e = std::getenv("PE_RESIDENT");
+  if (e && std::atoi(e) == 0) return;
+  if (!fused_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0) return;
+  const int nx = int(blk_.nx);
+  int cus = 256;
+  {
+    int dev = 0;
+    PE_HIP_CHECK(hipGetDevice(&dev));
+    PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int nstrips = k.nstrips;
+  if (nstrips > cus) return;
+  const int ntr = std::max(1, std::min(cus / nstrips, nx / 8));
+  if (nx < 2 * ntr) return;
+  std::vector<int> rs(size_t(ntr) + 1);
+  for (int t = 0; t <= ntr; ++t) rs[size_t(t)] = 1 + int(int64_t(t) * nx / ntr);
+  int rcap = 0;
+  for (int t = 0; t < ntr; ++t) rcap = std::max(rcap, rs[size_t(t) + 1] - rs[size_t(t)]);
+  if (rcap > dev::kResMaxRows) return;
+  // band nodes per tile region (rows I0-2 .. I0+R+1, columns J0-2 .. J0+125)
+  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
+  int nb_max = 0;
+  for (int t = 0; t < ntr; ++t)
+    for (int sx = 0; sx < nstrips; ++sx) {
+      int nb = 0;
+      const int J0 = 1 + dev::kFSW * sx;
+      for (int q = rs[size_t(t)] - 2; q < rs[size_t(t) + 1] + 2; ++q) {
+        if (q + 1 < 0 || q + 1 >= rows_tab) continue;
+        const int* r = &rowcls_host_[size_t(q + 1) * 4];
+        for (int c = J0 - 2; c < J0 + 126; ++c)
+          if (c >= r[2] && c <= r[3] && !(c >= r[0] && c <= r[1])) ++nb;
+      }
+      nb_max = std::max(nb_max, nb);
+    }
+  const int nbcap = nb_max + 8;
+  const size_t lds = dev::resident_lds_bytes(rcap, nbcap);
+  if (lds > 163840) return;
+  const int per_cu = dev::resident_max_blocks_per_cu(lds);
+  const int nwg = ntr * nstrips;
+  if (per_cu < 1 || nwg > per_cu * cus) return;
+  rp_ = std::make_unique<dev::ResParams>();
+  dev::ResParams& r = *rp_;
+  std::memset(&r, 0, sizeof(r));
+  r.nstrips = nstrips;
+  r.ntr = ntr;
+  r.nwg = nwg;
+  r.rcap = rcap;
+  r.nbcap = nbcap;
+  r.lds_bytes = unsigned(lds);
+  r.timeout_ticks = 200000000LL;  // 2 s per barrier wait
+  if (const char* t = std::getenv("PE_RES_TIMEOUT_S")) r.timeout_ticks = (long long)(std::atof(t) * 1e8);
+  PE_HIP_CHECK(hipMalloc(&res_rowstart_, sizeof(int) * rs.size()));
+  PE_HIP_CHECK(hipMemcpy(res_rowstart_, rs.data(), sizeof(int) * rs.size(), hipMemcpyHostToDevice));
+  const size_t nedge = size_t(2) * size_t(nwg) * dev::kResEdge, npart = size_t(2) * size_t(nwg) * 8;
+  PE_HIP_CHECK(hipMalloc(&res_buf_, sizeof(double) * (nedge + npart)));
+  PE_HIP_CHECK(hipMemset(res_buf_, 0, sizeof(double) * (nedge + npart)));
+  PE_HIP_CHECK(hipMalloc(&res_ctr_, sizeof(unsigned) * 8 * 32));
+  if (const char* t = std::getenv("PE_RES_STAMPS"); t && std::atoi(t) == 1) {
+    nstamps_ = size_t(nwg) * dev::kResStampIters * 8;
+    PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
+    PE_HIP_CHECK(hipMemset(stamps_, 0, sizeof(unsigned long long) * nstamps_));
+    r.stamps = stamps_;
+  }
+  r.rowstart = res_rowstart_;
+  r.edges = res_buf_;
+  r.partials = res_buf_ + nedge;
+  r.ctr = res_ctr_;
+  resident_ = true;
+}
+
 void DeviceSolver::create_halo_stream() {
   int least = 0, greatest = 0;
   PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
@@ -714,6 +793,9 @@ DeviceSolver::~DeviceSolver() {
   if (hist_) (void)hipFree(hist_);
   if (stamps_) (void)hipFree(stamps_);
   if (ilist_) (void)hipFree(ilist_);
+  if (res_rowstart_) (void)hipFree(res_rowstart_);
+  if (res_buf_) (void)hipFree(res_buf_);
+  if (res_ctr_) (void)hipFree(res_ctr_);
   if (hs_) (void)hipStreamDestroy(hs_);
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   (void)hipFree(st_);
@@ -839,7 +921,7 @@ hipEvent_t DeviceSolver::pooled_event() {
 
 void DeviceSolver::mark_begin(int ph, hipStream_t s) {
   if (!sampling_) return;
-  PhaseRec r{ph, sample_iter_, pooled_event(), nullptr};
+  PhaseRec r{ph, sample_iter_, 1, pooled_event(), nullptr};
   PE_HIP_CHECK(hipEventRecord(r.a, s));
   recs_.push_back(r);
 }
@@ -855,7 +937,7 @@ void DeviceSolver::harvest(size_t n) {
   for (size_t i = 0; i < n; ++i) {
     float ms = 0.f;
     PE_HIP_CHECK(hipEventElapsedTime(&ms, recs_[i].a, recs_[i].b));
-    samples_.push_back(PhaseSample{recs_[i].ph, recs_[i].iter, ms});
+    samples_.push_back(PhaseSample{recs_[i].ph, recs_[i].iter, recs_[i].n, ms});
     evpool_.push_back(recs_[i].a);
     evpool_.push_back(recs_[i].b);
   }
@@ -965,7 +1047,7 @@ hipGraphExec_t DeviceSolver::graph_for(int iters) {
 
 // (overlap: a graph may serialise the two streams' branches in any order,
 // and the halo branch waits on the sweep — always eager)
-bool DeviceSolver::graphs_usable() const { return comm_->capturable() && !overlap_; }
+bool DeviceSolver::graphs_usable() const { return comm_->capturable() && !overlap_ && !resident_; }
 
 void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   // The captured graph starts at parity 0 and has an even length; iterations
@@ -973,6 +1055,24 @@ void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   // chunk runs eagerly with event pairs around the phases of its first
   // `sample_iters` iterations.
   int it = 0;
+  if (resident_ && iters > 0) {
+    // one launch for the whole chunk (always timed: two events per chunk)
+    dev::ResParams r = *rp_;
+    r.niter = iters;
+    r.par0 = par_;
+    PE_HIP_CHECK(hipMemsetAsync(res_ctr_, 0, sizeof(unsigned) * 8 * 32, stream_));
+    const bool was = sampling_;
+    sampling_ = true;
+    mark_begin(kPhSweep, stream_);
+    recs_.back().n = iters;
+    dev::launch_resident(*kp_, r, stream_);
+    mark_end(stream_);
+    sampling_ = was;
+    sample_iter_ += iters;
+    par_ ^= iters & 1;
+    PE_HIP_CHECK(hipGetLastError());
+    return;
+  }
   if (sample_iters == 0 && opt_.use_graph && graphs_usable() && par_ == 0 && iters >= 2) {
     const int n = iters - (iters & 1);
     PE_HIP_CHECK(hipGraphLaunch(graph_for(n), stream_));
@@ -1170,7 +1270,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
-  res.algo = fused_ ? "fused" : "classic";
+  res.algo = resident_ ? "resident" : fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   // T_solver spans construction (allocation, tables, placement search) like
@@ -1308,6 +1408,8 @@ SolveResult DeviceSolver::solve() {
       sum[x.ph] += x.ms * 1e-3;
       if (x.ph == kPhCopy) {
         ++ncopy;
+      } else if (x.n > 1) {  // a resident launch: the iterations it ran before the solve stopped
+        nit += std::min<int64_t>(x.n, hs.iter - x.iter);
       } else if (x.iter >= start_iter && !seen[size_t(x.iter - start_iter)]) {
         seen[size_t(x.iter - start_iter)] = 1;
         ++nit;

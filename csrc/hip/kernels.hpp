@@ -140,6 +140,36 @@ constexpr int kBandBit = 1 << 30;
 constexpr int kRowMask = kBandBit - 1;
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
 
+// LDS-resident single sweep (resident.hip): small single-rank blocks run many
+// iterations in ONE launch.  The block is cut into tiles of one 124-column
+// strip × R rows, one workgroup per tile (≤ one per CU, all co-resident);
+// each keeps r, p (with a 2-deep ring) in LDS and w in registers, and per
+// iteration exchanges only the second ring of r with its 8 neighbours and
+// its 7 partial sums through global memory, behind one grid barrier.
+constexpr int kResThreads = 512;   // 8 waves
+constexpr int kResMaxRows = 64;    // R ≤ 64 rows per tile
+constexpr int kResEdge = 376;      // edge record: rowT[124] rowB[124] colL[64] colR[64]
+struct ResParams {
+  int nstrips, ntr, nwg;             // tiles: nwg = ntr × nstrips, tile = (band tr, strip s), wg = tr·nstrips + s
+  int rcap, nbcap;                   // LDS sizing: max tile rows, band-coefficient slots
+  const int* rowstart;               // ntr+1: first local row of band tr (rowstart[ntr] = nx + 1)
+  double* edges;                     // [2][nwg][kResEdge]
+  double* partials;                  // [2][nwg][8]
+  unsigned* ctr;                     // [8][32] barrier counters (zeroed before every launch)
+  int niter;                         // iterations of this launch
+  int par0;                          // parity of its first iteration
+  long long timeout_ticks;           // barrier wait limit (s_memrealtime ticks, 100 MHz)
+  unsigned lds_bytes;
+  // PE_RES_STAMPS=1 diagnostic: s_memrealtime of every workgroup at 8 points
+  // of its first kResStampIters iterations, [nwg][kResStampIters][8] (null: off)
+  unsigned long long* stamps;
+};
+constexpr int kResStampIters = 64;
+size_t resident_lds_bytes(int rcap, int nbcap);
+// Launch n iterations (the caller zeroes rp.ctr on the same stream first).
+void launch_resident(const KParams& k, const ResParams& rp, hipStream_t s);
+int resident_max_blocks_per_cu(size_t lds_bytes);
+
 void launch_init(const KParams& k, int init_random, unsigned long long seed, double amp, int variant,
                  hipStream_t s);
 void launch_F(const KParams& k, int par, int variant, hipStream_t s);

@@ -92,6 +92,7 @@ std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, Callba
 namespace dev {
 struct DevState;
 struct KParams;
+struct ResParams;
 }  // namespace dev
 
 class DeviceSolver {
@@ -137,6 +138,9 @@ class DeviceSolver {
   std::vector<HaloPhase> halo_phases(int buf) const;
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
+  // LDS-resident single sweep (resident.hip): small single-rank blocks run
+  // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
+  bool resident() const { return resident_; }
   bool overlap() const { return overlap_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
@@ -175,6 +179,7 @@ class DeviceSolver {
   void create_halo_stream();
   void choose_placement();
   void measure_exchange();  // sets exchange_us_ (collective)
+  void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
   void enqueue_iteration(int par);
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
   void enqueue_exchange(int buf);
@@ -185,12 +190,13 @@ class DeviceSolver {
   enum Phase { kPhSweep, kPhDot, kPhHalo, kPhReduce, kPhCopy, kNPhase };
   struct PhaseRec {
     int ph;
-    int64_t iter;  // iteration index (kPhCopy: the chunk's last), for dropping post-convergence samples
+    int64_t iter;  // first iteration covered (kPhCopy: the chunk's last), for dropping post-convergence samples
+    int64_t n;     // iterations covered (a resident launch covers its whole chunk)
     hipEvent_t a, b;
   };
   struct PhaseSample {
     int ph;
-    int64_t iter;
+    int64_t iter, n;
     float ms;
   };
   hipEvent_t pooled_event();
@@ -250,6 +256,11 @@ class DeviceSolver {
   double ctor_s_ = 0, copy_setup_s_ = 0, placement_s_ = 0;
   bool ctor_counted_ = false;
   int placement_best_ = 0;
+  bool resident_ = false;
+  std::unique_ptr<dev::ResParams> rp_;
+  int* res_rowstart_ = nullptr;
+  double* res_buf_ = nullptr;  // edges then partials
+  unsigned* res_ctr_ = nullptr;
   double exchange_us_ = 0;  // measured halo exchange (max over ranks), multi-rank only  // the first solve() carries the construction time
 };
 

@@ -392,3 +392,71 @@ def test_device_history_matches_cpu(gpu, algo):
     assert len(d.history) == d.iters == c.iters
     np.testing.assert_allclose(d.history, c.history, rtol=1e-6)
     assert d.history[-1] < prob.tol <= d.history[-2]
+
+
+# ---- LDS-resident single sweep (resident.hip) -------------------------------
+@pytest.mark.parametrize("M,N", [(40, 40), (257, 129), (400, 600), (800, 1200), (130, 1000), (1000, 130)])
+def test_resident_matches_streaming(gpu, M, N, monkeypatch):
+    """The resident kernel (tiles of 124 columns × R rows, one workgroup each,
+    ring-2 exchange + 7 partial sums per iteration behind a grid barrier)
+    against the streaming single sweep: same iteration count, same solution
+    (different summation order only), golden counts on the published grids."""
+    prob = EllipseProblem(M, N)
+    monkeypatch.setenv("PE_RESIDENT", "0")
+    ref = solve(prob, backend="hip", return_w=True)
+    monkeypatch.delenv("PE_RESIDENT")
+    res = solve(prob, backend="hip", return_w=True)
+    assert res.algo == "resident" and ref.algo == "fused"
+    assert res.iters == ref.iters
+    if (M, N, "weighted") in GOLDEN_ITERS:
+        assert res.iters == GOLDEN_ITERS[(M, N, "weighted")]
+    np.testing.assert_allclose(res.w, ref.w, rtol=0, atol=1e-10)
+    assert res.l2_err == pytest.approx(ref.l2_err, rel=1e-7)
+
+
+@pytest.mark.parametrize("parts", [[60], [7, 13, 40], [1, 1, 58]])
+def test_resident_launch_split_bitwise(gpu, nat, parts):
+    """A resident launch starts from and ends in the streaming layout/state:
+    how the iterations are split into launches does not change one bit."""
+    prob = EllipseProblem(300, 700)
+    blk = D.block(300, 700, 1, 0)
+    out = []
+    for split in ([60], parts):
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        opt.chunk = 1 << 20
+        s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
+        assert s.resident
+        s.reset()
+        for n in split:
+            s.run_iterations(n, True)
+        s.synchronize()
+        out.append((s.state(), s.w()))
+    (a, wa), (b, wb) = out
+    assert a["iter"] == b["iter"] == 60
+    # the live sums are those of the last iteration (parity 1 after 60 from parity 0)
+    assert a["fs"][1] == b["fs"][1] and a["alpha"] == b["alpha"] and a["gprev"] == b["gprev"]
+    assert np.array_equal(wa, wb)
+
+
+def test_resident_state_matches_streaming_kernel(gpu, nat, monkeypatch):
+    """α, β and the 7 sums after 25 resident iterations agree with the
+    streaming kernel's to rounding (the recurrence is the same)."""
+    prob = EllipseProblem(400, 600)
+    blk = D.block(400, 600, 1, 0)
+    st = {}
+    for flag in ("1", "0"):
+        monkeypatch.setenv("PE_RESIDENT", flag)
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
+        assert s.resident == (flag == "1")
+        s.reset()
+        s.run_iterations(25, False)
+        s.synchronize()
+        st[flag] = (s.state(), s.w())
+    (a, wa), (b, wb) = st["1"], st["0"]
+    assert a["iter"] == b["iter"] == 25
+    assert a["alpha"] == pytest.approx(b["alpha"], rel=1e-11)
+    assert a["beta"] == pytest.approx(b["beta"], rel=1e-11)
+    np.testing.assert_allclose(wa, wb, rtol=0, atol=1e-13 * np.abs(wb).max())
