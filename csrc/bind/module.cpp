@@ -515,4 +515,22 @@ PYBIND11_MODULE(_native, m) {
     return py::make_tuple(to_array(std::move(a), blk.rows, blk.pitch), to_array(std::move(b), blk.rows, blk.pitch),
                           to_array(std::move(D), blk.rows, blk.pitch));
   });
+  m.def("device_coefficients_fast", [](const Problem& P, const Block& blk) {
+    SolveOptions opt;
+    opt.algo = 2;  // single-sweep tables (row classes / chord tables past the halo)
+    DeviceSolver s(P, blk, nullptr, opt);
+    const int64_t rows = blk.nx + 2, cols = blk.ny + 2;
+    const size_t n = size_t(rows * cols), bytes = sizeof(double) * n;
+    double* d = nullptr;
+    PE_HIP_CHECK(hipMalloc(&d, 3 * bytes));
+    dev::launch_coef_fast(s.params(), d, d + n, d + 2 * n, s.stream());
+    PE_HIP_CHECK(hipStreamSynchronize(s.stream()));
+    std::vector<double> a(n), b(n), di(n);
+    PE_HIP_CHECK(hipMemcpy(a.data(), d, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipMemcpy(b.data(), d + n, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipMemcpy(di.data(), d + 2 * n, bytes, hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipFree(d));
+    return py::make_tuple(to_array(std::move(a), rows, cols), to_array(std::move(b), rows, cols),
+                          to_array(std::move(di), rows, cols));
+  });
 }

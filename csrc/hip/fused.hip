@@ -985,7 +985,31 @@ __global__ void kUnpack(KParams k, int b) {
   }
 }
 
+// Test op: the division-free coefficients the single-sweep kernels evaluate
+// (cset_rc from the row classes and chord tables) for every node of the block
+// plus its 1-wide ring, dense [(nx+2) × (ny+2)]: a(li, lj), b(li, lj), 1/D.
+__global__ void kCoefFast(KParams k, double* a, double* b, double* dinv) {
+  const int64_t W = k.ny + 2, n = (k.nx + 2) * W;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t li = idx / W, lj = idx % W;
+    const int* rc = k.rowcls + (li + 1) * 4;
+    const RowCls c{rc[0], rc[1], rc[2], rc[3]};
+    const double* ctr = k.colT + (li + 1) * 4;
+    const double* tv = k.rowT + (lj + 1) * 4;
+    const CS x = cset_rc(k, c, CT{ctr[0], ctr[4], ctr[1], ctr[2]}, lj, TV{tv[0], tv[1], tv[2], tv[6]});
+    a[idx] = x.a0;
+    b[idx] = x.b0;
+    dinv[idx] = x.d;
+  }
+}
+
 }  // namespace
+
+void launch_coef_fast(const KParams& k, double* a, double* b, double* dinv, hipStream_t s) {
+  const int64_t n = (k.nx + 2) * (k.ny + 2);
+  const unsigned g = unsigned(std::min<int64_t>(4096, std::max<int64_t>(1, (n + 255) / 256)));
+  hipLaunchKernelGGL(kCoefFast, dim3(g), dim3(256), 0, s, k, a, b, dinv);
+}
 
 // Kernel configuration (PE_SKERNEL, for tuning sweeps): 0 default = 4 rows
 // of loads in flight per wave + non-temporal w/output streams (8192² sweep:

@@ -197,6 +197,8 @@ void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hip
 // Debug/test ops (single-shot, no convergence logic).
 void launch_apply_A(const KParams& k, const double* p, double* Ap, hipStream_t s);
 void launch_coef(const KParams& k, double* a, double* b, double* D, hipStream_t s);
+// Single-sweep (division-free) coefficients of every node incl. the ring, dense (nx+2) × (ny+2).
+void launch_coef_fast(const KParams& k, double* a, double* b, double* dinv, hipStream_t s);
 int grid_blocks(const KParams& k);
 void launch_delay(double us, hipStream_t s);  // test transport: stream-ordered busy wait
 // Resident 256-thread blocks per CU of the marching kernels (occupancy API;

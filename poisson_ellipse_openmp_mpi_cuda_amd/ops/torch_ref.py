@@ -162,6 +162,59 @@ def pcg(prob: EllipseProblem, device="cpu", w0: Optional[torch.Tensor] = None, m
     return TorchPCGResult(k, converged, w, l2, mx, hist)
 
 
+@dataclass
+class SingleSweepState:
+    iters: int
+    sums: list    # per iteration k = 0 (S_0) .. K: the 7 unweighted sums of sweep k
+    alpha: list   # α_k, β_k for k = 1 .. K
+    beta: list
+    r: torch.Tensor
+    p: torch.Tensor
+    w: torch.Tensor
+
+
+def single_sweep(prob: EllipseProblem, iters: int, device="cpu") -> SingleSweepState:
+    """The single-reduction recurrence of the device sweep kernels
+    (csrc/hip/fused.hip header, sweep_scalars), on the reference operator.
+
+    Sweep 0 (S_0): z₀ = D⁻¹r₀, q₀ = A z₀ and their sums.  Sweep k ≥ 1, from
+    sweep k-1's sums R = {(r,z) (z,q) (z,s) (p,s) (z,z) (z,p) (p,p)}:
+        g = R₀h², β = g/g_prev (0 at k = 1), den = (R₁ + 2βR₂ + β²R₃)h², α = g/den
+        p = z + βp, s = Ap, w += αp, r -= αs, z = D⁻¹r, q = Az → sums of sweep k.
+    Algebraically the reference PCG (stage2-mpi/poisson_mpi_decomp.cpp:400-457)."""
+    a, b, B = assemble(prob, device)
+    h1, h2 = prob.h1, prob.h2
+    hh = h1 * h2
+    D = diag(a, b, h1, h2)
+    inner = lambda u, v: float((u[1:-1, 1:-1] * v[1:-1, 1:-1]).sum())  # noqa: E731  (unweighted)
+    r = B.clone()
+    p = torch.zeros_like(B)
+    w = torch.zeros_like(B)
+    s = torch.zeros_like(B)
+    z = apply_Dinv(r, D)
+    q = apply_A(z, a, b, h1, h2)
+    sums = [[inner(r, z), inner(z, q), inner(z, s), inner(p, s), inner(z, z), inner(z, p), inner(p, p)]]
+    alphas, betas = [], []
+    gprev = 0.0
+    for k in range(1, iters + 1):
+        R = sums[-1]
+        g = R[0] * hh
+        beta = 0.0 if k == 1 else g / gprev
+        den = R[1] * hh + 2.0 * beta * (R[2] * hh) + beta * beta * (R[3] * hh)
+        alpha = g / den
+        p = z + beta * p
+        s = apply_A(p, a, b, h1, h2)
+        w = w + alpha * p
+        r = r - alpha * s
+        z = apply_Dinv(r, D)
+        q = apply_A(z, a, b, h1, h2)
+        sums.append([inner(r, z), inner(z, q), inner(z, s), inner(p, s), inner(z, z), inner(z, p), inner(p, p)])
+        alphas.append(alpha)
+        betas.append(beta)
+        gprev = g
+    return SingleSweepState(iters, sums, alphas, betas, r, p, w)
+
+
 def error_vs_analytic(prob: EllipseProblem, w: torch.Tensor):
     """(L2 error in D, h-weighted; max error in D) against u = F(1-cx x²-cy y²)/(2cx+2cy)."""
     x, y = _grid(prob, w.device)

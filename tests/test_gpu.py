@@ -460,3 +460,80 @@ def test_resident_state_matches_streaming_kernel(gpu, nat, monkeypatch):
     assert a["alpha"] == pytest.approx(b["alpha"], rel=1e-11)
     assert a["beta"] == pytest.approx(b["beta"], rel=1e-11)
     np.testing.assert_allclose(wa, wb, rtol=0, atol=1e-13 * np.abs(wb).max())
+
+
+# ---- production single-sweep kernels vs the PyTorch fp64 recurrence ---------
+@pytest.mark.parametrize("M,N", [(300, 420), (257, 129)])
+@pytest.mark.parametrize("kernel", ["streaming", "resident"])
+def test_production_sweep_vs_torch_recurrence(gpu, nat, M, N, kernel, monkeypatch):
+    """S_0 + 20 sweeps of the production kernel (streaming kS, or the resident
+    kernel), convergence test off: the 7 reduced sums, α, β and the r / p
+    planes and w against torch_ref.single_sweep (reference operator,
+    divisions; the kernels use the division-free coefficient path) —
+    reference iteration: stage2-mpi/poisson_mpi_decomp.cpp:400-457."""
+    K = 20
+    monkeypatch.setenv("PE_RESIDENT", "1" if kernel == "resident" else "0")
+    prob = EllipseProblem(M, N)
+    opt = nat.SolveOptions()
+    opt.algo = 2
+    opt.check_tol = False
+    s = nat.DeviceSolver(prob.to_native(), D.block(M, N, 1, 0), None, opt)
+    assert s.resident == (kernel == "resident")
+    s.reset()
+    s.run_iterations(K, False)
+    s.synchronize()
+    st = s.state()
+    ref = torch_ref.single_sweep(prob, K)
+    par = (K - 1) & 1
+    got, want = st["fs"][par], ref.sums[K]
+    scale = max(abs(x) for x in want)
+    for n in range(7):
+        assert got[n] == pytest.approx(want[n], rel=1e-10, abs=1e-13 * scale), n
+    assert st["alpha"] == pytest.approx(ref.alpha[-1], rel=1e-12)
+    assert st["beta"] == pytest.approx(ref.beta[-1], rel=1e-12)
+    fields = {"r": s.field(0 if par == 0 else 4), "p": s.field(2 if par == 0 else 3)}
+    for name, f in fields.items():
+        want_f = getattr(ref, name)[1:M, 1:N].numpy()
+        np.testing.assert_allclose(f[2:M + 1, 2:N + 1], want_f, rtol=0, atol=1e-12 * np.abs(want_f).max(),
+                                   err_msg=name)
+    wref = ref.w[1:M, 1:N].numpy()
+    np.testing.assert_allclose(s.w(), wref, rtol=0, atol=1e-12 * np.abs(wref).max())
+
+
+def test_virtual_split_sweep_vs_torch_recurrence(gpu):
+    """2x2 virtual ranks (halo exchange, strips that cut boundary-band rows)
+    through the streaming kernel: w after 20 sweeps against the recurrence."""
+    prob = EllipseProblem(300, 420)
+    prob.max_iter = 20
+    rep = solve(prob, backend="hip-group", ranks=4, decomp="2x2", return_w=True, check_tol=False, algo="fused")
+    assert rep.iters == 20 and rep.Px * rep.Py == 4
+    wref = torch_ref.single_sweep(EllipseProblem(300, 420), 20).w[1:300, 1:420].numpy()
+    np.testing.assert_allclose(rep.w, wref, rtol=0, atol=1e-12 * np.abs(wref).max())
+
+
+@pytest.mark.parametrize("M,N,kw", [(40, 40, {}), (257, 129, {}), (800, 1200, {}),
+                                    (300, 200, dict(A1=-2.0, B1=2.0, A2=-1.0, B2=1.0, cx=0.25, cy=1.0))])
+def test_fast_coefficients_vs_assembly(gpu, nat, M, N, kw):
+    """The single-sweep kernels' division-free coefficients (cset_rc: t = l·(1/h),
+    t + (1-t)·(1/eps), reciprocal + Newton 1/D) against the reference assembly
+    (fic_reg_local, poisson_mpi_decomp.cpp:124-170).  Interior / exterior faces
+    are exact; a cut face's blend amplifies the one-rounding difference of t
+    by 1/eps, so it is held to (1/eps)·ulp(1) + 2 ulp; 1/D (a sum of faces ≥ 1
+    each, then a reciprocal) to a relative (1/eps)·ulp(1) + 4 ulp."""
+    prob = EllipseProblem(M, N, **kw)
+    a, b, di = (np.asarray(x) for x in nat.device_coefficients_fast(prob.to_native(), D.block(M, N, 1, 0)))
+    at, bt, _ = torch_ref.assemble(prob)
+    Dt = torch_ref.diag(at, bt, prob.h1, prob.h2).numpy()
+    at, bt = at.numpy(), bt.numpy()
+    assert a.shape == at.shape == (M + 1, N + 1)
+    inv_eps = 1.0 / prob.eps
+    plain_a = (at == 1.0) | (at == inv_eps)
+    plain_b = (bt == 1.0) | (bt == inv_eps)
+    assert np.array_equal(a[plain_a], at[plain_a]) and np.array_equal(b[plain_b], bt[plain_b])
+    bound = lambda ref: inv_eps * np.spacing(1.0) + 2 * np.spacing(np.abs(ref))  # noqa: E731
+    assert np.all(np.abs(a - at) <= bound(at))
+    assert np.all(np.abs(b - bt) <= bound(bt))
+    assert plain_a.sum() < a.size  # band faces exist
+    dref = 1.0 / Dt[1:M, 1:N]
+    rel = np.abs(di[1:M, 1:N] - dref) / dref
+    assert rel.max() <= (inv_eps + 4.0) * np.spacing(1.0)
