@@ -121,6 +121,10 @@ GOLDEN_ITERS = {
     (2048, 2048, "weighted"): 1730,
     (4096, 4096, "weighted"): 3226,
     (8192, 8192, "weighted"): 5889,
+    # 16384² (BASELINE.json config 5; no CPU replica run): pinned on 1x MI355X
+    # by the classic two-kernel path (reference recurrence, 2 reductions per
+    # iteration) and the single sweep, which agree — profiles/r2_pin_16384.txt
+    (16384, 16384, "weighted"): 10363,
 }
 
 # L2 error in D of the converged solution.
@@ -133,4 +137,5 @@ GOLDEN_L2 = {
     (2048, 2048): 1.67e-4,
     (4096, 4096): 2.71e-4,
     (8192, 8192): 5.88e-4,
+    (16384, 16384): 1.4227e-3,  # classic and single sweep: 1.422683e-3 (profiles/r2_pin_16384.txt)
 }

@@ -70,7 +70,7 @@ def test_fused_thin_blocks(gpu, M, N, ranks, decomp):
     np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("M,N", [(4096, 4096), (8192, 8192)])
+@pytest.mark.parametrize("M,N", [(4096, 4096), (8192, 8192), (16384, 16384)])
 def test_fused_large_golden(gpu, M, N):
     rep = solve(EllipseProblem(M, N), backend="hip", algo="fused")
     assert rep.converged and rep.iters == GOLDEN_ITERS[(M, N, "weighted")]
