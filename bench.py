@@ -168,6 +168,8 @@ def main() -> int:
             "exchange_us_measured": round(solver.exchange_us, 2),
             "item_order": "dynamic per-XCD queue" if solver.order == 3 else "static LPT layout",
             "rows_per_item": solver.ti,
+            "rows_per_item_tuning_ms": [round(x, 4) for x in solver.ti_tuning_ms],
+            "resident": bool(solver.resident),
             "chunk": solver.chunk,
             "placement": {"candidates_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
                           "chosen": solver.placement_choice, "search_s": round(solver.placement_s, 3)},

@@ -426,6 +426,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("placement_s", &DeviceSolver::placement_seconds)
       .def_property_readonly("construct_s", &DeviceSolver::construct_seconds)
       .def_property_readonly("exchange_us", &DeviceSolver::exchange_us)
+      .def_property_readonly("ti_tuning_ms", &DeviceSolver::ti_tuning_ms)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("order", [](DeviceSolver& s) { return s.params().order; })
       .def_property_readonly("xr", [](DeviceSolver& s) { return s.params().xr.peers != nullptr; },

@@ -224,29 +224,30 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const int64_t bands = std::max<int64_t>(1, wave_cap / std::max<int64_t>(1, strips));
     ti = int((nx + bands - 1) / bands);
   }
-  k.ti = ti;
   k.nstrips = int(strips);
-  k.nitems = int(strips * ((nx + ti - 1) / ti));
-  // fewest waves that keep every wave's share of the n items equal
-  auto grid_for = [&](int cap, int n) {
-    const int per = (n + cap - 1) / cap;
-    const int waves = (n + per - 1) / per;
-    return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
-  };
   int wave_cap0 = wave_cap;
   if (fused_ && !std::getenv("PE_WAVES")) {
     const int per0 = dev::resident_blocks_S(k, 0);
     if (per0 > 0) wave_cap0 = cus * per0 * dev::kWPB;
   }
-  k.nblocks = grid_for(wave_cap, k.nitems);
-  k.nblocks0 = grid_for(wave_cap0, k.nitems);
   wave_cap_ = std::min(wave_cap, wave_cap0);
+  wave_caps_[0] = wave_cap;
+  wave_caps_[1] = wave_cap0;
+  // Rows per item: fixed (PE_TI, the classic path, big dynamic sweeps), or
+  // tuned below among kTiCands for static single sweeps (the best depends
+  // on the block: 2400×3200 18 rows 76 µs vs 84 at 10; 1600×2400 and the
+  // 8-rank 8192² block 10 rows — profiles/r2_mid_tune.txt).
+  static constexpr int kTiCands[4] = {8, 10, 14, 18};
+  tune_ti_ = fused_ && ti_env == 0 && k.order == 0 && double(nx) * double(ny) >= double(1 << 20);
+  if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
+  const int ti_min = tune_ti_ ? kTiCands[0] : ti;
+  set_items(ti);
   // block partials: interior grid, then (overlap) the boundary grid after it
-  const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(k.nblocks, k.nblocks0)), 4096);
+  const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(wave_cap, wave_cap0) / dev::kWPB + 1), 4096);
   // item-sum slots: one per item, more when setup_items splits tail items
   // (static sweeps split heavy items into up to ti pieces: setup_items)
-  nslot_cap_ = fused_ ? (k.order == 0 ? ti + 1 : 2) * k.nitems + 64 : 0;
-  k.nslots = k.nitems;
+  const int64_t nitems_max = strips * ((nx + ti_min - 1) / ti_min);
+  nslot_cap_ = fused_ ? int((k.order == 0 ? ti + 1 : 2) * nitems_max + 64) : 0;
   PE_HIP_CHECK(hipMalloc(&partial_, sizeof(double) * (npart + 8 * int64_t(nslot_cap_))));
   k.partial = partial_;
   k.itemsum = fused_ ? partial_ + npart : nullptr;
@@ -261,10 +262,33 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (comm_->size() > 1) measure_exchange();
   setup_items();
   setup_resident();
-  if (static_waves_ > 0) {
-    // static list walk: the grid is the one the list was laid out for (plus
-    // the blocks the overlap keeps free for the halo stream)
-    k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
+  if (tune_ti_ && !resident_) {
+    // time S_0 + 2 + 6 local sweeps per candidate on real data (no
+    // communication: the in-sweep cross-rank sum is not set up yet) and keep
+    // the fastest; every rank tunes its own block
+    Range range("pe.tune_rows_per_item");
+    float best_ms = 0.f;
+    int best = ti;
+    for (int cand : kTiCands) {
+      set_items(cand);
+      setup_items();
+      enqueue_init();
+      dev::launch_S(*kp_, 1, stream_);
+      for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
+      PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+      for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
+      PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+      PE_HIP_CHECK(hipEventSynchronize(t1_));
+      float ms = 0.f;
+      PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+      ti_ms_.push_back(ms / 6.0f);
+      if (best_ms == 0.f || ms < best_ms) {
+        best_ms = ms;
+        best = cand;
+      }
+    }
+    set_items(best);
+    setup_items();
   }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
     const size_t nw = size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
@@ -328,6 +352,23 @@ void DeviceSolver::measure_exchange() {
   exchange_us_ = us[0];
 }
 
+// Items of `ti` rows: counts and the persistent grids sized for them.
+void DeviceSolver::set_items(int ti) {
+  KParams& k = *kp_;
+  k.ti = ti;
+  k.nitems = int(int64_t(k.nstrips) * ((blk_.nx + ti - 1) / ti));
+  // fewest waves that keep every wave's share of the n items equal
+  auto grid_for = [&](int cap, int n) {
+    const int per = (n + cap - 1) / cap;
+    const int waves = (n + per - 1) / per;
+    return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
+  };
+  k.nblocks = grid_for(wave_caps_[0], k.nitems);
+  k.nblocks0 = grid_for(wave_caps_[1], k.nitems);
+  k.nslots = k.nitems;
+  static_waves_ = 0;
+}
+
 // Halo/interior overlap (multi-rank single-sweep).  The sweep walks an item
 // list in which, per XCD shard, the boundary items (outputs sent to a
 // neighbour: first / last two owned rows and columns) come first; each bumps
@@ -371,6 +412,10 @@ void DeviceSolver::setup_items() {
   // heavy items split, below) and the overlap; orders 1 / 2 are plain
   // tuning walks.
   if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
+  if (ilist_) {  // re-laid out (rows-per-item tuning)
+    PE_HIP_CHECK(hipFree(ilist_));
+    ilist_ = nullptr;
+  }
   if (overlap_) {
     ov_reserve_ = 8;
     // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
@@ -524,6 +569,9 @@ void DeviceSolver::setup_items() {
     k.nslots = int(all.size());
     for (int x = 0; x <= 8; ++x) k.lbase[x] = ov_lbase_[x];
     for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+    // static list walk: the grid is the one the list was laid out for (plus
+    // the blocks the overlap keeps free for the halo stream)
+    k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
     if (overlap_) create_halo_stream();
     return;
   }
@@ -676,6 +724,7 @@ void DeviceSolver::setup_resident() {
 }
 
 void DeviceSolver::create_halo_stream() {
+  if (hs_) return;
   int least = 0, greatest = 0;
   PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
   PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));
@@ -700,7 +749,11 @@ void DeviceSolver::choose_placement() {
     ~Clock() { out = secs(t0, clk::now()); }
   } clock{placement_s_};
   const double pts = double(blk_.nx) * double(blk_.ny);
-  int tries = pts >= double(1 << 22) ? 8 : 1;
+  // Only large blocks: the two-speed placement was measured at 8192² (≈9 %);
+  // at 2400×3200 / 4096² the candidates differ by ≤ 3-7 % while the spacer
+  // allocations cost 0.02-6 s of construction (T_solver) depending on the
+  // allocator state (profiles/r2_ctor_probe.txt).
+  int tries = pts >= 24.0e6 ? 8 : 1;
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
   double skip_gb = 8.0;
   if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));

@@ -148,6 +148,7 @@ class DeviceSolver {
   double placement_seconds() const { return placement_s_; }      // wall time of the search
   double construct_seconds() const { return ctor_s_; }           // wall time of the constructor
   double exchange_us() const { return exchange_us_; }            // measured halo exchange (multi-rank)
+  const std::vector<float>& ti_tuning_ms() const { return ti_ms_; }  // per candidate (8, 10, 14, 18 rows)
   hipStream_t stream() const { return stream_; }
 
   // Checkpoint / resume of the full device state of this rank (raw fields,
@@ -180,6 +181,7 @@ class DeviceSolver {
   void choose_placement();
   void measure_exchange();  // sets exchange_us_ (collective)
   void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
+  void set_items(int ti);   // item counts and persistent grids for `ti` rows per item
   void enqueue_iteration(int par);
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
   void enqueue_exchange(int buf);
@@ -256,6 +258,9 @@ class DeviceSolver {
   double ctor_s_ = 0, copy_setup_s_ = 0, placement_s_ = 0;
   bool ctor_counted_ = false;
   int placement_best_ = 0;
+  bool tune_ti_ = false;          // rows per item chosen by timing candidate sweeps
+  std::vector<float> ti_ms_;      // their per-sweep times
+  int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;
   std::unique_ptr<dev::ResParams> rp_;
   int* res_rowstart_ = nullptr;
