@@ -119,6 +119,7 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
   const int wg = int(blockIdx.x);
   const int tr = wg / rp.nstrips, s = wg - tr * rp.nstrips;
   const int I0 = rp.rowstart[tr], R = rp.rowstart[tr + 1] - I0;
+  const int I0m = tr > 0 ? rp.rowstart[tr - 1] : 0;  // band tr-1's first row (ring-column imports)
   const int J0 = 1 + kFSW * s;
   const int nx = int(k.nx), ny = int(k.ny);
   const int wS = min(kFSW, ny - J0 + 1);  // owned columns of this strip
@@ -487,7 +488,7 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
         cv[u] = 0.0;
         if (rho < R + 3 && s2 >= 0 && s2 < rp.nstrips && c >= 1 && c <= ny && t >= 1 && t <= nx) {
           const int trs = t < I0 ? tr - 1 : (t >= I0 + R ? tr + 1 : tr);
-          const int idx = t - rp.rowstart[trs];
+          const int idx = t - (t < I0 ? I0m : (t >= I0 + R ? I0 + R : I0));
           cv[u] = ld_sc1(Eb + size_t(trs * rp.nstrips + s2) * kResEdge + (left ? ECOLR : ECOLL) + idx);
           cidx[u] = rho * 128 + (left ? 0 : 127);
         }
