@@ -7,9 +7,10 @@ Poisson problem (BASELINE.json: "PCG iters/sec + T_solver, 8192x8192 grid at
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
-A *step* is one full PCG iteration of the global solve on N GPUs (fused
-direction/stencil kernel, allreduce, fused update kernel, RCCL halo exchange,
-allreduce).  The timed region runs exactly K steps from the start of a fresh
+A *step* is one full PCG iteration of the global solve on N GPUs (the
+single-sweep kernel with its 7 sums summed over ranks inside the sweep over
+xGMI P2P, and the halo rows — row-slab blocks — pushed by the same sweep into
+the neighbours' receive buffers, or exchanged through RCCL otherwise).  The timed region runs exactly K steps from the start of a fresh
 solve (w⁰ = 0, as the reference) with the convergence test switched off so
 every step does full work; it is bracketed by a barrier + device synchronise
 on both sides and the max over ranks is reported.  `value` = job-wide PCG
@@ -158,12 +159,16 @@ def main() -> int:
             "unknowns": (M - 1) * (N - 1),
             "global_batch": 1,
             "seq_len": None,
-            "parallelism": f"2d-decomp {blk.Px}x{blk.Py} (RCCL)" if world > 1 else "single-gpu",
+            "parallelism": (f"2d-decomp {blk.Px}x{blk.Py} "
+                            + ("(xGMI halo push + P2P sums)" if solver.halo_push else "(RCCL halo)"))
+            if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
             "algo": "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else "classic (2 kernels, 2 allreduces / iter)",
             "decomposition": {"spec": a.decomp, "Px": blk.Px, "Py": blk.Py, "block": [blk.nx, blk.ny]},
             "transport": comm.name if comm is not None else "none",
             "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
+            "halo": ("in-sweep xGMI push (graph-captured)" if solver.halo_push else
+                     ("exchange: " + comm.name)) if world > 1 else "none",
             "overlap": bool(solver.overlap),
             "exchange_us_measured": round(solver.exchange_us, 2),
             "item_order": "dynamic per-XCD queue" if solver.order == 3 else "static LPT layout",

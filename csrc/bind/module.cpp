@@ -418,6 +418,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("overlap", &DeviceSolver::overlap)
+      .def_property_readonly("halo_push", &DeviceSolver::halo_push,
+                             "halo rows pushed by the sweep over xGMI (no exchange call; graph-capturable)")
       .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)

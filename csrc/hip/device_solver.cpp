@@ -258,8 +258,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
   build_tables(rows_hi, cols_hi);
+  setup_halo_push();
   if (fused_) choose_placement();
-  if (comm_->size() > 1) measure_exchange();
+  if (comm_->size() > 1 && !push_) measure_exchange();
   setup_items();
   setup_resident();
   if (tune_ti_ && !resident_) {
@@ -305,6 +306,21 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const char* e = std::getenv("PE_XR");
     if (!(e && std::atoi(e) == 0)) k.xr = *comm_->peer_sum();
   }
+  // The halo push goes live with the in-sweep sum (its flags are the push's
+  // delivery signal); the local sweeps above ran without either.
+  if (push_) {
+    const int64_t side = 2 * k.pitch;
+    double* lo = static_cast<double*>(hpeers_[size_t(blk_.nbr[LEFT] >= 0 ? blk_.nbr[LEFT] : blk_.rank)]);
+    double* hi = static_cast<double*>(hpeers_[size_t(blk_.nbr[RIGHT] >= 0 ? blk_.nbr[RIGHT] : blk_.rank)]);
+    for (int b = 0; b < 2; ++b) {
+      // my rows 1, 2 → the LEFT neighbour's side 1 (its rows nx'+1, nx'+2);
+      // my rows nx-1, nx → the RIGHT neighbour's side 0 (its rows -1, 0)
+      k.hpush_lo[b] = blk_.has(LEFT) ? lo + (2 * b + 1) * side : nullptr;
+      k.hpush_hi[b] = blk_.has(RIGHT) ? hi + (2 * b + 0) * side : nullptr;
+    }
+    k.hrecv = hrecv_;
+    k.push = 1;
+  }
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -316,6 +332,41 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   PE_HIP_CHECK(hipDeviceSynchronize());
   ctor_s_ = secs(t_ctor, clk::now());
+}
+
+// In-sweep halo push over xGMI (KParams::push).  Row-slab blocks (Py = 1:
+// one contiguous 2-row message per x-neighbour) whose per-iteration sums run
+// inside the sweep over the P2P transport: the sweep stores its edge rows
+// straight into the neighbours' fine-grained receive buffers, the sum's flags
+// tell the neighbours they have arrived, and a small import kernel moves them
+// into the halo rows — no exchange launch, no RCCL call, and the iteration
+// becomes graph-capturable.  Every input of the decision is global (grid,
+// process grid, environment, transport type), so every rank reaches
+// map_peer_buffers (collective) or none does.  PE_HALO=exchange opts out.
+void DeviceSolver::setup_halo_push() {
+  push_ = false;
+  if (!fused_ || comm_->size() < 2 || !comm_->peer_sum() || blk_.Py != 1) return;
+  if ((prob_.M - 1) / blk_.Px < 4) return;  // edge rows 1, 2 and nx-1, nx distinct
+  if (const char* e = std::getenv("PE_XR"); e && std::atoi(e) == 0) return;
+  if (const char* e = std::getenv("PE_HALO"); e && std::string(e) == "exchange") return;
+  const size_t bytes = sizeof(double) * 8 * size_t(kp_->pitch);  // [parity][side][2 rows]
+  void* buf = nullptr;
+  if (hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+    buf = nullptr;
+    (void)hipGetLastError();
+  } else {
+    PE_HIP_CHECK(hipMemset(buf, 0, bytes));
+    PE_HIP_CHECK(hipDeviceSynchronize());
+  }
+  // a rank without a buffer still takes part (its map fails → every rank gets
+  // an empty result and keeps the exchange)
+  hpeers_ = comm_->map_peer_buffers(buf);
+  if (hpeers_.empty()) {
+    if (buf) PE_HIP_CHECK(hipFree(buf));
+    return;
+  }
+  hrecv_ = static_cast<double*>(buf);
+  push_ = true;
 }
 
 void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
@@ -399,7 +450,7 @@ void DeviceSolver::setup_items() {
   // PE_OVERLAP=1 / 0 forces it on / off.
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = false;
-  if (fused_ && comm_->size() > 1 && nb) {
+  if (fused_ && comm_->size() > 1 && nb && !push_) {
     if (e) {
       overlap_ = std::atoi(e) != 0;
     } else {
@@ -842,6 +893,8 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(tables_);
   (void)hipFree(rowcls_);
   (void)hipFree(halo_);
+  if (push_) comm_->unmap_peer_buffers(hpeers_);
+  if (hrecv_) (void)hipFree(hrecv_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
   if (stamps_) (void)hipFree(stamps_);
@@ -918,7 +971,11 @@ std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
   return ph;
 }
 
-void DeviceSolver::enqueue_exchange(int buf) {
+void DeviceSolver::enqueue_exchange(int buf, bool after_sweep) {
+  if (push_ && after_sweep) {
+    dev::launch_halo_import(*kp_, buf, stream_);
+    return;
+  }
   for (const HaloPhase& ph : halo_phases(buf)) {
     comm_->exchange(ph.ex, stream_);
     if (ph.unpack) dev::launch_unpack(*kp_, buf, stream_);
@@ -1100,7 +1157,7 @@ hipGraphExec_t DeviceSolver::graph_for(int iters) {
 
 // (overlap: a graph may serialise the two streams' branches in any order,
 // and the halo branch waits on the sweep — always eager)
-bool DeviceSolver::graphs_usable() const { return comm_->capturable() && !overlap_ && !resident_; }
+bool DeviceSolver::graphs_usable() const { return (comm_->capturable() || push_) && !overlap_ && !resident_; }
 
 void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   // The captured graph starts at parity 0 and has an even length; iterations
@@ -1286,7 +1343,7 @@ void DeviceSolver::reset() {
     // r⁰ (and p = 0) in x[0] → halos → sweep S_0 (z₀, A z₀ and their sums,
     // no iteration counted) into x[1]; iteration 1 then reads x[1] (par 0).
     dev::launch_pack(*kp_, 0, stream_);
-    enqueue_exchange(0);
+    enqueue_exchange(0, false);
     dev::launch_S(*kp_, 1, stream_);
     enqueue_exchange(1);
     enqueue_fs_reduce(1);

@@ -285,7 +285,11 @@ __device__ __forceinline__ unsigned long long rtc() {
   return t;
 }
 
-template <int OCC, int PF, bool NT, int WM, bool STAMP = false>
+// PUSH — in-sweep halo push (KParams::push): output rows 1, 2 / nx-1, nx are
+// also stored into the x-neighbours' fine-grained receive buffers over xGMI
+// (system-scope write-through stores, drained and released before the item
+// ends, so they are delivered before this rank's cross-rank-sum flags).
+template <int OCC, int PF, bool NT, int WM, bool STAMP = false, bool PUSH = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   const unsigned long long t_entry = STAMP ? rtc() : 0ull;
@@ -504,6 +508,27 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
           sb[c0 + 1 - (ny - 1) + 2] = pa.y;
         }
       }
+    };
+    // In-sweep halo push of output row i (PUSH): rows 1, 2 → the LEFT
+    // neighbour's rows nx'+1, nx'+2, rows nx-1, nx → the RIGHT neighbour's
+    // rows -1, 0 (row tests are uniform; owned columns only — the receive
+    // buffers' halo columns stay zero, as the global boundary's are).
+    bool pushed = false;
+    auto push_row = [&](int i, const double2& rkI, const double2& pa) {
+      auto put = [&](double* base, int slot) {
+        double* d = base + int64_t(slot) * pitch + off;
+        if (o0) {
+          __hip_atomic_store(d, rkI.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(d + poff, pa.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        if (o1) {
+          __hip_atomic_store(d + 1, rkI.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(d + 1 + poff, pa.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+        pushed = true;
+      };
+      if (i <= 2 && k.hpush_lo[par] != nullptr) put(k.hpush_lo[par], i - 1);
+      if (i >= nx - 1 && k.hpush_hi[par] != nullptr) put(k.hpush_hi[par], i - (nx - 1));
     };
     // Strip chord entries → LDS, read by boundary-band rows only: staged only
     // when the item has band rows in this strip (a few % of items).
@@ -729,6 +754,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
             if constexpr (WM == 2) wd[0] = wv.x;
           }
           send_strips(i, rkI, pa);
+          if constexpr (PUSH) push_row(i, rkI, pa);
         }
         Z[b] = dd(zn0, zn1);
         S[(jj + 1) & 1] = dd(s0, s1);
@@ -736,6 +762,13 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         RIN[(jj + 1) & 1] = rQ0;
         sl = sl1;
         if (i - ib + 6 < 30) sstamp(i - ib + 6);  // after row step i: slots 4 ..
+      }
+    }
+    if constexpr (PUSH) {
+      if (pushed) {  // delivered before this wave arrives anywhere
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
     }
     if (persum) {
@@ -985,6 +1018,24 @@ __global__ void kUnpack(KParams k, int b) {
   }
 }
 
+// In-sweep halo push, receiving side: rows -1, 0 (from LEFT) and nx+1, nx+2
+// (from RIGHT) of x[b] ← the receive buffer of parity b.  The neighbours'
+// stores reached it before their cross-rank-sum flags, which this rank's
+// preceding reduction waited for; the loads are system-scope (the buffer is
+// written over xGMI, never through this GPU's caches).
+__global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
+  if (k.st->done) return;
+  const int64_t n = 2 * k.pitch;
+  double* x = k.x[b] - 1;  // row 0, column -1
+  for (int side = 0; side < 2; ++side) {
+    if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
+    const double* src = k.hrecv + (int64_t(b) * 2 + side) * n;
+    double* dst = x + (side == 0 ? int64_t(-1) : k.nx + 1) * k.pitch;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+      dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
 // Test op: the division-free coefficients the single-sweep kernels evaluate
 // (cset_rc from the row classes and chord tables) for every node of the block
 // plus its 1-wide ring, dense [(nx+2) × (ny+2)]: a(li, lj), b(li, lj), 1/D.
@@ -1028,6 +1079,7 @@ static int s_cfg() {
 template <int WM, class F>
 static auto with_kS(const KParams& k, F&& f) {
   if (k.stamps) return f(kS<2, 4, true, WM, true>);
+  if (k.push) return f(kS<2, 4, true, WM, false, true>);
   switch (s_cfg()) {
     case 1: return f(kS<2, 4, false, WM>);
     default: return f(kS<2, 4, true, WM>);
@@ -1094,6 +1146,13 @@ int resident_blocks_S(const KParams& k, int wm) {
 void launch_pack(const KParams& k, int b, hipStream_t s) {
   if (!k.has[DOWN] && !k.has[UP]) return;
   hipLaunchKernelGGL(kPack, dim3(unsigned((k.nx + 255) / 256)), dim3(256), 0, s, k, b);
+}
+
+void launch_halo_import(const KParams& k, int b, hipStream_t s) {
+  if (!k.push || (!k.has[LEFT] && !k.has[RIGHT])) return;
+  const int64_t n = 2 * k.pitch;
+  const unsigned g = unsigned(std::min<int64_t>(64, (n + 255) / 256));
+  hipLaunchKernelGGL(kHaloImport, dim3(g), dim3(256), 0, s, k, b);
 }
 
 void launch_unpack(const KParams& k, int b, hipStream_t s) {

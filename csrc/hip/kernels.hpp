@@ -127,6 +127,19 @@ struct KParams {
   // reduction block sums the 7 sums over ranks itself (xr.peers == null: the
   // host enqueues the comm's allreduce instead).
   PeerSum xr;
+  // In-sweep halo push over xGMI (row-slab blocks, P2P transport, k.xr set):
+  // the sweep that writes buffer b also stores its owned rows 1, 2 into the
+  // LEFT neighbour's receive buffer (hpush_lo[b]) and rows nx-1, nx into the
+  // RIGHT neighbour's (hpush_hi[b]) with system-scope write-through stores;
+  // the in-sweep cross-rank sum's flags then double as "halo delivered", and
+  // kHaloImport copies this rank's receive buffer hrecv into the halo rows of
+  // x[b] before the next sweep.  hrecv = [parity b][side: 0 rows -1,0 from
+  // LEFT, 1 rows nx+1,nx+2 from RIGHT][2 × pitch], laid out like x rows from
+  // column -1.  push = 0: the halo travels through the comm's exchange.
+  double* hpush_lo[2];
+  double* hpush_hi[2];
+  const double* hrecv;
+  int push;
 };
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
@@ -186,6 +199,10 @@ void launch_pack(const KParams& k, int b, hipStream_t s);
 // Add a pending deferred w term (no-op when none is pending).
 void launch_wflush(const KParams& k, hipStream_t s);
 void launch_unpack(const KParams& k, int b, hipStream_t s);
+// In-sweep halo push: copy the receive buffer's rows of parity b (filled by
+// the neighbours' sweeps, delivered once the sweep's cross-rank sum has
+// completed) into x[b]'s halo rows -1, 0 / nx+1, nx+2 (no-op once done).
+void launch_halo_import(const KParams& k, int b, hipStream_t s);
 // Overlap: spin until st->sig reaches `target` (every boundary item of the
 // running sweep is in L2) or the solve is done, then write every XCD's L2
 // back.  Put on the halo stream ahead of the exchange.

@@ -86,22 +86,35 @@ class P2PAllreduceComm final : public DeviceComm {
   void abort() override { base_->abort(); }
   const dev::PeerSum* peer_sum() const override { return &ps_; }
 
- private:
-  // Map every peer's receive buffer; false on any local failure (no abort:
-  // the ranks must still reach the agreement collective).
-  bool setup(int P, int me, hipStream_t s) {
-    const size_t bytes = sizeof(double) * 2 * size_t(P) * dev::kP2PSlot;
-    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocFinegrained) != hipSuccess) {
-      mine_ = nullptr;
-      (void)hipGetLastError();
+  std::vector<void*> map_peer_buffers(void* mine) override {
+    const int P = size(), me = rank();
+    hipStream_t s = nullptr;
+    PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    std::vector<void*> peers;
+    bool ok = open_peers(mine, P, me, s, peers);
+    ok = agree(ok, s);
+    PE_HIP_CHECK(hipStreamDestroy(s));
+    if (!ok) {
+      unmap_peer_buffers(peers);
+      return {};
     }
-    bool ok = mine_ != nullptr;
+    return peers;
+  }
+  void unmap_peer_buffers(const std::vector<void*>& peers) override {
+    for (size_t r = 0; r < peers.size(); ++r)
+      if (int(r) != rank() && peers[r]) (void)hipIpcCloseMemHandle(peers[r]);
+  }
+
+ private:
+  // All-gather the IPC handles of every rank's `mine` through the base
+  // transport (byte b of rank r's handle at table[r*HB + b]: a max-allreduce
+  // of a zero table; every rank takes part even after a local failure) and
+  // open the peers'.  peers[r] = rank r's buffer in this process (peers[me] =
+  // mine; null where not opened).  False on any local failure.
+  bool open_peers(void* mine, int P, int me, hipStream_t s, std::vector<void*>& peers) {
     hipIpcMemHandle_t h{};
-    if (ok) ok = hipMemset(mine_, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess &&
-                 hipIpcGetMemHandle(&h, mine_) == hipSuccess;
-    // all-gather the handles through the base transport: byte b of rank r's
-    // handle at table[r*HB + b] (a max-allreduce of a zero table; every rank
-    // takes part even after a local failure)
+    bool ok = mine != nullptr && hipIpcGetMemHandle(&h, mine) == hipSuccess;
+    if (!ok) (void)hipGetLastError();
     constexpr int HB = int(sizeof(hipIpcMemHandle_t));
     std::vector<double> tbl(size_t(P) * HB, 0.0);
     const unsigned char* hb = reinterpret_cast<const unsigned char*>(&h);
@@ -113,10 +126,10 @@ class P2PAllreduceComm final : public DeviceComm {
     PE_HIP_CHECK(hipStreamSynchronize(s));
     PE_HIP_CHECK(hipMemcpy(tbl.data(), dt, sizeof(double) * tbl.size(), hipMemcpyDeviceToHost));
     PE_HIP_CHECK(hipFree(dt));
-    std::vector<double*> peers(size_t(P), nullptr);
+    peers.assign(size_t(P), nullptr);
     for (int r = 0; r < P && ok; ++r) {
       if (r == me) {
-        peers[r] = mine_;
+        peers[r] = mine;
         continue;
       }
       hipIpcMemHandle_t hr;
@@ -129,8 +142,27 @@ class P2PAllreduceComm final : public DeviceComm {
         ok = false;
         break;
       }
-      peers[r] = static_cast<double*>(p);
-      opened_.push_back(p);
+      peers[r] = p;
+    }
+    return ok;
+  }
+
+  // Map every peer's receive buffer; false on any local failure (no abort:
+  // the ranks must still reach the agreement collective).
+  bool setup(int P, int me, hipStream_t s) {
+    const size_t bytes = sizeof(double) * 2 * size_t(P) * dev::kP2PSlot;
+    if (hipExtMallocWithFlags(reinterpret_cast<void**>(&mine_), bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+      mine_ = nullptr;
+      (void)hipGetLastError();
+    }
+    bool ok = mine_ != nullptr;
+    if (ok) ok = hipMemset(mine_, 0, bytes) == hipSuccess && hipDeviceSynchronize() == hipSuccess;
+    std::vector<void*> opened;
+    ok = open_peers(ok ? mine_ : nullptr, P, me, s, opened);
+    std::vector<double*> peers(size_t(P), nullptr);
+    for (int r = 0; r < P; ++r) {
+      peers[r] = static_cast<double*>(opened.empty() ? nullptr : opened[r]);
+      if (r != me && peers[r]) opened_.push_back(peers[r]);
     }
     PE_HIP_CHECK(hipMalloc(&peers_dev_, sizeof(double*) * P));
     PE_HIP_CHECK(hipMemcpy(peers_dev_, peers.data(), sizeof(double*) * P, hipMemcpyHostToDevice));

@@ -52,6 +52,16 @@ class DeviceComm {
   // One-shot P2P sum tables (P2P transport only): the single-sweep solver
   // then sums its per-iteration scalars over ranks inside the sweep.
   virtual const dev::PeerSum* peer_sum() const { return nullptr; }
+  // Collective (every rank calls it, in the same order): map every rank's
+  // `mine` — a fine-grained device buffer of that process — into this one.
+  // result[r] = rank r's buffer (result[rank()] = mine); empty on EVERY rank
+  // when any rank cannot map (no peer-mapping transport, or a failure).
+  virtual std::vector<void*> map_peer_buffers(void* mine) {
+    (void)mine;
+    return {};
+  }
+  // Release a mapping made by map_peer_buffers (this process's side only).
+  virtual void unmap_peer_buffers(const std::vector<void*>& peers) { (void)peers; }
 };
 
 class SelfDeviceComm final : public DeviceComm {
@@ -142,6 +152,9 @@ class DeviceSolver {
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
   bool resident() const { return resident_; }
   bool overlap() const { return overlap_; }
+  // Halo rows pushed by the sweep itself over xGMI (row slabs + in-sweep P2P
+  // sums): no exchange call in the iteration, which is then graph-capturable.
+  bool halo_push() const { return push_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   int placement_choice() const { return placement_best_; }       // index into placement_ms()
@@ -184,7 +197,10 @@ class DeviceSolver {
   void set_items(int ti);   // item counts and persistent grids for `ti` rows per item
   void enqueue_iteration(int par);
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
-  void enqueue_exchange(int buf);
+  // after_sweep: the halo of `buf` was produced by a sweep (with the halo
+  // push: import it); false for the initial state (the comm's exchange).
+  void enqueue_exchange(int buf, bool after_sweep = true);
+  void setup_halo_push();  // collective: decides push_ identically on every rank
   void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
   void enqueue_chunk(int iters, int sample_iters = 0);
   // Sampled phase timing (Timers): hipEvent pairs around the phases of the
@@ -266,6 +282,9 @@ class DeviceSolver {
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials
   unsigned* res_ctr_ = nullptr;
+  bool push_ = false;               // in-sweep halo push (KParams::push)
+  double* hrecv_ = nullptr;         // its fine-grained receive buffer [2][2][2 × pitch]
+  std::vector<void*> hpeers_;       // every rank's receive buffer mapped here (comm_->map_peer_buffers)
   double exchange_us_ = 0;  // measured halo exchange (max over ranks), multi-rank only  // the first solve() carries the construction time
 };
 

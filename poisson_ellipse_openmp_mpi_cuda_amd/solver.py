@@ -57,6 +57,7 @@ class SolveReport:
     history: Optional[list] = None  # ‖Δw‖ per iteration (keep_history=True)
     comm: str = ""  # device transport of a multi-rank HIP run (e.g. "rccl", "p2p-allreduce+rccl")
     xr: bool = False  # the sweep sums its scalars over ranks itself (P2P transport, no allreduce launch)
+    halo_push: bool = False  # the sweep pushes its edge rows to the neighbours over xGMI (no exchange call)
 
     @property
     def iters_per_s(self) -> float:
@@ -189,4 +190,5 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     rep = _report("hip", prob, res, world, 1, init, w, rank)
     rep.comm = comm.name if comm is not None else "self"
     rep.xr = bool(solver.xr)
+    rep.halo_push = bool(solver.halo_push)
     return rep

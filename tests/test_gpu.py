@@ -295,7 +295,8 @@ def test_two_process_device_path_host_staged(gpu):
 @pytest.mark.parametrize("nproc,decomp,overlap,allreduce", [(4, "aspect", "1", "rccl"), (3, "aspect", "1", "rccl"),
                                                         (4, "aspect", "0", "rccl"), (4, "aspect", "1", "p2p"),
                                                         (2, "aspect", "0", "p2p"), (4, "aspect", "1", "p2p-kernel"),
-                                                        (3, "rows", "0", "p2p")])
+                                                        (3, "rows", "0", "p2p"), (4, "rows", "0", "p2p"),
+                                                        (3, "rows", "0", "p2p-exchange")])
 def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
     rows through the x phase of the single-sweep halo) — and 3×1 — match the
@@ -304,11 +305,14 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     host-staged transport, through the P2P transport (IPC-mapped buffers of
     the other processes) summed inside the sweep's final reduction block
     ("p2p"), or through the standalone one-shot P2P kernel ("p2p-kernel",
-    PE_XR=0)."""
+    PE_XR=0).  Row slabs with the in-sweep sums push their halo rows from the
+    sweep into the neighbours' receive buffers (no exchange call);
+    "p2p-exchange" (PE_HALO=exchange) keeps the exchange."""
     from conftest import free_port
 
     env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce.split("-")[0],
-               PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1")
+               PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1",
+               PE_HALO="exchange" if allreduce == "p2p-exchange" else "push")
     outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}_{allreduce}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -319,11 +323,39 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
     assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
-    assert d["xr"] == (allreduce == "p2p")
+    assert d["xr"] == (allreduce in ("p2p", "p2p-exchange"))
+    assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p")
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
     np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_halo_push_graphs(gpu, nproc):
+    """bench.py on row slabs over the P2P transport (processes sharing the
+    one GPU, host-staged base transport for set-up only): the sweep pushes its
+    edge rows into the neighbours' IPC-mapped receive buffers, the in-sweep
+    sum's flags deliver them, and the iterations run as captured hipGraphs —
+    the timed steps are valid and the full solve converges in the
+    single-GPU iteration count."""
+    from conftest import free_port
+
+    M = N = 1024
+    one = solve(EllipseProblem(M, N), backend="hip")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--steps", "40", "--warmup", "4", "--grid", str(M), str(N), "--decomp", "rows"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    c = d["config"]
+    assert c["decomposition"]["Px"] == nproc and c["decomposition"]["Py"] == 1
+    assert c["halo"] == "in-sweep xGMI push (graph-captured)", c
+    assert c["allreduce"] == "in-sweep P2P over xGMI"
+    assert d["valid"] and d["converged"] and abs(d["iters_converged"] - one.iters) <= 1
+    assert d["l2_err"] == pytest.approx(one.l2_err, rel=1e-6)
 
 
 @pytest.mark.parametrize("algo", ["fused", "classic"])

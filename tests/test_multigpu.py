@@ -57,17 +57,21 @@ def single():
     return solve(EllipseProblem(*GRID), backend="hip", return_w=True)
 
 
-@pytest.mark.parametrize("nproc,decomp,allreduce,overlap", [
-    (2, "device", "p2p", "1"), (2, "2x1", "rccl", "0"), (2, "1x2", "p2p", "1"),
-    (4, "2x2", "p2p", "1"), (4, "device", "rccl", "1"), (4, "2x2", "rccl", "0"),
-    (8, "device", "p2p", "1"), (8, "device", "p2p", "0"), (8, "4x2", "p2p", "1"), (8, "4x2", "rccl", "0"),
+@pytest.mark.parametrize("nproc,decomp,allreduce,overlap,halo", [
+    (2, "device", "p2p", "1", "push"), (2, "2x1", "rccl", "0", "push"), (2, "1x2", "p2p", "1", "push"),
+    (4, "2x2", "p2p", "1", "push"), (4, "device", "rccl", "1", "push"), (4, "2x2", "rccl", "0", "push"),
+    (8, "device", "p2p", "1", "push"), (8, "device", "p2p", "0", "push"), (8, "4x2", "p2p", "1", "push"),
+    (8, "4x2", "rccl", "0", "push"),
+    # row slabs with the in-sweep P2P sums: halo rows pushed by the sweep over xGMI (or exchanged: PE_HALO)
+    (2, "rows", "p2p", "0", "push"), (4, "rows", "p2p", "0", "push"), (8, "rows", "p2p", "0", "push"),
+    (8, "rows", "p2p", "0", "exchange"),
 ])
-def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, overlap, tmp_path):
+def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, overlap, halo, tmp_path):
     _need(nproc)
     from conftest import free_port
 
     env = dict(os.environ, PE_ALLREDUCE=allreduce, PE_OVERLAP=overlap, PE_P2P_TIMEOUT_S="30",
-               PE_WATCHDOG_S="60")
+               PE_WATCHDOG_S="60", PE_HALO=halo)
     env.pop("PE_COMM", None)
     outp = str(tmp_path / "w.npy")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -79,6 +83,7 @@ def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, ove
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
     assert d["comm"].endswith("rccl")
     assert d["comm"].startswith("p2p-allreduce") == (allreduce == "p2p")
+    assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p" and halo == "push")
     assert abs(d["iters"] - single.iters) <= 1
     np.testing.assert_allclose(np.load(outp), single.w, rtol=0, atol=1e-9)
 
@@ -95,7 +100,7 @@ def test_pe_launch_rccl(gpu):
     assert d["iters"] == 989 and d["ranks"] == 2 and d["converged"]
 
 
-@pytest.mark.parametrize("nproc", [2, 8])
+@pytest.mark.parametrize("nproc", [2, 4, 8])
 def test_bench_multi_gpu_contract(gpu, nproc):
     """bench.py under torchrun (the driver's scaling run, shortened): one JSON
     line, valid fixed-work steps, decomposition and transport reported."""
@@ -115,3 +120,6 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     c = d["config"]
     assert c["decomposition"]["Px"] * c["decomposition"]["Py"] == nproc
     assert "rccl" in c["transport"]
+    # 2047 rows: slabs while every rank keeps >= 512 rows (2 and 4 GPUs) → the
+    # halo is pushed by the sweep and the iterations run as captured graphs
+    assert c["halo"].startswith("in-sweep xGMI push") == (c["decomposition"]["Py"] == 1)
