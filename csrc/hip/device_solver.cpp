@@ -513,10 +513,13 @@ void DeviceSolver::setup_items() {
     const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
-  auto is_boundary = [&](int64_t ib, int64_t ie, int s) {  // outputs a neighbour needs (overlap)
+  // outputs a neighbour needs: first in the layout under the overlap (they
+  // feed the exchange) and under the halo push (their xGMI stores then
+  // overlap the rest of the sweep instead of ending it)
+  auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
     const int64_t J = -1 + int64_t(s) * dev::kFSW;
     const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
-    return overlap_ && !(ov_debug_ & 4) &&
+    return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
            ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
             (blk_.has(UP) && jhi >= blk_.ny - 1));
   };
