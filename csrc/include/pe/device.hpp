@@ -192,6 +192,7 @@ class DeviceSolver {
   void setup_items();  // item lists: static LPT layout or dynamic per-XCD shards (+ halo/interior overlap)
   void create_halo_stream();
   void choose_placement();
+  void carve_placement();  // PE_PLACEMENT=carve experiment (relative offsets within one allocation)
   void measure_exchange();  // sets exchange_us_ (collective)
   void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
   void set_items(int ti);   // item counts and persistent grids for `ti` rows per item
