@@ -283,6 +283,7 @@ class DeviceSolver {
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials
   unsigned* res_ctr_ = nullptr;
+  int alloc_mode_ = 0;              // field allocation: 0 hipMalloc, 2 shuffled physical chunks (large blocks)
   bool push_ = false;               // in-sweep halo push (KParams::push)
   double* hrecv_ = nullptr;         // its fine-grained receive buffer [2][2][2 × pitch]
   std::vector<void*> hpeers_;       // every rank's receive buffer mapped here (comm_->map_peer_buffers)
