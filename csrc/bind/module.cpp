@@ -490,8 +490,10 @@ PYBIND11_MODULE(_native, m) {
     double *dp = nullptr, *dA = nullptr;
     PE_HIP_CHECK(hipMalloc(&dp, bytes));
     PE_HIP_CHECK(hipMalloc(&dA, bytes));
-    PE_HIP_CHECK(hipMemcpy(dp, p.data(), bytes, hipMemcpyHostToDevice));
-    PE_HIP_CHECK(hipMemset(dA, 0, bytes));
+    // everything on the solver's (non-blocking) stream: a null-stream memset
+    // is not ordered with it
+    PE_HIP_CHECK(hipMemcpyAsync(dp, p.data(), bytes, hipMemcpyHostToDevice, s.stream()));
+    PE_HIP_CHECK(hipMemsetAsync(dA, 0, bytes, s.stream()));
     dev::launch_apply_A(s.params(), dp, dA, s.stream());
     std::vector<double> out(blk.rows * blk.pitch);
     PE_HIP_CHECK(hipStreamSynchronize(s.stream()));
@@ -507,7 +509,7 @@ PYBIND11_MODULE(_native, m) {
     const size_t n = size_t(blk.rows * blk.pitch), bytes = sizeof(double) * n;
     double* d = nullptr;
     PE_HIP_CHECK(hipMalloc(&d, 3 * bytes));
-    PE_HIP_CHECK(hipMemset(d, 0, 3 * bytes));
+    PE_HIP_CHECK(hipMemsetAsync(d, 0, 3 * bytes, s.stream()));  // ordered with the kernel (non-blocking stream)
     dev::launch_coef(s.params(), d, d + n, d + 2 * n, s.stream());
     PE_HIP_CHECK(hipStreamSynchronize(s.stream()));
     std::vector<double> a(n), b(n), D(n);

@@ -156,6 +156,16 @@ static bool fused_possible(const Problem& P, const Block& b) {
 DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* comm, const SolveOptions& opt)
     : prob_(prob), blk_(blk), comm_(comm), opt_(opt), kp_(std::make_unique<KParams>()) {
   const auto t_ctor = clk::now();
+  // PE_CTOR_TRACE=1: wall time of each construction phase → stderr
+  const bool ctor_trace = std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) == 1;
+  auto t_mark = t_ctor;
+  auto mark = [&](const char* phase) {
+    if (!ctor_trace) return;
+    PE_HIP_CHECK(hipDeviceSynchronize());
+    const auto now = clk::now();
+    std::fprintf(stderr, "[pe] ctor %-14s %8.3f ms\n", phase, 1e3 * secs(t_mark, now));
+    t_mark = now;
+  };
   if (!comm_) {
     self_ = std::make_unique<SelfDeviceComm>();
     comm_ = self_.get();
@@ -165,7 +175,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     throw std::invalid_argument("single-sweep algorithm needs variant 0 and >= 2 rows/columns per split block");
   fused_ = opt_.algo == 2 || (opt_.algo == 0 && can_fuse);
 
+  mark("start");
   PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  mark("stream");
   KParams& k = *kp_;
   std::memset(&k, 0, sizeof(KParams));
   const int64_t nx = blk_.nx, ny = blk_.ny;
@@ -196,6 +208,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     fields_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_, alloc_mode_));
     xalt_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_, alloc_mode_));
     walt_ = static_cast<double*>(field_alloc(sizeof(double) * wsize_, alloc_mode_));
+    mark("field allocs");
     set_fused_fields(fields_, xalt_, walt_);
     hsize_ = std::max<int64_t>(1, nx) * 4;
     rows_hi = nx + 3;
@@ -212,6 +225,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     k.p[1] = fields_ + 3 * A + blk_.base;
     hsize_ = std::max<int64_t>(1, nx);
   }
+  mark("fields");
   const int64_t ntab = (rows_hi + 2) * 4 + (cols_hi + 2) * 4;
   PE_HIP_CHECK(hipMalloc(&tables_, sizeof(double) * ntab));
   PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * (rows_hi + 2) * 4));
@@ -353,12 +367,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.D_out = (k.inv_eps + k.inv_eps) / k.h1sq + (k.inv_eps + k.inv_eps) / k.h2sq;
   k.dinv_in = 1.0 / ((1.0 + 1.0) * k.ih1sq + (1.0 + 1.0) * k.ih2sq);
   k.dinv_out = 1.0 / ((k.inv_eps + k.inv_eps) * k.ih1sq + (k.inv_eps + k.inv_eps) * k.ih2sq);
+  mark("buffers");
   build_tables(rows_hi, cols_hi);
+  mark("tables");
   setup_halo_push();
   if (fused_) choose_placement();
+  mark("placement");
   if (comm_->size() > 1 && !push_) measure_exchange();
   setup_items();
+  mark("items");
   setup_resident();
+  mark("resident");
   if (tune_ti_ && !resident_) {
     // time S_0 + 2 + 6 local sweeps per candidate on real data (no
     // communication: the in-sweep cross-rank sum is not set up yet) and keep
@@ -426,6 +445,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   c += c & 1;
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
+  mark("tuning+rest");
   PE_HIP_CHECK(hipDeviceSynchronize());
   ctor_s_ = secs(t_ctor, clk::now());
 }
@@ -711,7 +731,7 @@ void DeviceSolver::setup_items() {
     for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
     PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
     const auto tc = clk::now();
-    PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+    upload(ilist_, all.data(), sizeof(int2) * all.size());
     copy_setup_s_ += secs(tc, clk::now());
     k.ilist = ilist_;
     k.lnsh = 1;
@@ -784,7 +804,7 @@ void DeviceSolver::setup_items() {
   if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
   PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
   const auto tc = clk::now();
-  PE_HIP_CHECK(hipMemcpy(ilist_, all.data(), sizeof(int2) * all.size(), hipMemcpyHostToDevice));
+  upload(ilist_, all.data(), sizeof(int2) * all.size());
   copy_setup_s_ += secs(tc, clk::now());
   // Every dynamic sweep walks the list (the plain one counts no boundary
   // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).
@@ -855,7 +875,7 @@ void DeviceSolver::setup_resident() {
   r.timeout_ticks = 200000000LL;  // 2 s per barrier wait
   if (const char* t = std::getenv("PE_RES_TIMEOUT_S")) r.timeout_ticks = (long long)(std::atof(t) * 1e8);
   PE_HIP_CHECK(hipMalloc(&res_rowstart_, sizeof(int) * rs.size()));
-  PE_HIP_CHECK(hipMemcpy(res_rowstart_, rs.data(), sizeof(int) * rs.size(), hipMemcpyHostToDevice));
+  upload(res_rowstart_, rs.data(), sizeof(int) * rs.size());
   const size_t nedge = size_t(2) * size_t(nwg) * dev::kResEdge, npart = size_t(2) * size_t(nwg) * 8;
   PE_HIP_CHECK(hipMalloc(&res_buf_, sizeof(double) * (nedge + npart)));
   PE_HIP_CHECK(hipMemset(res_buf_, 0, sizeof(double) * (nedge + npart)));
@@ -1046,6 +1066,7 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(halo_);
   if (push_) comm_->unmap_peer_buffers(hpeers_);
   if (hrecv_) (void)hipFree(hrecv_);
+  if (stage_) (void)hipHostFree(stage_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
   if (stamps_) (void)hipFree(stamps_);
@@ -1075,17 +1096,33 @@ std::vector<unsigned long long> DeviceSolver::stamps() {
   return v;
 }
 
+// Host → device set-up data through a pinned staging buffer and a copy
+// kernel (launch_copy_words: no hipMemcpy in T_solver); synchronous.
+void DeviceSolver::upload(void* dst, const void* src, size_t bytes) {
+  if (bytes == 0) return;
+  if (bytes % 4) throw std::logic_error("upload: size must be a multiple of 4 bytes");
+  if (bytes > stage_bytes_) {
+    if (stage_) PE_HIP_CHECK(hipHostFree(stage_));
+    stage_bytes_ = std::max(bytes, size_t(1) << 20);
+    PE_HIP_CHECK(hipHostMalloc(&stage_, stage_bytes_, hipHostMallocDefault));
+  }
+  std::memcpy(stage_, src, bytes);
+  dev::launch_copy_words(dst, stage_, bytes, false, stream_);
+  PE_HIP_CHECK(hipGetLastError());
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+}
+
 void DeviceSolver::build_tables(int64_t rows_hi, int64_t cols_hi) {
   const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi);
   const auto t0 = clk::now();
-  PE_HIP_CHECK(hipMemcpy(tables_, t.data(), sizeof(double) * t.size(), hipMemcpyHostToDevice));
+  upload(tables_, t.data(), sizeof(double) * t.size());
   copy_setup_s_ += secs(t0, clk::now());
   const double* col = t.data();
   const double* row = t.data() + (rows_hi + 2) * 4;
   rowcls_host_ = row_classes(col, row, rows_hi, cols_hi);
   const std::vector<int>& rc = rowcls_host_;
   const auto t1 = clk::now();
-  PE_HIP_CHECK(hipMemcpy(rowcls_, rc.data(), sizeof(int) * rc.size(), hipMemcpyHostToDevice));
+  upload(rowcls_, rc.data(), sizeof(int) * rc.size());
   copy_setup_s_ += secs(t1, clk::now());
 }
 
@@ -1456,7 +1493,7 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
   load(halo_, size_t(h.halo_bytes));
   std::fclose(f);
   par_ = h.par;
-  PE_HIP_CHECK(hipMemset(&st_->sig, 0, sizeof(st_->sig)));  // overlap targets restart
+  PE_HIP_CHECK(hipMemsetAsync(&st_->sig, 0, sizeof(st_->sig), stream_));  // overlap targets restart
   ov_epoch_ = 0;
 }
 
@@ -1592,7 +1629,7 @@ SolveResult DeviceSolver::solve() {
       sampling_ = sample;
       sample_iter_ = enq - 1;
       mark_begin(kPhCopy, stream_);
-      PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+      dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
       mark_end(stream_);
       sampling_ = false;
       PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));

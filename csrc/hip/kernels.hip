@@ -574,6 +574,25 @@ void launch_G(const KParams& k, int par, int variant, hipStream_t s) {
   else hipLaunchKernelGGL(kG<false>, dim3(k.nblocks), dim3(TJ), 0, s, k, par);
 }
 
+// Word copy by a kernel (host-mapped pinned memory on either side): the
+// solver's set-up uploads and per-chunk state reads, so that no hipMemcpy
+// runs in T_solver — a fresh process's first hipMemcpy costs 17-170 ms of
+// runtime initialisation (profiles/r2_ctor.txt), a kernel 0.5 ms.
+__global__ __launch_bounds__(256) void kCopyWords(const unsigned* __restrict__ src, unsigned* __restrict__ dst,
+                                                  int64_t n, int to_host) {
+  for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+    dst[i] = src[i];
+  if (to_host) __threadfence_system();
+}
+
+void launch_copy_words(void* dst, const void* src, size_t bytes, bool to_host, hipStream_t s) {
+  const int64_t n = int64_t(bytes / 4);
+  if (n == 0) return;
+  const unsigned g = unsigned(std::min<int64_t>(1024, (n + 255) / 256));
+  hipLaunchKernelGGL(kCopyWords, dim3(g), dim3(256), 0, s, static_cast<const unsigned*>(src),
+                     static_cast<unsigned*>(dst), n, to_host ? 1 : 0);
+}
+
 void launch_error(const KParams& k, hipStream_t s) {
   hipLaunchKernelGGL(kError, dim3(flat_blocks(k)), dim3(TJ), 0, s, k);
 }

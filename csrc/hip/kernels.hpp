@@ -188,6 +188,9 @@ void launch_init(const KParams& k, int init_random, unsigned long long seed, dou
 void launch_F(const KParams& k, int par, int variant, hipStream_t s);
 void launch_G(const KParams& k, int par, int variant, hipStream_t s);
 void launch_error(const KParams& k, hipStream_t s);
+// 4-byte-word copy by a kernel (bytes % 4 == 0); either side may be pinned
+// host memory (to_host: system-scope fence after the stores).
+void launch_copy_words(void* dst, const void* src, size_t bytes, bool to_host, hipStream_t s);
 // Single-sweep PCG (fused.hip): one kernel + one 7-scalar reduction per iteration.
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red = true);  // with_red: + launch_red (dynamic order)
 // Deterministic reduction of per-item sums + state update (dynamic / listed sweeps).

@@ -168,6 +168,7 @@ class P2PAllreduceComm final : public DeviceComm {
     PE_HIP_CHECK(hipMemcpy(peers_dev_, peers.data(), sizeof(double*) * P, hipMemcpyHostToDevice));
     PE_HIP_CHECK(hipMalloc(&seq_dev_, sizeof(unsigned long long)));
     PE_HIP_CHECK(hipMemset(seq_dev_, 0, sizeof(unsigned long long)));
+    PE_HIP_CHECK(hipDeviceSynchronize());  // before any stream uses the counter (non-blocking streams)
     ps_.peers = peers_dev_;
     ps_.seq = seq_dev_;
     ps_.me = me;

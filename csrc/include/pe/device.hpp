@@ -188,6 +188,7 @@ class DeviceSolver {
 
  private:
   void build_tables(int64_t rows_hi, int64_t cols_hi);
+  void upload(void* dst, const void* src, size_t bytes);  // set-up data via pinned staging + copy kernel
   void set_fused_fields(double* x0, double* x1, double* w);
   void setup_items();  // item lists: static LPT layout or dynamic per-XCD shards (+ halo/interior overlap)
   void create_halo_stream();
@@ -283,6 +284,8 @@ class DeviceSolver {
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials
   unsigned* res_ctr_ = nullptr;
+  void* stage_ = nullptr;           // pinned staging buffer of upload()
+  size_t stage_bytes_ = 0;
   int alloc_mode_ = 0;              // field allocation: 0 hipMalloc, 2 shuffled physical chunks (large blocks)
   bool push_ = false;               // in-sweep halo push (KParams::push)
   double* hrecv_ = nullptr;         // its fine-grained receive buffer [2][2][2 × pitch]
