@@ -421,6 +421,25 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const char* e = std::getenv("PE_XR");
     if (!(e && std::atoi(e) == 0)) k.xr = *comm_->peer_sum();
   }
+  // In-kernel item-sum fold for dynamic sweeps, opt-in (PE_FOLD=1): it saves
+  // the reduction kernel (≈10 µs + a launch gap per iteration at 8192²) but
+  // its per-item publication (drained write-through stores + a returning
+  // counter add) stalls every wave at every item boundary: 1762 / 1734 it/s
+  // vs 1796 / 1752 with kRed, same boxes (profiles/r2_fold.txt).  Counters
+  // are zeroed by enqueue_init.
+  if (fused_ && k.order == 3 && std::getenv("PE_FOLD") && std::atoi(std::getenv("PE_FOLD")) == 1) {
+    const int ng = (nslot_cap_ + dev::kFoldGroup - 1) / dev::kFoldGroup;
+    // [shard exit counters, one 64-B line each, + the shards-done line][group
+    // counters] → 64-B aligned [group sums, 8 doubles each]
+    fold_bytes_ = ((sizeof(unsigned) * (16 * 9 + size_t(ng)) + 63) / 64) * 64;
+    PE_HIP_CHECK(hipMalloc(&fold_buf_, fold_bytes_ + sizeof(double) * 8 * size_t(ng)));
+    PE_HIP_CHECK(hipMemset(fold_buf_, 0, fold_bytes_));
+    PE_HIP_CHECK(hipDeviceSynchronize());
+    k.xcnt = static_cast<unsigned*>(fold_buf_);
+    k.gcnt = k.xcnt + 16 * 9;
+    k.gsum = reinterpret_cast<double*>(static_cast<char*>(fold_buf_) + fold_bytes_);
+    k.fold = 1;
+  }
   // The halo push goes live with the in-sweep sum (its flags are the push's
   // delivery signal); the local sweeps above ran without either.
   if (push_) {
@@ -1067,6 +1086,7 @@ DeviceSolver::~DeviceSolver() {
   if (push_) comm_->unmap_peer_buffers(hpeers_);
   if (hrecv_) (void)hipFree(hrecv_);
   if (stage_) (void)hipHostFree(stage_);
+  if (fold_buf_) (void)hipFree(fold_buf_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
   if (stamps_) (void)hipFree(stamps_);
@@ -1186,6 +1206,7 @@ void DeviceSolver::enqueue_init() {
   }
   PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * hsize_ * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
+  if (fold_buf_) PE_HIP_CHECK(hipMemsetAsync(fold_buf_, 0, fold_bytes_, stream_));
   ov_epoch_ = 0;
   dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
   PE_HIP_CHECK(hipGetLastError());
@@ -1257,7 +1278,7 @@ void DeviceSolver::enqueue_iteration(int par) {
     mark_begin(kPhSweep, stream_);
     dev::launch_S(ko, par, stream_, false);  // boundary items first in every shard
     mark_end(stream_);
-    if (ko.order == 3) {
+    if (ko.order == 3 && !ko.fold) {
       mark_begin(kPhDot, stream_);
       dev::launch_red(ko, par, stream_);
       mark_end(stream_);
@@ -1287,7 +1308,7 @@ void DeviceSolver::enqueue_iteration(int par) {
     mark_begin(kPhSweep, stream_);
     dev::launch_S(*kp_, par, stream_, false);
     mark_end(stream_);
-    if (kp_->order == 3) {
+    if (kp_->order == 3 && !kp_->fold) {
       mark_begin(kPhDot, stream_);
       dev::launch_red(*kp_, par, stream_);
       mark_end(stream_);
@@ -1721,7 +1742,7 @@ SolveResult DeviceSolver::solve() {
     res.t.reduce = sum[kPhReduce] * scale;
     res.t.copy = copy_s + (ncopy > 0 ? sum[kPhCopy] * double(chunks_run) / double(ncopy) : 0.0);
     res.t.sampled = double(nit);
-    res.t.dot_fused = !(fused_ && kp_->order == 3);
+    res.t.dot_fused = !(fused_ && kp_->order == 3 && !kp_->fold);
     if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
   }
   res.t.solver = construct + secs(t_start, clk::now());

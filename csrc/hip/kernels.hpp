@@ -140,7 +140,19 @@ struct KParams {
   double* hpush_hi[2];
   const double* hrecv;
   int push;
+  // In-kernel item-sum fold (dynamic sweeps, fold = 1): the wave that counts
+  // the last item of a group of kFoldGroup consecutive slots sums that group
+  // (fixed lane order) into gsum[g]; the last wave to leave the sweep — every
+  // wave has read the state by then — sums the groups in order and updates
+  // the state, so no separate reduction kernel runs.  Counters: gcnt[g] per
+  // group, xcnt[16·x] per XCD shard of exiting waves, xcnt[16·8] shards done;
+  // each is reset by the wave that completes it.
+  int fold;
+  unsigned* gcnt;
+  unsigned* xcnt;
+  double* gsum;
 };
+constexpr int kFoldGroup = 64;
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
 constexpr int kWPB = 4;          // waves per block

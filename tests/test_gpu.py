@@ -143,6 +143,7 @@ def test_fused_item_orders_deterministic(gpu, order, monkeypatch):
     # order 3 = per-XCD dynamic work queue: which wave takes which item varies
     # run to run, the per-item sums keep the result bitwise reproducible
     monkeypatch.setenv("PE_ORDER", order)
+    monkeypatch.setenv("PE_RESIDENT", "0")  # the streaming sweep (800×1200 would run resident)
     prob = EllipseProblem(800, 1200)
     a = solve(prob, backend="hip", return_w=True, algo="fused")
     b = solve(prob, backend="hip", return_w=True, algo="fused")
@@ -150,6 +151,26 @@ def test_fused_item_orders_deterministic(gpu, order, monkeypatch):
     assert np.array_equal(a.w, b.w)
     monkeypatch.setenv("PE_ORDER", "0")
     c = solve(prob, backend="hip", return_w=True, algo="fused")
+    np.testing.assert_allclose(a.w, c.w, rtol=0, atol=1e-10)
+
+
+@pytest.mark.parametrize("M,N", [(800, 1200), (2048, 2048)])
+def test_item_sum_fold_matches_reduction_kernel(gpu, M, N, monkeypatch):
+    """PE_FOLD=1: dynamic sweeps fold their per-item sums inside the sweep
+    (groups of 64 slots summed by the wave that completes the group, the
+    groups by the last wave to leave) instead of launching kRed: same
+    iteration count, w equal to rounding, bitwise reproducible run to run."""
+    monkeypatch.setenv("PE_ORDER", "3")
+    monkeypatch.setenv("PE_RESIDENT", "0")
+    monkeypatch.setenv("PE_FOLD", "1")
+    prob = EllipseProblem(M, N)
+    a = solve(prob, backend="hip", return_w=True)
+    b = solve(prob, backend="hip", return_w=True)
+    monkeypatch.setenv("PE_FOLD", "0")
+    c = solve(prob, backend="hip", return_w=True)
+    assert a.iters == b.iters and abs(a.iters - c.iters) <= 1
+    assert a.iters == {(800, 1200): 989, (2048, 2048): 1730}[(M, N)]
+    assert np.array_equal(a.w, b.w)
     np.testing.assert_allclose(a.w, c.w, rtol=0, atol=1e-10)
 
 
@@ -296,7 +317,8 @@ def test_two_process_device_path_host_staged(gpu):
                                                         (4, "aspect", "0", "rccl"), (4, "aspect", "1", "p2p"),
                                                         (2, "aspect", "0", "p2p"), (4, "aspect", "1", "p2p-kernel"),
                                                         (3, "rows", "0", "p2p"), (4, "rows", "0", "p2p"),
-                                                        (3, "rows", "0", "p2p-exchange")])
+                                                        (3, "rows", "0", "p2p-exchange"), (3, "rows", "0", "p2p-dyn"),
+                                                        (4, "aspect", "0", "p2p-dyn")])
 def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
     rows through the x phase of the single-sweep halo) — and 3×1 — match the
@@ -307,12 +329,17 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     ("p2p"), or through the standalone one-shot P2P kernel ("p2p-kernel",
     PE_XR=0).  Row slabs with the in-sweep sums push their halo rows from the
     sweep into the neighbours' receive buffers (no exchange call);
-    "p2p-exchange" (PE_HALO=exchange) keeps the exchange."""
+    "p2p-exchange" (PE_HALO=exchange) keeps the exchange; "p2p-dyn" runs the
+    dynamic item queue (PE_ORDER=3) with the in-sweep fold of its item sums
+    (PE_FOLD=1), whose cross-rank sum is then done by one wave."""
     from conftest import free_port
 
     env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce.split("-")[0],
                PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1",
                PE_HALO="exchange" if allreduce == "p2p-exchange" else "push")
+    if allreduce == "p2p-dyn":
+        env["PE_ORDER"] = "3"
+        env["PE_FOLD"] = "1"
     outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}_{allreduce}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -323,8 +350,8 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
     assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
-    assert d["xr"] == (allreduce in ("p2p", "p2p-exchange"))
-    assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p")
+    assert d["xr"] == (allreduce in ("p2p", "p2p-exchange", "p2p-dyn"))
+    assert d["halo_push"] == (d["Py"] == 1 and allreduce in ("p2p", "p2p-dyn"))
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
