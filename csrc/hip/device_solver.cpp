@@ -410,7 +410,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     const size_t nw = size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
     nstamps_ = 4 * size_t(nslot_cap_) + 2 * nw + 32 * nw;
     PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
-    PE_HIP_CHECK(hipMemset(stamps_, 0, sizeof(unsigned long long) * nstamps_));
+    PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
     k.stamps = stamps_;
     k.stamps2 = stamps_ + nstamps_ - 32 * nw;  // the last 32 × waves entries
   }
@@ -433,7 +433,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // counters] → 64-B aligned [group sums, 8 doubles each]
     fold_bytes_ = ((sizeof(unsigned) * (16 * 9 + size_t(ng)) + 63) / 64) * 64;
     PE_HIP_CHECK(hipMalloc(&fold_buf_, fold_bytes_ + sizeof(double) * 8 * size_t(ng)));
-    PE_HIP_CHECK(hipMemset(fold_buf_, 0, fold_bytes_));
+    PE_HIP_CHECK(hipMemsetAsync(fold_buf_, 0, fold_bytes_, stream_));
     PE_HIP_CHECK(hipDeviceSynchronize());
     k.xcnt = static_cast<unsigned*>(fold_buf_);
     k.gcnt = k.xcnt + 16 * 9;
@@ -465,6 +465,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   mark("tuning+rest");
+  // One small runtime copy at construction: the runtime initialises its copy
+  // path lazily at the first hipMemcpy of the process (7-170 ms,
+  // profiles/r2_init_probe.txt); without this the cost lands inside the
+  // iteration loop (the final state read) and inflates the loop time by
+  // 4 µs per iteration at 1600×2400 (profiles/r2_ctor_phases.txt).  Either
+  // way it is inside T_solver.  PE_WARM_COPY=0 skips it.
+  if (!(std::getenv("PE_WARM_COPY") && std::atoi(std::getenv("PE_WARM_COPY")) == 0)) {
+    double h = 0.0;
+    PE_HIP_CHECK(hipMemcpy(partial_, &h, sizeof(double), hipMemcpyHostToDevice));
+  }
   PE_HIP_CHECK(hipDeviceSynchronize());
   ctor_s_ = secs(t_ctor, clk::now());
 }
@@ -490,7 +500,7 @@ void DeviceSolver::setup_halo_push() {
     buf = nullptr;
     (void)hipGetLastError();
   } else {
-    PE_HIP_CHECK(hipMemset(buf, 0, bytes));
+    PE_HIP_CHECK(hipMemsetAsync(buf, 0, bytes, stream_));
     PE_HIP_CHECK(hipDeviceSynchronize());
   }
   // a rank without a buffer still takes part (its map fails → every rank gets
@@ -897,12 +907,14 @@ void DeviceSolver::setup_resident() {
   upload(res_rowstart_, rs.data(), sizeof(int) * rs.size());
   const size_t nedge = size_t(2) * size_t(nwg) * dev::kResEdge, npart = size_t(2) * size_t(nwg) * 8;
   PE_HIP_CHECK(hipMalloc(&res_buf_, sizeof(double) * (nedge + npart)));
-  PE_HIP_CHECK(hipMemset(res_buf_, 0, sizeof(double) * (nedge + npart)));
+  // stream-ordered: a null-stream operation would create that stream's
+  // hardware queue (≈10 ms inside T_solver in a fresh process, profiles/r2_ctor_phases.txt)
+  PE_HIP_CHECK(hipMemsetAsync(res_buf_, 0, sizeof(double) * (nedge + npart), stream_));
   PE_HIP_CHECK(hipMalloc(&res_ctr_, sizeof(unsigned) * 8 * 32));
   if (const char* t = std::getenv("PE_RES_STAMPS"); t && std::atoi(t) == 1) {
     nstamps_ = size_t(nwg) * dev::kResStampIters * 8;
     PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
-    PE_HIP_CHECK(hipMemset(stamps_, 0, sizeof(unsigned long long) * nstamps_));
+    PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
     r.stamps = stamps_;
   }
   r.rowstart = res_rowstart_;
@@ -946,7 +958,7 @@ void DeviceSolver::choose_placement() {
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
   double skip_gb = 8.0;
   if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
-  double fast_tbs = 4.6;
+  double fast_tbs = 4.75;
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return;
   // spacers are transient; never let the search take more than 40 % of the
@@ -999,14 +1011,18 @@ void DeviceSolver::choose_placement() {
     PE_HIP_CHECK(hipEventRecord(t1_, stream_));
     PE_HIP_CHECK(hipEventSynchronize(t1_));
     PE_HIP_CHECK(hipEventElapsedTime(&c[t].ms, t0_, t1_));
-    // The placements differ by up to ~15 %: stop at the first candidate in
-    // the fast class — streaming the sweep's average 40 B/node at
-    // >= PE_PLACEMENT_FAST_TBS (4.6 TB/s; 8192²: fast 4.75-4.9, slow
-    // 4.1-4.4) — else keep the best of all tries.  (A "5 % faster than the
-    // slowest seen" stop settled for 0.59-0.60 ms sweeps when 0.55-0.575 ones
-    // were a few candidates further.)
+    // The placements differ by up to ~15 % (8192²: fast 0.546-0.562 ms per
+    // sweep, intermediate 0.57-0.61, slow 0.62-0.65): stop at the first
+    // candidate in the fast class — streaming the sweep's average 40 B/node
+    // at >= PE_PLACEMENT_FAST_TBS (4.75 TB/s = 0.565 ms at 8192²) — or 7 %
+    // faster than the slowest seen (blocks whose fast class streams slower),
+    // else keep the best of all tries.  (A "5 % faster than the slowest"
+    // stop settled for 0.59-0.60 ms, and a 4.6 TB/s one for 0.577 ms, when
+    // 0.55-0.56 ms placements were a candidate or two further.)
     const double tbs = 40.0 * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
-    if (tbs >= fast_tbs) break;
+    float worst = 0.f;
+    for (const Cand& x : c) worst = std::max(worst, x.ms);
+    if (tbs >= fast_tbs || (t > 0 && c[t].ms < 0.93f * worst)) break;
   }
   (void)hipGetLastError();  // clear a failed search allocation
   size_t best = 0;
@@ -1613,6 +1629,10 @@ SolveResult DeviceSolver::solve() {
   res.t.construct = construct;
   res.t.setup = construct + secs(t_start, clk::now());
   const int64_t ck_every = opt_.checkpoint_path.empty() ? 0 : opt_.checkpoint_every;
+  // per-chunk state read: a copy kernel into mapped pinned memory (default),
+  // or PE_STATE_COPY=memcpy (hipMemcpyAsync; its first use initialises the
+  // runtime's copy path inside T_solver)
+  state_memcpy_ = std::getenv("PE_STATE_COPY") && std::string(std::getenv("PE_STATE_COPY")) == "memcpy";
 
   // Phase sampling: every `sample_every`-th chunk, its first two iterations
   // (all of them with opt_.timing); no host sync beyond the per-chunk state
@@ -1650,7 +1670,10 @@ SolveResult DeviceSolver::solve() {
       sampling_ = sample;
       sample_iter_ = enq - 1;
       mark_begin(kPhCopy, stream_);
-      dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
+      if (state_memcpy_)
+        PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+      else
+        dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
       mark_end(stream_);
       sampling_ = false;
       PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
@@ -1706,7 +1729,9 @@ SolveResult DeviceSolver::solve() {
   res.last_diff = hs.last_diff;
   if (hist_ && hs.iter > 0) {
     res.history.resize(size_t(std::min<long long>(hs.iter, kp_->hist_n)));
-    PE_HIP_CHECK(hipMemcpy(res.history.data(), hist_, sizeof(double) * res.history.size(), hipMemcpyDeviceToHost));
+    PE_HIP_CHECK(hipMemcpyAsync(res.history.data(), hist_, sizeof(double) * res.history.size(), hipMemcpyDeviceToHost,
+                                stream_));
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
   }
   res.zr = hs.rz_cur;
   if (opt_.compute_error) {

@@ -394,7 +394,8 @@ __device__ __forceinline__ unsigned long long rtc() {
 // also stored into the x-neighbours' fine-grained receive buffers over xGMI
 // (system-scope write-through stores, drained and released before the item
 // ends, so they are delivered before this rank's cross-rank-sum flags).
-template <int OCC, int PF, bool NT, int WM, bool STAMP = false, bool PUSH = false>
+// FOLD — in-kernel item-sum fold (KParams::fold, dynamic sweeps, opt-in).
+template <int OCC, int PF, bool NT, int WM, bool STAMP = false, bool PUSH = false, bool FOLD = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   const unsigned long long t_entry = STAMP ? rtc() : 0ull;
@@ -537,7 +538,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       } else {
         w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
       }
-      if ((!persum || k.fold) && arrive_last(&st->ticket[0], gridDim.x, &sflag) && threadIdx.x == 0) {
+      if ((!persum || FOLD) && arrive_last(&st->ticket[0], gridDim.x, &sflag) && threadIdx.x == 0) {
         sweep_terminal(k, st, sc, tm);
         __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -882,7 +883,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       // wave pulled which item
       double v[7] = {sg, sd, se, sps, szz, szp, spp};
       wave_sum7(v);
-      if (k.fold) {
+      if constexpr (FOLD) {
         fold_item(k, slot, v);
       } else if (lane == 0) {
         double* dst = k.itemsum + 8 * slot;
@@ -916,7 +917,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   }
   if (!state_ok && leave()) return;
   if (persum) {  // kRed reduces the item sums and finalizes — or the fold, here
-    if (k.fold) fold_exit<WM>(k, st, par, sc);
+    if constexpr (FOLD) fold_exit<WM>(k, st, par, sc);
     return;
   }
 
@@ -1186,7 +1187,8 @@ static int s_cfg() {
 template <int WM, class F>
 static auto with_kS(const KParams& k, F&& f) {
   if (k.stamps) return f(kS<2, 4, true, WM, true>);
-  if (k.push) return f(kS<2, 4, true, WM, false, true>);
+  if (k.push) return k.fold ? f(kS<2, 4, true, WM, false, true, true>) : f(kS<2, 4, true, WM, false, true>);
+  if (k.fold) return f(kS<2, 4, true, WM, false, false, true>);
   switch (s_cfg()) {
     case 1: return f(kS<2, 4, false, WM>);
     default: return f(kS<2, 4, true, WM>);

@@ -286,6 +286,7 @@ class DeviceSolver {
   unsigned* res_ctr_ = nullptr;
   void* fold_buf_ = nullptr;        // item-sum fold: counters, then group sums (KParams::gcnt/xcnt/gsum)
   size_t fold_bytes_ = 0;           // its counter part (zeroed per solve)
+  bool state_memcpy_ = false;       // PE_STATE_COPY=memcpy: per-chunk state read by hipMemcpyAsync
   void* stage_ = nullptr;           // pinned staging buffer of upload()
   size_t stage_bytes_ = 0;
   int alloc_mode_ = 0;              // field allocation: 0 hipMalloc, 2 shuffled physical chunks (large blocks)
