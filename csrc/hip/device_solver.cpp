@@ -512,6 +512,55 @@ void DeviceSolver::setup_halo_push() {
   }
   hrecv_ = static_cast<double*>(buf);
   push_ = true;
+  // Collective self-test of the path, in its own store / load forms: every
+  // rank fills its neighbours' receive buffers with rank-coded values, the
+  // ranks synchronise, every rank checks what arrived; all ranks keep the
+  // exchange if any check fails.  The buffers are then cleared (their halo
+  // columns must stay zero) and the ranks synchronise again before any
+  // sweep can push.
+  {
+    KParams t = *kp_;
+    const int64_t side = 2 * t.pitch;
+    for (int b = 0; b < 2; ++b) {
+      t.hpush_lo[b] = blk_.has(LEFT) ? static_cast<double*>(hpeers_[size_t(blk_.nbr[LEFT])]) + (2 * b + 1) * side
+                                     : nullptr;
+      t.hpush_hi[b] = blk_.has(RIGHT) ? static_cast<double*>(hpeers_[size_t(blk_.nbr[RIGHT])]) + (2 * b + 0) * side
+                                      : nullptr;
+    }
+    t.hrecv = hrecv_;
+    int* bad = nullptr;
+    PE_HIP_CHECK(hipMalloc(&bad, sizeof(int)));
+    PE_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), stream_));
+    dev::launch_push_test_write(t, blk_.rank, stream_);
+    PE_HIP_CHECK(hipGetLastError());
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    comm_->barrier(stream_);
+    dev::launch_push_test_check(t, blk_.has(LEFT) ? blk_.nbr[LEFT] : -1, blk_.has(RIGHT) ? blk_.nbr[RIGHT] : -1, bad,
+                                stream_);
+    PE_HIP_CHECK(hipGetLastError());
+    int hbad = 0;
+    PE_HIP_CHECK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    PE_HIP_CHECK(hipFree(bad));
+    // PE_FAULT_INJECT=pushtest@rank:R — rank R's check fails (fallback test)
+    if (const char* e = std::getenv("PE_FAULT_INJECT"); e && std::string(e).rfind("pushtest@rank:", 0) == 0 &&
+                                                        std::atoi(e + 14) == blk_.rank)
+      hbad = 1;
+    double fail[1] = {hbad != 0 ? 1.0 : 0.0};
+    if (hbad) std::fprintf(stderr, "[pe] rank %d: halo-push self-test: %d wrong values received\n", blk_.rank, hbad);
+    comm_->host_max(fail, 1, stream_);
+    PE_HIP_CHECK(hipMemsetAsync(buf, 0, bytes, stream_));
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    comm_->barrier(stream_);
+    if (fail[0] != 0.0) {
+      if (blk_.rank == 0) std::fprintf(stderr, "[pe] halo push unavailable on this job (self-test), using the exchange\n");
+      comm_->unmap_peer_buffers(hpeers_);
+      hpeers_.clear();
+      PE_HIP_CHECK(hipFree(buf));
+      hrecv_ = nullptr;
+      push_ = false;
+    }
+  }
 }
 
 void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {

@@ -1144,6 +1144,38 @@ __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
   }
 }
 
+// Halo-push set-up self-test (DeviceSolver::setup_halo_push): every rank
+// fills its neighbours' receive buffers through the push's own store form
+// with values naming sender, side, parity and index; after a cross-rank
+// barrier every rank checks what arrived (system-scope loads).
+__device__ __forceinline__ double push_code(int rank, int side, int b, int64_t i) {
+  return double((rank * 2 + side) * 2 + b) * 1e7 + double(i);
+}
+__global__ __launch_bounds__(256) void kPushTestWrite(KParams k, int me) {
+  const int64_t n = 2 * k.pitch;
+  for (int b = 0; b < 2; ++b)
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
+      if (k.hpush_lo[b]) __hip_atomic_store(k.hpush_lo[b] + i, push_code(me, 1, b, i), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+      if (k.hpush_hi[b]) __hip_atomic_store(k.hpush_hi[b] + i, push_code(me, 0, b, i), __ATOMIC_RELAXED,
+                                            __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+}
+__global__ __launch_bounds__(256) void kPushTestCheck(KParams k, int left, int right, int* bad) {
+  const int64_t n = 2 * k.pitch;
+  int nbad = 0;
+  for (int b = 0; b < 2; ++b)
+    for (int side = 0; side < 2; ++side) {
+      const int from = side == 0 ? left : right;
+      if (from < 0) continue;
+      const double* src = k.hrecv + (int64_t(b) * 2 + side) * n;
+      for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+        nbad += __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != push_code(from, side, b, i);
+    }
+  if (nbad) atomicAdd(bad, nbad);
+}
+
 // Test op: the division-free coefficients the single-sweep kernels evaluate
 // (cset_rc from the row classes and chord tables) for every node of the block
 // plus its 1-wide ring, dense [(nx+2) × (ny+2)]: a(li, lj), b(li, lj), 1/D.
@@ -1255,6 +1287,13 @@ int resident_blocks_S(const KParams& k, int wm) {
 void launch_pack(const KParams& k, int b, hipStream_t s) {
   if (!k.has[DOWN] && !k.has[UP]) return;
   hipLaunchKernelGGL(kPack, dim3(unsigned((k.nx + 255) / 256)), dim3(256), 0, s, k, b);
+}
+
+void launch_push_test_write(const KParams& k, int me, hipStream_t s) {
+  hipLaunchKernelGGL(kPushTestWrite, dim3(64), dim3(256), 0, s, k, me);
+}
+void launch_push_test_check(const KParams& k, int left, int right, int* bad, hipStream_t s) {
+  hipLaunchKernelGGL(kPushTestCheck, dim3(64), dim3(256), 0, s, k, left, right, bad);
 }
 
 void launch_halo_import(const KParams& k, int b, hipStream_t s) {

@@ -218,6 +218,12 @@ void launch_unpack(const KParams& k, int b, hipStream_t s);
 // the neighbours' sweeps, delivered once the sweep's cross-rank sum has
 // completed) into x[b]'s halo rows -1, 0 / nx+1, nx+2 (no-op once done).
 void launch_halo_import(const KParams& k, int b, hipStream_t s);
+// Halo-push set-up self-test: write rank-coded values into the neighbours'
+// receive buffers (k.hpush_*), then — after a cross-rank barrier — count in
+// *bad the received values (k.hrecv) that differ from the neighbours' codes
+// (left / right: neighbour ranks, -1 where none).
+void launch_push_test_write(const KParams& k, int me, hipStream_t s);
+void launch_push_test_check(const KParams& k, int left, int right, int* bad, hipStream_t s);
 // Overlap: spin until st->sig reaches `target` (every boundary item of the
 // running sweep is in L2) or the solve is done, then write every XCD's L2
 // back.  Put on the halo stream ahead of the exchange.

@@ -358,6 +358,24 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)
 
 
+def test_halo_push_selftest_failure_falls_back(gpu):
+    """A failed halo-push self-test on ONE rank (PE_FAULT_INJECT=pushtest@rank:1)
+    makes every rank keep the exchange: the job still solves correctly."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60",
+               PE_FAULT_INJECT="pushtest@rank:1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+           "--quiet", "--decomp", "rows", "400", "600"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["ranks"] == 3 and d["Py"] == 1 and d["xr"] and not d["halo_push"]
+    assert d["iters"] == 546
+    assert "halo push unavailable" in out.stderr
+
+
 @pytest.mark.parametrize("nproc", [2, 4])
 def test_bench_halo_push_graphs(gpu, nproc):
     """bench.py on row slabs over the P2P transport (processes sharing the
