@@ -1,3 +1,4 @@
+# Placement experiment: the three arrays carved from ONE allocation at relative offsets (PE_PLACEMENT=carve), 4 solvers per process, 3 processes.
 cd $GRAFT_REPO_ROOT
 mkdir -p gpurun_out/place
 for r in 1 2 3; do
