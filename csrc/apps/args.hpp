@@ -54,7 +54,7 @@ class Args {
 
  private:
   static bool is_bool_flag(const std::string& k) {
-    static const char* b[] = {"json", "legacy", "verbose", "no-graph", "timing", "no-tol", "help", "history", "quiet"};
+    static const char* b[] = {"json", "legacy", "verbose", "no-graph", "graph", "timing", "no-tol", "help", "history", "quiet"};
     for (auto* s : b)
       if (k == s) return true;
     return false;

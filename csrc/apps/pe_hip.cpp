@@ -3,7 +3,7 @@
 //
 //   pe_hip [--tol 1e-6] [--max-iter K] [--decomp device|aspect|reference|rows|cols|PxxPy]
 //          [--init zero|random] [--seed S] [--variant 0|1] [--algo auto|classic|fused] [--chunk K]
-//          [--no-graph] [--timing] [--vranks P] [--json] [M N]
+//          [--graph] [--timing] [--vranks P] [--json] [M N]
 //
 // Multi-GPU: `pe_launch -n 8 bin/pe_hip 8192 8192` (or torchrun-style env
 // RANK / WORLD_SIZE / LOCAL_RANK).  The RCCL unique id is exchanged through
@@ -77,7 +77,7 @@ int main(int argc, char** argv) {
     opt.algo = a == "classic" ? 1 : a == "fused" ? 2 : 0;
   }
   opt.chunk = int(args.geti("chunk", 0));
-  opt.use_graph = !args.flag("no-graph");
+  opt.use_graph = args.flag("graph") && !args.flag("no-graph");
   opt.timing = args.flag("timing");
   opt.check_tol = !args.flag("no-tol");  // fixed-iteration runs (with --max-iter) for profiling
   opt.checkpoint_path = args.get("checkpoint", "");

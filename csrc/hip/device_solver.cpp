@@ -465,13 +465,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   mark("tuning+rest");
-  // One small runtime copy at construction: the runtime initialises its copy
-  // path lazily at the first hipMemcpy of the process (7-170 ms,
-  // profiles/r2_init_probe.txt); without this the cost lands inside the
-  // iteration loop (the final state read) and inflates the loop time by
-  // 4 µs per iteration at 1600×2400 (profiles/r2_ctor_phases.txt).  Either
-  // way it is inside T_solver.  PE_WARM_COPY=0 skips it.
-  if (!(std::getenv("PE_WARM_COPY") && std::atoi(std::getenv("PE_WARM_COPY")) == 0)) {
+  // PE_WARM_COPY=1: one small pageable copy at construction.  The runtime
+  // sets up its pageable-copy path lazily at the first such copy of the
+  // process (≈19 ms, profiles/r2_init_probe.txt) — which a graph
+  // instantiation triggers; with graph-replayed solves (--graph) this keeps
+  // that cost out of the iteration loop (4 µs per iteration at 1600×2400
+  // otherwise).  The default eager solve never takes that path.
+  if (std::getenv("PE_WARM_COPY") && std::atoi(std::getenv("PE_WARM_COPY")) == 1) {
     double h = 0.0;
     PE_HIP_CHECK(hipMemcpy(partial_, &h, sizeof(double), hipMemcpyHostToDevice));
   }

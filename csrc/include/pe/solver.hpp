@@ -61,7 +61,12 @@ struct SolveOptions {
   bool verbose = false;
   // Device backend knobs.
   int chunk = 0;             // iterations enqueued per host check (0 = auto)
-  bool use_graph = true;     // capture a chunk of iterations into a hipGraph
+  // Capture a chunk of iterations into a hipGraph.  Off for solves: eager
+  // launches keep up with the GPU (≥ 12 µs of kernel per iteration) and a
+  // graph's instantiation pays the runtime's lazy copy-path set-up inside
+  // T_solver (1600×2400: 0.126 vs 0.134-0.150 s, same µs / iteration,
+  // profiles/r2_graph_ab.txt).  bench.py replays instantiated graphs.
+  bool use_graph = false;
   bool timing = false;       // time every iteration's phases (default: a sample of them)
   bool check_tol = true;     // false: never stop on ‖Δw‖ (fixed-iteration benchmarking)
   int variant = 0;           // device arithmetic: 0 fast (1/h², 1/D), 1 reference expression trees

@@ -48,7 +48,8 @@ def build_parser():
     ap.add_argument("--checkpoint-every", type=int, default=0, help="hip: iterations between checkpoints")
     ap.add_argument("--resume", default=None, help="hip: resume from checkpoint prefix")
     ap.add_argument("--log-every", type=int, default=0, help="print ||dw|| every K iterations (hip: chunk-granular)")
-    ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-graph", action="store_true", help="(default) eager launches")
+    ap.add_argument("--graph", action="store_true", help="replay chunks of iterations from hipGraphs")
     ap.add_argument("--json", action="store_true")
     ap.add_argument("--quiet", action="store_true", help="suppress the legacy lines")
     ap.add_argument("--dump", default=None, help="write w (interior) to this .npy")
@@ -66,7 +67,7 @@ def main(argv=None) -> int:
     prob.norm = a.norm
     want_w = bool(a.dump or a.pgm)
     rep = solve(prob, backend=a.backend, ranks=a.ranks, threads=a.threads, decomp=a.decomp, init=a.init,
-                seed=a.seed, return_w=want_w, variant=a.variant, timing=a.timing, graph=not a.no_graph,
+                seed=a.seed, return_w=want_w, variant=a.variant, timing=a.timing, graph=a.graph and not a.no_graph,
                 algo=a.algo, checkpoint=a.checkpoint, checkpoint_every=a.checkpoint_every, resume=a.resume,
                 log_every=a.log_every)
     if rep.rank != 0:

@@ -74,7 +74,7 @@ class SolveReport:
 ALGOS = {"auto": 0, "classic": 1, "fused": 2}
 
 
-def _options(init="zero", seed=1234, threads=1, chunk=0, graph=True, timing=False, check_tol=True, variant=0,
+def _options(init="zero", seed=1234, threads=1, chunk=0, graph=False, timing=False, check_tol=True, variant=0,
              keep_history=False, log_every=0, algo="auto", checkpoint_every=0, checkpoint=None, resume=None):
     nat = native()
     o = nat.SolveOptions()
@@ -164,7 +164,7 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
         world = tdist.get_world_size()
     else:
         world = _dist.env_rank_world()[1]
-    opt = _options(init, seed, chunk=kw.get("chunk", 0), graph=kw.get("graph", True), timing=kw.get("timing", False),
+    opt = _options(init, seed, chunk=kw.get("chunk", 0), graph=kw.get("graph", False), timing=kw.get("timing", False),
                    check_tol=kw.get("check_tol", True), variant=kw.get("variant", 0), algo=kw.get("algo", "auto"),
                    checkpoint_every=kw.get("checkpoint_every", 0), checkpoint=kw.get("checkpoint"),
                    resume=kw.get("resume"), keep_history=kw.get("keep_history", False),

@@ -210,11 +210,12 @@ def test_random_init_matches_cpu(gpu):
     np.testing.assert_allclose(d.w, c.w, rtol=0, atol=1e-9)
 
 
-def test_bitwise_deterministic_and_graph_equivalent(gpu):
+def test_bitwise_deterministic_and_graph_equivalent(gpu, monkeypatch):
+    monkeypatch.setenv("PE_RESIDENT", "0")  # the streaming sweep (500×700 would run resident)
     prob = EllipseProblem(500, 700)
-    a = solve(prob, backend="hip", return_w=True)
+    a = solve(prob, backend="hip", return_w=True)  # eager launches (default)
     b = solve(prob, backend="hip", return_w=True)
-    c = solve(prob, backend="hip", return_w=True, graph=False)
+    c = solve(prob, backend="hip", return_w=True, graph=True)  # chunks replayed from hipGraphs
     assert a.iters == b.iters == c.iters
     assert np.array_equal(a.w, b.w) and np.array_equal(a.w, c.w)
 

@@ -40,6 +40,21 @@ int main() {
   T("hipMalloc 1 MB (first)", (void)hipMalloc(&a, 1 << 20));
   T("hipMalloc 1 MB (second)", (void)hipMalloc(&b, 1 << 20));
   T("hipMalloc 1 GB", (void)hipMalloc(&c, size_t(1) << 30));
+  hipStream_t s0;
+  T("hipStreamCreate (first)", (void)hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
+  T("kernel launch on it (first)", hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s0, a, 1 << 14));
+  double* hp = nullptr;
+  T("hipHostMalloc 1 MB pinned (first)", (void)hipHostMalloc(&hp, 1 << 20, hipHostMallocDefault));
+  T("kernel writes pinned host memory (first)", hipLaunchKernelGGL(k_copy, dim3(64), dim3(256), 0, s0, a, hp, 1 << 14));
+  T("kernel writes pinned host memory (second)", hipLaunchKernelGGL(k_copy, dim3(64), dim3(256), 0, s0, a, hp, 1 << 14));
+  T("kernel reads pinned host memory (first)", hipLaunchKernelGGL(k_copy, dim3(64), dim3(256), 0, s0, hp, b, 1 << 14));
+  hipEvent_t e0, e1;
+  T("hipEventCreate x2", ((void)hipEventCreate(&e0), (void)hipEventCreate(&e1)));
+  T("hipEventRecord + sync", ((void)hipEventRecord(e0, s0), (void)hipEventRecord(e1, s0), (void)hipEventSynchronize(e1)));
+  float ms = 0;
+  T("hipEventElapsedTime", (void)hipEventElapsedTime(&ms, e0, e1));
+  T("hipMemcpyAsync D2H 8 B pinned on stream (first copy)", ((void)hipMemcpyAsync(hp, a, 8, hipMemcpyDeviceToHost, s0), (void)hipStreamSynchronize(s0)));
+  T("hipMemcpyAsync D2H 8 B pinned on stream (second)", ((void)hipMemcpyAsync(hp, a, 8, hipMemcpyDeviceToHost, s0), (void)hipStreamSynchronize(s0)));
   std::vector<double> host(1 << 14, 1.0);
   T("hipMemcpy H2D 128 KB pageable (first)", (void)hipMemcpy(a, host.data(), host.size() * 8, hipMemcpyHostToDevice));
   T("hipMemcpy H2D 128 KB pageable (second)", (void)hipMemcpy(b, host.data(), host.size() * 8, hipMemcpyHostToDevice));
