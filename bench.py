@@ -53,6 +53,8 @@ def main() -> int:
     ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solve")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused"))
+    ap.add_argument("--launch", default="graph", choices=("graph", "eager"),
+                    help="timed steps replayed from instantiated hipGraphs (default) or launched eagerly")
     a = ap.parse_args()
     M, N = (a.grid[0], a.grid[-1])
 
@@ -102,18 +104,20 @@ def main() -> int:
 
     # warmup: first-touch / RCCL connections, then instantiate every chunk
     # graph the timed run will launch (no capture inside the timed region)
+    use_graph = a.launch == "graph"
     solver.reset()
     if a.warmup > 0:
-        solver.run_iterations(a.warmup, True)
+        solver.run_iterations(a.warmup, use_graph)
     solver.synchronize()
-    solver.prepare_graphs(a.steps)
+    if use_graph:
+        solver.prepare_graphs(a.steps)
     solver.reset()  # the timed steps start a fresh solve (w⁰ = 0)
     solver.synchronize()
     torch.cuda.synchronize()
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    solver.run_iterations(a.steps, True)
+    solver.run_iterations(a.steps, use_graph)
     solver.synchronize()
     torch.cuda.synchronize()
     barrier()
@@ -124,19 +128,17 @@ def main() -> int:
 
     extra = {}
     if not a.no_solve:
-        sopt = nat.SolveOptions()
-        sopt.variant = a.variant
-        sopt.algo = opt.algo
-        full = nat.DeviceSolver(P, blk, comm, sopt)
+        # the full solve runs on the same solver (one construction, one
+        # placement search; its T_solver still spans that construction)
+        solver.set_check_tol(True)
         barrier()
-        res = full.solve()
+        res = solver.solve()
         tm = res.timers
         extra = dict(t_solver_s=maxval(tm["solver"]), t_setup_s=maxval(tm["setup"]), t_iterate_s=maxval(tm["iterate"]),
                      t_breakdown_s={k: maxval(tm[k]) for k in ("gpu", "dot", "halo", "reduce", "copy")},
                      iters_converged=int(res.iters), converged=bool(res.converged),
                      l2_err=float(res.l2_err), max_err=float(res.max_err),
                      solve_iters_per_s=float(res.iters) / maxval(tm["iterate"]))
-        del full
 
     ips = a.steps / dt
     out = {
@@ -176,6 +178,7 @@ def main() -> int:
             "rows_per_item_tuning_ms": [round(x, 4) for x in solver.ti_tuning_ms],
             "resident": bool(solver.resident),
             "chunk": solver.chunk,
+            "launch": a.launch,
             "placement": {"candidates_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
                           "chosen": solver.placement_choice, "search_s": round(solver.placement_s, 3)},
             "construct_s": round(solver.construct_s, 3),

@@ -379,6 +379,7 @@ PYBIND11_MODULE(_native, m) {
              s.run_iterations(n, g);
            },
            py::arg("iters"), py::arg("use_graph") = true)
+      .def("set_check_tol", &DeviceSolver::set_check_tol, py::arg("on"))
       .def("prepare_graphs",
            [](DeviceSolver& s, int64_t n) {
              py::gil_scoped_release nogil;

@@ -121,6 +121,9 @@ class DeviceSolver {
   // Capture + instantiate every chunk graph run_iterations(iters, true)
   // will launch, so a timed run_iterations contains no capture.
   void prepare_graphs(int64_t iters);
+  // Switch the convergence test on / off (drops cached graphs): the bench
+  // times fixed-work steps, then solves to convergence on the same solver.
+  void set_check_tol(bool on);
   double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
   void synchronize();
 
