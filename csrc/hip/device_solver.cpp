@@ -383,9 +383,26 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // communication: the in-sweep cross-rank sum is not set up yet) and keep
     // the fastest; every rank tunes its own block
     Range range("pe.tune_rows_per_item");
+    // candidates: the fixed set plus, for q = 2..5 items per wave, the
+    // smallest item height that gives every wave at most q items — a static
+    // layout's sweep lasts as long as its most loaded wave, and 3.4 items per
+    // wave means a quarter of the waves runs a 4th item while the rest idle
+    // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
+    std::vector<int> cands(kTiCands, kTiCands + 4);
+    {
+      const int64_t W = std::max(dev::kWPB, wave_cap_);
+      for (int q = 2; q <= 5; ++q)
+        for (int t = kTiCands[0]; t <= 40; ++t)
+          if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
+            cands.push_back(t);
+            break;
+          }
+      std::sort(cands.begin(), cands.end());
+      cands.erase(std::unique(cands.begin(), cands.end()), cands.end());
+    }
     float best_ms = 0.f;
     int best = ti;
-    for (int cand : kTiCands) {
+    for (int cand : cands) {
       set_items(cand);
       setup_items();
       enqueue_init();

@@ -35,8 +35,10 @@ for P, spec in configs:
         s.reset()
         s.time_iterations(20, False)
         dt = s.time_iterations(iters, False)
+        tune = " ".join(f"{x * 1e3:.1f}" for x in s.ti_tuning_ms)
         print(f"P={P} {g.Px}x{g.Py} block {blk.nx}x{blk.ny} [{env or 'default'}]: {dt / iters * 1e6:7.1f} us/iter "
-              f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)", flush=True)
+              f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)  ti {s.ti}" + (f"  tuning us/sweep [{tune}]" if tune else ""),
+              flush=True)
         del s, comm
         for k, v in saved.items():
             if v is None:
