@@ -40,6 +40,20 @@ int main() {
   T("hipMalloc 1 MB (first)", (void)hipMalloc(&a, 1 << 20));
   T("hipMalloc 1 MB (second)", (void)hipMalloc(&b, 1 << 20));
   T("hipMalloc 1 GB", (void)hipMalloc(&c, size_t(1) << 30));
+  T("kernel launch on hipStreamPerThread (first)",
+    hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, hipStreamPerThread, a, 1 << 14));
+  T("kernel launch on hipStreamPerThread (second)",
+    hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, hipStreamPerThread, a, 1 << 14));
+  {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    const hipError_t e0 = hipStreamBeginCapture(hipStreamPerThread, hipStreamCaptureModeThreadLocal);
+    hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, hipStreamPerThread, a, 1 << 14);
+    const hipError_t e1 = hipStreamEndCapture(hipStreamPerThread, &g);
+    const hipError_t e2 = g ? hipGraphInstantiate(&ge, g, nullptr, nullptr, 0) : hipErrorInvalidValue;
+    std::printf("capture on hipStreamPerThread: begin %d end %d instantiate %d\n", int(e0), int(e1), int(e2));
+    (void)hipGetLastError();
+  }
   hipStream_t s0;
   T("hipStreamCreate (first)", (void)hipStreamCreateWithFlags(&s0, hipStreamNonBlocking));
   T("kernel launch on it (first)", hipLaunchKernelGGL(k_fill, dim3(64), dim3(256), 0, s0, a, 1 << 14));
