@@ -380,6 +380,7 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("iters"), py::arg("use_graph") = true)
       .def("set_check_tol", &DeviceSolver::set_check_tol, py::arg("on"))
+      .def("relayout", &DeviceSolver::relayout, py::arg("ti"))
       .def("prepare_graphs",
            [](DeviceSolver& s, int64_t n) {
              py::gil_scoped_release nogil;
@@ -430,6 +431,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("construct_s", &DeviceSolver::construct_seconds)
       .def_property_readonly("exchange_us", &DeviceSolver::exchange_us)
       .def_property_readonly("ti_tuning_ms", &DeviceSolver::ti_tuning_ms)
+      .def_property_readonly("ti_tuning_rows", &DeviceSolver::ti_tuning_rows)
+      .def_property_readonly("layout_load", &DeviceSolver::layout_load)
       .def_property_readonly("ti", [](DeviceSolver& s) { return s.params().ti; })
       .def_property_readonly("order", [](DeviceSolver& s) { return s.params().order; })
       .def_property_readonly("xr", [](DeviceSolver& s) { return s.params().xr.peers != nullptr; },

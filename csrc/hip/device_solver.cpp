@@ -415,6 +415,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       float ms = 0.f;
       PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
       ti_ms_.push_back(ms / 6.0f);
+      ti_rows_.push_back(cand);
       if (best_ms == 0.f || ms < best_ms) {
         best_ms = ms;
         best = cand;
@@ -578,6 +579,15 @@ void DeviceSolver::setup_halo_push() {
       push_ = false;
     }
   }
+}
+
+void DeviceSolver::relayout(int ti) {
+  if (!fused_ || resident_) return;
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+  for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));
+  graphs_.clear();
+  set_items(std::max(2, std::min(ti, 64)));
+  setup_items();
 }
 
 void DeviceSolver::set_check_tol(bool on) {
@@ -817,6 +827,15 @@ void DeviceSolver::setup_items() {
     }
     size_t rounds = 0;
     for (const auto& v : per) rounds = std::max(rounds, v.size());
+    lay_max_ = 0.0;
+    lay_mean_ = 0.0;
+    for (int w = 0; w < W; ++w) {
+      double l = 0.0;
+      for (int i : per[size_t(w)]) l += pcs[size_t(i)].cost;
+      lay_max_ = std::max(lay_max_, l);
+      lay_mean_ += l / W;
+    }
+    lay_items_ = int(rounds);
     std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)
     for (int w = 0; w < W; ++w)
       for (size_t r = 0; r < per[size_t(w)].size(); ++r) {
@@ -847,6 +866,8 @@ void DeviceSolver::setup_items() {
     if (overlap_) create_halo_stream();
     return;
   }
+  lay_max_ = lay_mean_ = 0.0;
+  lay_items_ = 0;
   std::vector<double> cost(size_t(k.nitems));
   std::vector<double> ccost(size_t(nchunks) + 1, 0.0);  // prefix sums per chunk
   for (int ch = 0; ch < nchunks; ++ch) {
@@ -863,10 +884,14 @@ void DeviceSolver::setup_items() {
     cut[size_t(x)] = c;
   }
   cut[size_t(nsh)] = nchunks;
-  // Tail split (dynamic sweeps): the last PE_TAIL_FRAC of every shard's light
-  // items are cut into PE_TAIL_SPLIT shorter items, so the round of items
-  // running when the queues drain is short (the drain is ≈ one item long).
-  double tail_frac = k.order == 3 ? 0.3 : 0.0;
+  // Tail split (dynamic sweeps, opt-in): the last PE_TAIL_FRAC of every
+  // shard's light items are cut into PE_TAIL_SPLIT shorter items, so the round
+  // of items running when the queues drain is short.  Off by default since the
+  // per-XCD queues: at one placement every extra item costs more than the
+  // shorter drain saves (8192², 18 rows: 545.5 µs per iteration unsplit vs
+  // 550.6 / 552.1 / 556.1 with 5 / 10 / 30 % split; 2 ranks 297.8 vs 307.5 —
+  // profiles/r2_layout.txt).
+  double tail_frac = 0.0;
   int tail_split = 2;
   if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
   if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));

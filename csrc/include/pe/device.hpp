@@ -124,6 +124,10 @@ class DeviceSolver {
   // Switch the convergence test on / off (drops cached graphs): the bench
   // times fixed-work steps, then solves to convergence on the same solver.
   void set_check_tol(bool on);
+  // Tuning probe: re-lay out the work items for `ti` rows per item, re-reading
+  // the PE_* layout knobs (same allocation, so configurations compare at one
+  // memory placement).  Drops cached graphs.
+  void relayout(int ti);
   double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
   void synchronize();
 
@@ -165,6 +169,10 @@ class DeviceSolver {
   double construct_seconds() const { return ctor_s_; }           // wall time of the constructor
   double exchange_us() const { return exchange_us_; }            // measured halo exchange (multi-rank)
   const std::vector<float>& ti_tuning_ms() const { return ti_ms_; }  // per candidate (8, 10, 14, 18 rows)
+  const std::vector<int>& ti_tuning_rows() const { return ti_rows_; }  // the candidates
+  // static layout: {most loaded wave, mean wave load, max items on a wave}
+  // in row-step cost units (0s for a dynamic layout)
+  std::vector<double> layout_load() const { return {lay_max_, lay_mean_, double(lay_items_)}; }
   hipStream_t stream() const { return stream_; }
 
   // Checkpoint / resume of the full device state of this rank (raw fields,
@@ -281,6 +289,9 @@ class DeviceSolver {
   int placement_best_ = 0;
   bool tune_ti_ = false;          // rows per item chosen by timing candidate sweeps
   std::vector<float> ti_ms_;      // their per-sweep times
+  std::vector<int> ti_rows_;      // the candidates timed
+  double lay_max_ = 0, lay_mean_ = 0;  // static layout: heaviest / mean wave load (row steps)
+  int lay_items_ = 0;                  // static layout: most items on one wave
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;
   std::unique_ptr<dev::ResParams> rp_;
