@@ -501,8 +501,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 // one contiguous 2-row message per x-neighbour) whose per-iteration sums run
 // inside the sweep over the P2P transport: the sweep stores its edge rows
 // straight into the neighbours' fine-grained receive buffers, the sum's flags
-// tell the neighbours they have arrived, and a small import kernel moves them
-// into the halo rows — no exchange launch, no RCCL call, and the iteration
+// tell the neighbours they have arrived, and the next sweep reads them from
+// there (no import copy) — no exchange launch, no RCCL call, and the iteration
 // becomes graph-capturable.  Every input of the decision is global (grid,
 // process grid, environment, transport type), so every rank reaches
 // map_peer_buffers (collective) or none does.  PE_HALO=exchange opts out.
@@ -1298,14 +1298,22 @@ std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
 }
 
 void DeviceSolver::enqueue_exchange(int buf, bool after_sweep) {
-  if (push_ && after_sweep) {
-    dev::launch_halo_import(*kp_, buf, stream_);
-    return;
-  }
+  // halo push: the sweep that wrote `buf` has pushed its edge rows into the
+  // neighbours' receive buffers, from which the next sweep reads them
+  if (push_ && after_sweep) return;
   for (const HaloPhase& ph : halo_phases(buf)) {
     comm_->exchange(ph.ex, stream_);
     if (ph.unpack) dev::launch_unpack(*kp_, buf, stream_);
   }
+  // initial state through the comm: its halo rows into the receive buffer
+  if (push_) dev::launch_halo_seed(*kp_, buf, stream_);
+}
+
+// halo push: x's halo rows ← the receive buffers (checkpoint, read-back)
+void DeviceSolver::import_halos() {
+  if (!push_) return;
+  for (int b = 0; b < 2; ++b) dev::launch_halo_import(*kp_, b, stream_);
+  PE_HIP_CHECK(hipGetLastError());
 }
 
 double* DeviceSolver::red_F_dev() { return st_->red_F; }
@@ -1551,6 +1559,7 @@ void ck_io(FILE* f, void* host, size_t n, bool write, const std::string& path) {
 
 void DeviceSolver::save_checkpoint(const std::string& path) {
   Range range("pe.checkpoint");
+  import_halos();  // whole x planes (the halo push keeps halo rows in the receive buffers)
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
   std::vector<std::pair<void*, size_t>> bufs;
   if (fused_) {
@@ -1633,6 +1642,9 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
   std::fclose(f);
   par_ = h.par;
   PE_HIP_CHECK(hipMemsetAsync(&st_->sig, 0, sizeof(st_->sig), stream_));  // overlap targets restart
+  // halo push: the next sweep (parity par_) reads x[par_ ^ 1]'s halo rows
+  // from the receive buffer
+  if (push_ && fused_) dev::launch_halo_seed(*kp_, par_ ^ 1, stream_);
   ov_epoch_ = 0;
 }
 
@@ -1907,6 +1919,7 @@ int64_t DeviceSolver::field_cols() const { return fused_ ? plane_ : blk_.pitch; 
 void DeviceSolver::copy_field(int which, double* host) {
   const KParams& k = *kp_;
   if (fused_) {
+    import_halos();
     // rows -1..nx+2 of one plane, columns -1.. (plane width)
     const double* base = which == 0 ? k.x[0] : which == 1 ? k.w : which == 2 ? k.x[0] + k.poff
                          : which == 3 ? k.x[1] + k.poff : k.x[1];

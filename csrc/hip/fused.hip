@@ -419,6 +419,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   double* __restrict__ Ym = k.x[par] - 1;
   double* __restrict__ Wm = k.w - 1;
   const int64_t pitch = k.pitch, poff = k.poff, wp = k.wpitch;
+  // halo push: the receive buffer of the parity this sweep reads ([side][2 rows])
+  const double* hrd = PUSH ? k.hrecv + int64_t(par ^ 1) * 4 * pitch : nullptr;
   const int nx = int(k.nx), ny = int(k.ny);
   const int lane = threadIdx.x & 63;
   double sg = 0.0, sd = 0.0, se = 0.0, sps = 0.0, szz = 0.0, szp = 0.0, spp = 0.0;
@@ -730,18 +732,33 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       }
     };
 
+    // x row t at element offset o.  Under the halo push the slab's halo rows
+    // (-1, 0 from LEFT, nx+1, nx+2 from RIGHT) are read straight from the
+    // receive buffer the neighbours pushed them into during the previous
+    // sweep (system-scope loads: written over xGMI, never through this GPU's
+    // caches; delivered before the cross-rank-sum flags that sweep waited
+    // for) — no import kernel between the sweeps.  Row tests are uniform.
+    auto ldx = [&](int t, unsigned o) -> double2 {
+      if constexpr (PUSH) {
+        if ((t < 1 && k.has[LEFT]) || (t > nx && k.has[RIGHT])) {
+          const double* h = hrd + int64_t(t < 1 ? t + 1 : t - nx + 1) * pitch + o;
+          return dd(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                    __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+        }
+      }
+      return ld2(Xm + int64_t(t) * pitch + o);
+    };
     // prologue: p_k on rows ib-2, ib-1; x rows ib .. ib+PF-1 and w rows
     // ib-2 .. ib-3+PF queued
-    const double* xb = Xm + int64_t(ib - 2) * pitch;
-    const double2 rA = ld2(xb + off), pA = ld2(xb + poff + off);
-    double2 rin1 = ld2(xb + pitch + off);  // r_{k-1}(i+1) at step i
-    const double2 pB = ld2(xb + pitch + poff + off);
+    const double2 rA = ldx(ib - 2, off), pA = ldx(ib - 2, poff + off);
+    double2 rin1 = ldx(ib - 1, off);  // r_{k-1}(i+1) at step i
+    const double2 pB = ldx(ib - 1, poff + off);
     double2 rq[PF], pq[PF], wq[PF];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
-      const double* xr = Xm + int64_t(min(ib + q, ie + 2)) * pitch;
-      rq[q] = ld2(xr + off);
-      pq[q] = ld2(xr + poff + off);
+      const int t = min(ib + q, ie + 2);
+      rq[q] = ldx(t, off);
+      pq[q] = ldx(t, poff + off);
       if constexpr (WM == 2) wq[q] = (ib - 2 + q >= ib) ? ldw<NT>(Wm + int64_t(ib - 2 + q) * wp + off) : dd(0.0, 0.0);
       else wq[q] = dd(0.0, 0.0);
     }
@@ -810,9 +827,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
         const int sl1 = sl == 2 ? 0 : sl + 1, sl2 = sl == 0 ? 2 : sl - 1;  // ring slots of rows i+1, i+2
         const double2 rQ0 = RQ[c], pQ0 = PQ[c], wQ0 = WQ[a];
         {  // prefetch x row i+6 and w row i+4 into the slots just consumed
-          const double* xn = Xm + int64_t(min(i + 2 + PF, ie + 2)) * pitch;
-          RQ[c] = ld2(xn + off);
-          PQ[c] = ld2(xn + poff + off);
+          const int t = min(i + 2 + PF, ie + 2);
+          RQ[c] = ldx(t, off);
+          PQ[c] = ldx(t, poff + off);
           if constexpr (WM == 2) WQ[a] = ldw<NT>(Wm + int64_t(min(i + PF, ie)) * wp + off);
         }
         // p_k(i+2) = z_{k-1} + β p_{k-1}
@@ -1127,12 +1144,13 @@ __global__ void kUnpack(KParams k, int b) {
 }
 
 // In-sweep halo push, receiving side: rows -1, 0 (from LEFT) and nx+1, nx+2
-// (from RIGHT) of x[b] ← the receive buffer of parity b.  The neighbours'
-// stores reached it before their cross-rank-sum flags, which this rank's
-// preceding reduction waited for; the loads are system-scope (the buffer is
+// (from RIGHT) of x[b] ← the receive buffer of parity b.  The sweeps read the
+// halo rows from the receive buffer themselves (kS, ldx); this copy only makes
+// x[b] whole for a checkpoint or a field read-back.  The neighbours' stores
+// reached the buffer before their cross-rank-sum flags, which this rank's
+// last reduction waited for; the loads are system-scope (the buffer is
 // written over xGMI, never through this GPU's caches).
 __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
-  if (k.st->done) return;
   const int64_t n = 2 * k.pitch;
   double* x = k.x[b] - 1;  // row 0, column -1
   for (int side = 0; side < 2; ++side) {
@@ -1142,6 +1160,23 @@ __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
       dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
+}
+
+// The reverse copy: the receive buffer of parity b ← x[b]'s halo rows, after
+// an exchange through the comm (the initial state) or a checkpoint load, so
+// the next sweep's halo reads find them there.  System-scope stores, as the
+// pushes': the sweep's loads bypass this GPU's caches.
+__global__ __launch_bounds__(256) void kHaloSeed(KParams k, int b) {
+  const int64_t n = 2 * k.pitch;
+  const double* x = k.x[b] - 1;  // row 0, column -1
+  for (int side = 0; side < 2; ++side) {
+    if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
+    double* dst = const_cast<double*>(k.hrecv) + (int64_t(b) * 2 + side) * n;  // this rank's own buffer
+    const double* src = x + (side == 0 ? int64_t(-1) : k.nx + 1) * k.pitch;
+    for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
+      __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 
 // Halo-push set-up self-test (DeviceSolver::setup_halo_push): every rank
@@ -1301,6 +1336,13 @@ void launch_halo_import(const KParams& k, int b, hipStream_t s) {
   const int64_t n = 2 * k.pitch;
   const unsigned g = unsigned(std::min<int64_t>(64, (n + 255) / 256));
   hipLaunchKernelGGL(kHaloImport, dim3(g), dim3(256), 0, s, k, b);
+}
+
+void launch_halo_seed(const KParams& k, int b, hipStream_t s) {
+  if (!k.push || (!k.has[LEFT] && !k.has[RIGHT])) return;
+  const int64_t n = 2 * k.pitch;
+  const unsigned g = unsigned(std::min<int64_t>(64, (n + 255) / 256));
+  hipLaunchKernelGGL(kHaloSeed, dim3(g), dim3(256), 0, s, k, b);
 }
 
 void launch_unpack(const KParams& k, int b, hipStream_t s) {

@@ -132,8 +132,10 @@ struct KParams {
   // LEFT neighbour's receive buffer (hpush_lo[b]) and rows nx-1, nx into the
   // RIGHT neighbour's (hpush_hi[b]) with system-scope write-through stores;
   // the in-sweep cross-rank sum's flags then double as "halo delivered", and
-  // kHaloImport copies this rank's receive buffer hrecv into the halo rows of
-  // x[b] before the next sweep.  hrecv = [parity b][side: 0 rows -1,0 from
+  // the next sweep (PUSH) reads the halo rows of x[b] from this rank's receive
+  // buffer hrecv itself (kHaloImport copies them into x only for checkpoints /
+  // read-back; kHaloSeed fills hrecv from x after an exchange or a resume).
+  // hrecv = [parity b][side: 0 rows -1,0 from
   // LEFT, 1 rows nx+1,nx+2 from RIGHT][2 × pitch], laid out like x rows from
   // column -1.  push = 0: the halo travels through the comm's exchange.
   double* hpush_lo[2];
@@ -216,8 +218,10 @@ void launch_wflush(const KParams& k, hipStream_t s);
 void launch_unpack(const KParams& k, int b, hipStream_t s);
 // In-sweep halo push: copy the receive buffer's rows of parity b (filled by
 // the neighbours' sweeps, delivered once the sweep's cross-rank sum has
-// completed) into x[b]'s halo rows -1, 0 / nx+1, nx+2 (no-op once done).
+// completed) into x[b]'s halo rows -1, 0 / nx+1, nx+2.  The sweeps read them
+// from the buffer directly; this makes x[b] whole for checkpoints / read-back.
 void launch_halo_import(const KParams& k, int b, hipStream_t s);
+void launch_halo_seed(const KParams& k, int b, hipStream_t s);  // receive buffer b <- x[b]'s halo rows
 // Halo-push set-up self-test: write rank-coded values into the neighbours'
 // receive buffers (k.hpush_*), then — after a cross-rank barrier — count in
 // *bad the received values (k.hrecv) that differ from the neighbours' codes

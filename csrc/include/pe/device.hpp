@@ -214,6 +214,7 @@ class DeviceSolver {
   // push: import it); false for the initial state (the comm's exchange).
   void enqueue_exchange(int buf, bool after_sweep = true);
   void setup_halo_push();  // collective: decides push_ identically on every rank
+  void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
   void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
   void enqueue_chunk(int iters, int sample_iters = 0);
   // Sampled phase timing (Timers): hipEvent pairs around the phases of the

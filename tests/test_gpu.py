@@ -377,6 +377,34 @@ def test_halo_push_selftest_failure_falls_back(gpu):
     assert "halo push unavailable" in out.stderr
 
 
+def test_halo_push_checkpoint_resume_bitwise(gpu, tmp_path):
+    """Row slabs with the halo push keep their halo rows in the receive
+    buffers (the sweeps read them there): a checkpoint imports them into x
+    first, a resume seeds the receive buffer from x — the resumed 3-rank job
+    ends bitwise where the uninterrupted one does."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+    ck = str(tmp_path / "ck")
+
+    def run(*extra):
+        outp = str(tmp_path / f"w{len(extra)}.npy")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+               "--quiet", "--decomp", "rows", "--dump", outp, *extra, "400", "600"]
+        out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-3000:]
+        d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert d["halo_push"]
+        return d, np.load(outp)
+
+    full, wf = run("--checkpoint", ck, "--checkpoint-every", "200")
+    assert full["iters"] == 546 and os.path.exists(ck + ".r2")
+    res, wr = run("--resume", ck)
+    assert res["iters"] == full["iters"]
+    assert np.array_equal(wr, wf)
+
+
 @pytest.mark.parametrize("nproc", [2, 4])
 def test_bench_halo_push_graphs(gpu, nproc):
     """bench.py on row slabs over the P2P transport (processes sharing the
