@@ -1263,8 +1263,9 @@ static auto with_kS(const KParams& k, F&& f) {
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
-  // each variant runs on its own resident grid (the deferring one needs
-  // fewer registers: 3 waves/SIMD instead of 2)
+  // each variant runs on its own resident grid (from the occupancy API; both
+  // are 2 workgroups per CU since the band-coefficient LDS ring, 74 KB per
+  // workgroup — the deferring sweep's 212 VGPRs alone would allow 2 as well)
   const int nb = par == 0 ? k.nblocks0 : k.nblocks;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(nb), dim3(TJ), 0, s, k, par);
