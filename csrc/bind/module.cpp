@@ -380,7 +380,7 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("iters"), py::arg("use_graph") = true)
       .def("set_check_tol", &DeviceSolver::set_check_tol, py::arg("on"))
-      .def("relayout", &DeviceSolver::relayout, py::arg("ti"))
+      .def("relayout", &DeviceSolver::relayout, py::arg("ti"), py::arg("order") = -1)
       .def("prepare_graphs",
            [](DeviceSolver& s, int64_t n) {
              py::gil_scoped_release nogil;

@@ -309,17 +309,22 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
   // rows per item and item order first: they select the sweep kernel variant
   // whose occupancy sizes the grid
-  const bool big = double(nx) * double(ny) >= double(1 << 24);
-  // sweeps: 8192² dynamic 18 rows (= 5 unrolled groups of 4 row steps, 3.29 s
-  // vs 3.31-3.74 at 16); smaller blocks static 10 (1600×2400 /
-  // 2400×3200 / 4096² / the 8-rank 8192² block: 3-8 % faster than 8 or 6 rows,
-  // profiles/r2_tune.txt)
-  if (fused_ && ti_env == 0) ti = big ? 18 : 10;
-  // Single-sweep item order: the per-XCD dynamic queue (order 3) when the
-  // block is large (8192²: +8 % — boundary-band strips cost more, a static
-  // deal leaves waves idle), static chunk-major otherwise (small blocks: the
-  // queue's pull latency and the extra reduction launch do not pay).
-  k.order = (fused_ && big) ? 3 : 0;
+  const double npts = double(nx) * double(ny);
+  const bool big = npts >= double(1 << 24), huge = npts > double(1 << 26);
+  // Single-sweep item order and rows per item (profiles/r2_order.txt,
+  // profiles/r2_bench_static.txt; one memory placement per comparison):
+  //  * blocks > 2²⁶ nodes (16384²): the per-XCD dynamic queue, 18 rows —
+  //    with ≈45 items per wave a static layout's per-wave durations drift
+  //    apart (2150 vs 2195 µs per iteration static 24 rows);
+  //  * 2²⁴ .. 2²⁶ (8192², the 2-rank 8192² block): the cost-aware static LPT
+  //    layout, 24 rows, untuned — no item-sum reduction kernel, no queue
+  //    atomics, and with 6-12 items per wave its load is even (8192²: 540-542
+  //    vs 548 µs dynamic; 2-rank block 315-318 vs 333);
+  //  * smaller blocks: static, rows per item tuned below (small blocks: the
+  //    queue's pull latency and the reduction launch never pay — 4-rank block
+  //    155-159 vs 188 µs, 2400×3200 80 vs 109).
+  if (fused_ && ti_env == 0) ti = huge ? 18 : big ? 24 : 10;
+  k.order = (fused_ && huge) ? 3 : 0;
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
   if (!fused_ && k.order > 1) k.order = 0;
   k.ti = (fused_ && ti_env < 0) ? 1 << 20 : ti;  // bands mode: long items → general kernel
@@ -343,12 +348,12 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   wave_cap_ = std::min(wave_cap, wave_cap0);
   wave_caps_[0] = wave_cap;
   wave_caps_[1] = wave_cap0;
-  // Rows per item: fixed (PE_TI, the classic path, big dynamic sweeps), or
-  // tuned below among kTiCands for static single sweeps (the best depends
+  // Rows per item: fixed (PE_TI, the classic path, blocks ≥ 2²⁴ nodes), or
+  // tuned below among kTiCands for smaller static single sweeps (the best depends
   // on the block: 2400×3200 18 rows 76 µs vs 84 at 10; 1600×2400 and the
   // 8-rank 8192² block 10 rows — profiles/r2_mid_tune.txt).
   static constexpr int kTiCands[4] = {8, 10, 14, 18};
-  tune_ti_ = fused_ && ti_env == 0 && k.order == 0 && double(nx) * double(ny) >= double(1 << 20);
+  tune_ti_ = fused_ && ti_env == 0 && k.order == 0 && npts >= double(1 << 20) && !big;
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
   const int ti_min = tune_ti_ ? kTiCands[0] : ti;
   set_items(ti);
@@ -371,11 +376,19 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   build_tables(rows_hi, cols_hi);
   mark("tables");
   setup_halo_push();
-  if (fused_) choose_placement();
-  mark("placement");
+  // The placement search times the item layout the solve will run (after
+  // setup_items): its best class then reaches the early-stop rate (8192²
+  // static layout 0.536-0.545 ms vs 0.564-0.567 for the plain walk), so it
+  // stops after 2-3 tries instead of 8 — construction 0.10-0.14 vs 0.15-0.25 s,
+  // the same iteration speed (profiles/r2_bench_psearch.txt).
+  // PE_PLACEMENT_LISTED=0: search with the plain walk, before the layout.
+  const bool listed_search = !(std::getenv("PE_PLACEMENT_LISTED") && std::atoi(std::getenv("PE_PLACEMENT_LISTED")) == 0);
+  if (fused_ && !listed_search) choose_placement();
   if (comm_->size() > 1 && !push_) measure_exchange();
   setup_items();
   mark("items");
+  if (fused_ && listed_search) choose_placement();
+  mark("placement");
   setup_resident();
   mark("resident");
   if (tune_ti_ && !resident_) {
@@ -581,8 +594,9 @@ void DeviceSolver::setup_halo_push() {
   }
 }
 
-void DeviceSolver::relayout(int ti) {
+void DeviceSolver::relayout(int ti, int order) {
   if (!fused_ || resident_) return;
+  if (order == 0 || order == 3) kp_->order = order;  // static LPT list / dynamic per-XCD queue
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
   for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));
   graphs_.clear();

@@ -127,7 +127,7 @@ class DeviceSolver {
   // Tuning probe: re-lay out the work items for `ti` rows per item, re-reading
   // the PE_* layout knobs (same allocation, so configurations compare at one
   // memory placement).  Drops cached graphs.
-  void relayout(int ti);
+  void relayout(int ti, int order = -1);  // probe: re-lay out the items (ti rows; order 0 / 3, -1 keeps)
   double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
   void synchronize();
 

@@ -3,7 +3,8 @@ re-laid out (DeviceSolver.relayout) for each configuration, then timed.
 
     PROBE_GRID=8192x8192 PROBE_P=1 PROBE_CFGS="18;18 PE_TAIL_SPLIT=3;18 PE_TAIL_FRAC=0.5" python tools/layout_probe.py
 
-Each configuration: "<rows per item> [PE_X=v ...]"; configurations are timed
+Each configuration: "<rows per item>[s|d] [PE_X=v ...]" (s / d: static LPT
+layout / dynamic queue; default: the solver's own); configurations are timed
 in rounds (the list repeated PROBE_ROUNDS times) so drift shows.
 """
 import os
@@ -37,13 +38,14 @@ for r in range(rounds):
         kv = dict(x.split("=") for x in parts[1:])
         saved = {k: os.environ.get(k) for k in kv}
         os.environ.update(kv)
-        s.relayout(int(parts[0]))
+        t = parts[0]
+        s.relayout(int(t.rstrip("sd")), 0 if t.endswith("s") else 3 if t.endswith("d") else -1)
         s.reset()
         s.time_iterations(20, False)
         dt = s.time_iterations(iters, False)
         mx, mean, per = s.layout_load
         lay = f"  wave load max {mx:.0f} / mean {mean:.0f} = {mx / mean:.3f}, <= {per:.0f} items" if mx else ""
-        print(f"  round {r} [{c}]: {dt / iters * 1e6:7.1f} us/iter  items {s.nitems}{lay}", flush=True)
+        print(f"  round {r} [{c}]: {dt / iters * 1e6:7.1f} us/iter  order {s.order}  items {s.nitems}{lay}", flush=True)
         for k, v in saved.items():
             if v is None:
                 os.environ.pop(k, None)
