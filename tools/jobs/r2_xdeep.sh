@@ -1,4 +1,5 @@
 # Deferring sweep with 8 x rows in flight (PE_SKERNEL=3) vs 4 (default): correctness subset, headline bench and the 8-rank block, alternating fresh processes.
+# (experiment build: kS took an x-prefetch-depth template parameter XD and PE_SKERNEL=3 selected XD=8 for WM=0; reverted after this run)
 cd $GRAFT_REPO_ROOT
 PE_SKERNEL=3 timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 200 --timeout-method thread -k "golden_iterations and fused or matches_cpu_oracle or large_golden or item_orders or thin_blocks" 2>&1 | tail -2 || exit 1
 for i in 1 2; do
