@@ -402,6 +402,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // wave means a quarter of the waves runs a 4th item while the rest idle
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
     std::vector<int> cands(kTiCands, kTiCands + 4);
+    // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
+    // at 18, one placement, profiles/r2_ti_big.txt)
+    if (npts >= 12e6) cands.insert(cands.end(), {24, 30});
     {
       const int64_t W = std::max(dev::kWPB, wave_cap_);
       for (int q = 2; q <= 5; ++q)
