@@ -13,7 +13,11 @@ xGMI P2P, and the halo rows — row-slab blocks — pushed by the same sweep int
 the neighbours' receive buffers, or exchanged through RCCL otherwise).  The timed region runs exactly K steps from the start of a fresh
 solve (w⁰ = 0, as the reference) with the convergence test switched off so
 every step does full work; it is bracketed by a barrier + device synchronise
-on both sides and the max over ranks is reported.  `value` = job-wide PCG
+on both sides and the max over ranks is reported (each rank's clock stops at
+its closing device synchronise, before the closing CPU barrier: the ranks are
+coupled every iteration by the in-sweep sums, so the max over ranks is the
+job's time, without the gloo barrier's ~0.1-0.3 ms, which at 8 ranks would be
+≈10 % of a 20-step window).  `value` = job-wide PCG
 iterations/s (the grid is fixed → strong scaling).  Outside the timed region
 the script also runs one complete solve to convergence and reports T_solver,
 its iteration count and the L2 error against the analytic solution.
@@ -120,8 +124,8 @@ def main() -> int:
     solver.run_iterations(a.steps, use_graph)
     solver.synchronize()
     torch.cuda.synchronize()
+    t1 = time.perf_counter()  # this rank's steps are done; the slowest rank is the job's time (max below)
     barrier()
-    t1 = time.perf_counter()
     dt = maxval(t1 - t0)
     st = solver.state()
     valid = int(st["status"]) == 0 and int(st["iter"]) == a.steps
