@@ -29,121 +29,20 @@
 
 #include "../hip/kernels.hpp"
 #include "pe/device.hpp"
+#include "solver_internal.hpp"
 
 namespace pe {
 
 using dev::DevState;
 using dev::KParams;
 
-namespace {
-// Host-side phase ranges for rocprofv3 --marker-trace (no-ops without a tool).
-struct Range {
-  explicit Range(const char* n) { roctxRangePushA(n); }
-  ~Range() { roctxRangePop(); }
-};
-using clk = std::chrono::steady_clock;
-double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
-}  // namespace
+using detail::clk;
+using detail::field_alloc;
+using detail::field_free;
+using detail::field_try_alloc;
+using detail::Range;
+using detail::secs;
 
-// Field allocation.  PE_MALLOC=1 requests physically contiguous memory
-// (hipDeviceMallocContiguous); PE_MALLOC=2 builds the range from
-// PE_VMM_CHUNK_MB-sized physical chunks (default 2) mapped into one virtual
-// range in a shuffled order (virtual memory API) — experiments on the
-// allocation-dependent speed of the streaming sweep (docs/PERFORMANCE.md).
-namespace {
-struct VmmRange {
-  size_t size;
-  std::vector<hipMemGenericAllocationHandle_t> h;
-};
-std::mutex g_vmm_mu;
-std::map<void*, VmmRange> g_vmm;
-
-void* vmm_alloc_shuffled(size_t bytes) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  hipMemAllocationProp prop{};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = dev;
-  size_t gran = 0;
-  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || gran == 0)
-    return nullptr;
-  size_t chunk = size_t(2) << 20;
-  if (const char* e = std::getenv("PE_VMM_CHUNK_MB")) chunk = size_t(std::max(1, std::atoi(e))) << 20;
-  chunk = (chunk + gran - 1) / gran * gran;
-  const size_t n = (bytes + chunk - 1) / chunk, size = n * chunk;
-  void* va = nullptr;
-  if (hipMemAddressReserve(&va, size, chunk, nullptr, 0) != hipSuccess) return nullptr;
-  VmmRange r{size, std::vector<hipMemGenericAllocationHandle_t>(n)};
-  for (size_t i = 0; i < n; ++i)
-    if (hipMemCreate(&r.h[i], chunk, &prop, 0) != hipSuccess) {
-      for (size_t j = 0; j < i; ++j) (void)hipMemRelease(r.h[j]);
-      (void)hipMemAddressFree(va, size);
-      return nullptr;
-    }
-  // chunk i of the range ← physical chunk perm[i] (fixed-seed shuffle)
-  std::vector<size_t> perm(n);
-  for (size_t i = 0; i < n; ++i) perm[i] = i;
-  unsigned long long x = 0x9E3779B97F4A7C15ull;
-  for (size_t i = n; i > 1; --i) {
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    std::swap(perm[i - 1], perm[size_t(x % i)]);
-  }
-  for (size_t i = 0; i < n; ++i)
-    PE_HIP_CHECK(hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, r.h[perm[i]], 0));
-  hipMemAccessDesc acc{};
-  acc.location.type = hipMemLocationTypeDevice;
-  acc.location.id = dev;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  PE_HIP_CHECK(hipMemSetAccess(va, size, &acc, 1));
-  std::lock_guard<std::mutex> g(g_vmm_mu);
-  g_vmm.emplace(va, std::move(r));
-  return va;
-}
-}  // namespace
-
-// mode: 0 hipMalloc, 1 physically contiguous, 2 shuffled physical chunks;
-// PE_MALLOC overrides.  nullptr when the device is out of memory.
-static void* field_try_alloc(size_t bytes, int mode = 0) {
-  void* p = nullptr;
-  if (const char* e = std::getenv("PE_MALLOC")) mode = std::atoi(e);
-  if (mode == 2) {
-    if (void* v = vmm_alloc_shuffled(bytes)) return v;
-    (void)hipGetLastError();
-    mode = 0;  // no virtual memory API: plain allocation
-  }
-  const hipError_t r = mode == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) : hipMalloc(&p, bytes);
-  if (r != hipSuccess) {
-    (void)hipGetLastError();
-    return nullptr;
-  }
-  return p;
-}
-
-static void* field_alloc(size_t bytes, int mode = 0) {
-  void* p = field_try_alloc(bytes, mode);
-  if (!p) PE_HIP_CHECK(hipErrorOutOfMemory);
-  return p;
-}
-
-static void field_free(void* p) {
-  if (!p) return;
-  {
-    std::lock_guard<std::mutex> g(g_vmm_mu);
-    auto it = g_vmm.find(p);
-    if (it != g_vmm.end()) {
-      (void)hipDeviceSynchronize();
-      (void)hipMemUnmap(p, it->second.size);
-      for (auto h : it->second.h) (void)hipMemRelease(h);
-      (void)hipMemAddressFree(p, it->second.size);
-      g_vmm.erase(it);
-      return;
-    }
-  }
-  (void)hipFree(p);
-}
 
 // Can the single-sweep kernel run this block?  It needs the fast arithmetic
 // variant and neighbours at least two nodes deep in every split direction
@@ -648,396 +547,6 @@ void DeviceSolver::measure_exchange() {
   exchange_us_ = us[0];
 }
 
-// Items of `ti` rows: counts and the persistent grids sized for them.
-void DeviceSolver::set_items(int ti) {
-  KParams& k = *kp_;
-  k.ti = ti;
-  k.nitems = int(int64_t(k.nstrips) * ((blk_.nx + ti - 1) / ti));
-  // fewest waves that keep every wave's share of the n items equal
-  auto grid_for = [&](int cap, int n) {
-    const int per = (n + cap - 1) / cap;
-    const int waves = (n + per - 1) / per;
-    return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
-  };
-  k.nblocks = grid_for(wave_caps_[0], k.nitems);
-  k.nblocks0 = grid_for(wave_caps_[1], k.nitems);
-  k.nslots = k.nitems;
-  static_waves_ = 0;
-}
-
-// Halo/interior overlap (multi-rank single-sweep).  The sweep walks an item
-// list in which, per XCD shard, the boundary items (outputs sent to a
-// neighbour: first / last two owned rows and columns) come first; each bumps
-// st->sig when stored.  A one-wave kernel on a high-priority halo stream waits
-// for the count, then the exchange runs there while the interior items are
-// still being computed.  The sweep keeps its full persistent grid minus
-// `PE_OV_RESERVE` blocks (default 8) left free for the wait / exchange /
-// unpack kernels.  PE_OVERLAP=0 disables.
-//
-// Every dynamic (order 3) sweep walks such lists, overlap or not.  Item cost
-// estimate (from stamps of the sweep, tools/stamp_probe.py): a row of a
-// strip that contains boundary-band nodes (coefficients evaluated from the
-// chord tables) costs ≈ kGenCost plain rows; an item's rows are its own plus
-// the 4 halo rows it re-reads.  Shards are contiguous chunk ranges of equal
-// estimated cost (consecutive chunks stay on one XCD), and each shard lists
-// its boundary items (overlap) first, then its heavy items in decreasing
-// cost, then the rest chunk-major: the sweep's tail is then made of light
-// items, and waves steal from other shards once their own is empty.
-void DeviceSolver::setup_items() {
-  KParams& k = *kp_;
-  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
-  // Overlap only pays when the exchange costs more than what the overlap
-  // itself costs the sweep (boundary-first item order, blocks kept free for
-  // the halo stream: +9-11 µs per iteration on 2-8 ranks with a zero-latency
-  // transport, profiles/r1_overlap_probe_device_decomp.txt).  Auto: measure
-  // the real exchange here (max over ranks, so every rank decides the same)
-  // and overlap when it exceeds PE_OVERLAP_MIN_US (default 12).
-  // PE_OVERLAP=1 / 0 forces it on / off.
-  const char* e = std::getenv("PE_OVERLAP");
-  overlap_ = false;
-  if (fused_ && comm_->size() > 1 && nb && !push_) {
-    if (e) {
-      overlap_ = std::atoi(e) != 0;
-    } else {
-      double min_us = 12.0;
-      if (const char* m = std::getenv("PE_OVERLAP_MIN_US")) min_us = std::atof(m);
-      overlap_ = exchange_us_ > min_us;
-    }
-  }
-  // Lists: dynamic sweeps (order 3), static chunk-major sweeps (order 0:
-  // heavy items split, below) and the overlap; orders 1 / 2 are plain
-  // tuning walks.
-  if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
-  if (ilist_) {  // re-laid out (rows-per-item tuning)
-    PE_HIP_CHECK(hipFree(ilist_));
-    ilist_ = nullptr;
-  }
-  if (overlap_) {
-    ov_reserve_ = 8;
-    // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
-    // order (no boundary-first list)
-    if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
-    if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
-  }
-  const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - (overlap_ ? ov_reserve_ : 0));
-  const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
-  const int nchunks = int((blk_.nx + k.ti - 1) / k.ti);
-  double gen_cost = 3.0;
-  if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
-  const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
-  const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
-  // per-item cost: rows ib-2 .. ie+2, band rows weighted
-  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
-  // Does local row q have a boundary-band node in strip s's 128 loaded
-  // columns?  (The kernel's has_gen on the same row-class table.)
-  auto row_gen = [&](int64_t q, int s) {
-    const int64_t J = -1 + int64_t(s) * dev::kFSW;
-    const int64_t t = q + 1;  // table index of local row q
-    if (t < 0 || t >= rows_tab) return false;
-    const int* r = &rowcls_host_[size_t(t) * 4];
-    const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
-    return lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
-  };
-  auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
-    double c = 0.0;
-    for (int64_t q = ib - 2; q <= ie + 2; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
-    return c;
-  };
-  auto rows_band = [&](int64_t ib, int64_t ie, int s) {
-    for (int64_t q = ib - 2; q <= ie + 2; ++q)
-      if (row_gen(q, s)) return true;
-    return false;
-  };
-  auto item_cost = [&](int ch, int s) {
-    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-    return rows_cost(ib, ie, s);
-  };
-  // {first row | band flag, strip | rows << 20}; the band flag selects the
-  // kernel's coefficient path (rows ib-2 .. ie+2 include a boundary-band row)
-  auto entry = [&](int64_t ib, int64_t rows, int s) {
-    const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
-    return int2{int(ib) | flag, s | int(rows << 20)};
-  };
-  // outputs a neighbour needs: first in the layout under the overlap (they
-  // feed the exchange) and under the halo push (their xGMI stores then
-  // overlap the rest of the sweep instead of ending it)
-  auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
-    const int64_t J = -1 + int64_t(s) * dev::kFSW;
-    const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
-    return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
-           ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
-            (blk_.has(UP) && jhi >= blk_.ny - 1));
-  };
-
-  if (k.order == 0) {
-    // ---- Static sweeps: a longest-processing-time-first layout ----
-    // Every wave walks list positions w, w + W, w + 2W, … (W = the grid's
-    // waves), so the host decides who does what: items are cut where one
-    // would exceed a wave's fair share (band items cost ≈2-3× a plain one;
-    // on small blocks, where each wave gets about one item, the band items
-    // alone were the sweep's tail — profiles/r2_small_before.txt), then
-    // assigned heaviest first to the least-loaded wave, and a wave's k-th
-    // item goes to position k·W + w (empty entries fill the gaps).  Equal
-    // costs keep chunk-major order, so each round of positions still covers
-    // a compact window of rows.  Overlap: boundary items take the first
-    // positions (they run in the first round).
-    struct Piece {
-      int64_t ib, rows;
-      int s;
-      double cost;
-      bool bnd;
-    };
-    const double overhead = 3.0;  // per-item prologue / epilogue, in row steps (stamps)
-    int waves_avail = std::max(dev::kWPB, wave_cap_ - (overlap_ ? ov_reserve_ * dev::kWPB : 0));
-    if (const char* w = std::getenv("PE_WAVES")) waves_avail = std::max(dev::kWPB, std::atoi(w));
-    double total = 0.0;
-    for (int id = 0; id < k.nitems; ++id) total += item_cost(id / k.nstrips, id % k.nstrips) + overhead;
-    // cut only when there are fewer items than waves (small blocks): with
-    // more items than waves the layout balances them, and every cut re-reads
-    // 4 more halo rows (2048²: 96 vs 91 µs per iteration with cuts)
-    const int W0 = std::max(1, std::min(waves_avail, k.nitems));
-    const double share = k.nitems >= waves_avail ? 1e300 : std::max(total / W0, (double(k.ti + 4) + overhead) * 1.15);
-    std::vector<Piece> pcs;
-    for (int ch = 0; ch < nchunks; ++ch)
-      for (int s = 0; s < k.nstrips; ++s) {
-        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-        const int64_t n = ie - ib + 1;
-        const bool bnd = is_boundary(ib, ie, s);
-        int parts = 1;
-        if (split_heavy && !bnd) {
-          for (; 2 * (parts + 1) <= n; ++parts) {  // pieces of >= 2 rows
-            double worst = 0.0;
-            for (int q = 0; q < parts; ++q)
-              worst = std::max(worst, rows_cost(ib + n * q / parts, ib + n * (q + 1) / parts - 1, s) + overhead);
-            if (worst <= share) break;
-          }
-        }
-        for (int q = 0; q < parts; ++q) {
-          const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
-          pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
-        }
-      }
-    const int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
-    std::vector<std::vector<int>> per(static_cast<size_t>(W));
-    std::vector<double> load(static_cast<size_t>(W), 0.0);
-    std::vector<int> order;
-    int nbnd = 0;
-    for (int i = 0; i < int(pcs.size()); ++i) {
-      if (pcs[size_t(i)].bnd) {  // boundary pieces: positions 0, 1, … in order
-        per[size_t(nbnd % W)].push_back(i);
-        load[size_t(nbnd % W)] += pcs[size_t(i)].cost;
-        ++nbnd;
-      } else {
-        order.push_back(i);
-      }
-    }
-    std::stable_sort(order.begin(), order.end(),
-                     [&](int a, int b) { return pcs[size_t(a)].cost > pcs[size_t(b)].cost; });
-    using LW = std::pair<double, int>;
-    std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
-    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
-    for (int i : order) {
-      const LW t = heap.top();
-      heap.pop();
-      per[size_t(t.second)].push_back(i);
-      heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
-    }
-    size_t rounds = 0;
-    for (const auto& v : per) rounds = std::max(rounds, v.size());
-    lay_max_ = 0.0;
-    lay_mean_ = 0.0;
-    for (int w = 0; w < W; ++w) {
-      double l = 0.0;
-      for (int i : per[size_t(w)]) l += pcs[size_t(i)].cost;
-      lay_max_ = std::max(lay_max_, l);
-      lay_mean_ += l / W;
-    }
-    lay_items_ = int(rounds);
-    std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)
-    for (int w = 0; w < W; ++w)
-      for (size_t r = 0; r < per[size_t(w)].size(); ++r) {
-        const Piece& p = pcs[size_t(per[size_t(w)][r])];
-        all[r * size_t(W) + size_t(w)] = entry(p.ib, p.rows, p.s);
-      }
-    static_waves_ = W;
-    nslot_cap_ = std::max<int>(nslot_cap_, int(all.size()));
-    ov_nb_ = nbnd;
-    ov_lnsh_ = 1;
-    ov_lbase_[0] = 0;
-    for (int x = 1; x <= 8; ++x) ov_lbase_[x] = int(all.size());
-    ov_lnb_[0] = nbnd;
-    for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
-    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
-    const auto tc = clk::now();
-    upload(ilist_, all.data(), sizeof(int2) * all.size());
-    copy_setup_s_ += secs(tc, clk::now());
-    k.ilist = ilist_;
-    k.lnsh = 1;
-    k.lwaves = W;
-    k.nslots = int(all.size());
-    for (int x = 0; x <= 8; ++x) k.lbase[x] = ov_lbase_[x];
-    for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
-    // static list walk: the grid is the one the list was laid out for (plus
-    // the blocks the overlap keeps free for the halo stream)
-    k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
-    if (overlap_) create_halo_stream();
-    return;
-  }
-  lay_max_ = lay_mean_ = 0.0;
-  lay_items_ = 0;
-  std::vector<double> cost(size_t(k.nitems));
-  std::vector<double> ccost(size_t(nchunks) + 1, 0.0);  // prefix sums per chunk
-  for (int ch = 0; ch < nchunks; ++ch) {
-    double cc = 0.0;
-    for (int s = 0; s < k.nstrips; ++s) cc += cost[size_t(ch) * k.nstrips + s] = item_cost(ch, s);
-    ccost[size_t(ch) + 1] = ccost[size_t(ch)] + cc;
-  }
-  const double light = double(k.ti + 4);
-  std::vector<int> cut(size_t(nsh) + 1, 0);
-  for (int x = 1; x < nsh; ++x) {
-    const double target = ccost.back() * x / nsh;
-    int c = cut[size_t(x) - 1];
-    while (c < nchunks && ccost[size_t(c) + 1] <= target) ++c;
-    cut[size_t(x)] = c;
-  }
-  cut[size_t(nsh)] = nchunks;
-  // Tail split (dynamic sweeps, opt-in): the last PE_TAIL_FRAC of every
-  // shard's light items are cut into PE_TAIL_SPLIT shorter items, so the round
-  // of items running when the queues drain is short.  Off by default since the
-  // per-XCD queues: at one placement every extra item costs more than the
-  // shorter drain saves (8192², 18 rows: 545.5 µs per iteration unsplit vs
-  // 550.6 / 552.1 / 556.1 with 5 / 10 / 30 % split; 2 ranks 297.8 vs 307.5 —
-  // profiles/r2_layout.txt).
-  double tail_frac = 0.0;
-  int tail_split = 2;
-  if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
-  if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));
-  std::vector<int2> all;
-  ov_nb_ = 0;
-  ov_lnsh_ = nsh;
-  for (int x = 0; x < nsh; ++x) {
-    std::vector<int> b, heavy, in;
-    for (int ch = cut[size_t(x)]; ch < cut[size_t(x) + 1]; ++ch)
-      for (int s = 0; s < k.nstrips; ++s) {
-        const int id = ch * k.nstrips + s;
-        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-        if (is_boundary(ib, ie, s)) b.push_back(id);
-        else if (sort_heavy && cost[size_t(id)] > 1.25 * light) heavy.push_back(id);
-        else in.push_back(id);
-      }
-    std::stable_sort(heavy.begin(), heavy.end(), [&](int a, int c) { return cost[size_t(a)] > cost[size_t(c)]; });
-    ov_lbase_[x] = int(all.size());
-    ov_lnb_[x] = int(b.size());
-    ov_nb_ += int(b.size());
-    const size_t nsplit = size_t(tail_frac * double(in.size()) + 0.5);
-    auto push = [&](int id, int parts) {
-      const int ch = id / k.nstrips, s = id % k.nstrips;
-      const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-      const int64_t n = ie - ib + 1;
-      parts = int(std::min<int64_t>(parts, n));
-      for (int q = 0; q < parts; ++q) {
-        const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
-        all.push_back(entry(a0, a1 - a0, s));
-      }
-    };
-    for (int id : b) push(id, 1);
-    for (int id : heavy) push(id, 1);
-    for (size_t i = 0; i < in.size(); ++i) push(in[i], i + nsplit >= in.size() ? tail_split : 1);
-  }
-  ov_lbase_[nsh] = int(all.size());
-  if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
-  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
-  const auto tc = clk::now();
-  upload(ilist_, all.data(), sizeof(int2) * all.size());
-  copy_setup_s_ += secs(tc, clk::now());
-  // Every dynamic sweep walks the list (the plain one counts no boundary
-  // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).
-  k.ilist = ilist_;
-  k.lnsh = nsh;
-  k.nslots = int(all.size());
-  for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
-  for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
-  if (overlap_) create_halo_stream();
-}
-
-// LDS-resident geometry: tiles of one 124-column strip × R rows (the
-// streaming sweep's strips), one workgroup each, at most one per CU, R ≥ 8
-// where the block allows and ≤ kResMaxRows; the band-coefficient table is
-// sized from the host row classes (the kernel's exact band test).
-void DeviceSolver::setup_resident() {
-  KParams& k = *kp_;
-  resident_ = false;
-  const char* e = std::getenv("PE_RESIDENT");
-  if (e && std::atoi(e) == 0) return;
-  if (!fused_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0) return;
-  const int nx = int(blk_.nx);
-  int cus = 256;
-  {
-    int dev = 0;
-    PE_HIP_CHECK(hipGetDevice(&dev));
-    PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  const int nstrips = k.nstrips;
-  if (nstrips > cus) return;
-  const int ntr = std::max(1, std::min(cus / nstrips, nx / 8));
-  if (nx < 2 * ntr) return;
-  std::vector<int> rs(size_t(ntr) + 1);
-  for (int t = 0; t <= ntr; ++t) rs[size_t(t)] = 1 + int(int64_t(t) * nx / ntr);
-  int rcap = 0;
-  for (int t = 0; t < ntr; ++t) rcap = std::max(rcap, rs[size_t(t) + 1] - rs[size_t(t)]);
-  if (rcap > dev::kResMaxRows) return;
-  // band nodes per tile region (rows I0-2 .. I0+R+1, columns J0-2 .. J0+125)
-  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
-  int nb_max = 0;
-  for (int t = 0; t < ntr; ++t)
-    for (int sx = 0; sx < nstrips; ++sx) {
-      int nb = 0;
-      const int J0 = 1 + dev::kFSW * sx;
-      for (int q = rs[size_t(t)] - 2; q < rs[size_t(t) + 1] + 2; ++q) {
-        if (q + 1 < 0 || q + 1 >= rows_tab) continue;
-        const int* r = &rowcls_host_[size_t(q + 1) * 4];
-        for (int c = J0 - 2; c < J0 + 126; ++c)
-          if (c >= r[2] && c <= r[3] && !(c >= r[0] && c <= r[1])) ++nb;
-      }
-      nb_max = std::max(nb_max, nb);
-    }
-  const int nbcap = nb_max + 8;
-  const size_t lds = dev::resident_lds_bytes(rcap, nbcap);
-  if (lds > 163840) return;
-  const int per_cu = dev::resident_max_blocks_per_cu(lds);
-  const int nwg = ntr * nstrips;
-  if (per_cu < 1 || nwg > per_cu * cus) return;
-  rp_ = std::make_unique<dev::ResParams>();
-  dev::ResParams& r = *rp_;
-  std::memset(&r, 0, sizeof(r));
-  r.nstrips = nstrips;
-  r.ntr = ntr;
-  r.nwg = nwg;
-  r.rcap = rcap;
-  r.nbcap = nbcap;
-  r.lds_bytes = unsigned(lds);
-  r.timeout_ticks = 200000000LL;  // 2 s per barrier wait
-  if (const char* t = std::getenv("PE_RES_TIMEOUT_S")) r.timeout_ticks = (long long)(std::atof(t) * 1e8);
-  PE_HIP_CHECK(hipMalloc(&res_rowstart_, sizeof(int) * rs.size()));
-  upload(res_rowstart_, rs.data(), sizeof(int) * rs.size());
-  const size_t nedge = size_t(2) * size_t(nwg) * dev::kResEdge, npart = size_t(2) * size_t(nwg) * 8;
-  PE_HIP_CHECK(hipMalloc(&res_buf_, sizeof(double) * (nedge + npart)));
-  // stream-ordered: a null-stream operation would create that stream's
-  // hardware queue (≈10 ms inside T_solver in a fresh process, profiles/r2_ctor_phases.txt)
-  PE_HIP_CHECK(hipMemsetAsync(res_buf_, 0, sizeof(double) * (nedge + npart), stream_));
-  PE_HIP_CHECK(hipMalloc(&res_ctr_, sizeof(unsigned) * 8 * 32));
-  if (const char* t = std::getenv("PE_RES_STAMPS"); t && std::atoi(t) == 1) {
-    nstamps_ = size_t(nwg) * dev::kResStampIters * 8;
-    PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
-    PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
-    r.stamps = stamps_;
-  }
-  r.rowstart = res_rowstart_;
-  r.edges = res_buf_;
-  r.partials = res_buf_ + nedge;
-  r.ctr = res_ctr_;
-  resident_ = true;
-}
 
 void DeviceSolver::create_halo_stream() {
   if (hs_) return;
@@ -1047,158 +556,6 @@ void DeviceSolver::create_halo_stream() {
   PE_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
 }
 
-// Memory-placement autotune (single-sweep, large blocks).  The same sweep
-// runs at two distinct speeds depending on which physical memory its arrays
-// land in (8192²: ≈1380 vs ≈1510 it/s; stable per allocation; consecutive
-// allocations come in slow and fast runs of several GB; no dependence on
-// row padding, virtual address or TLB misses — the slow placements show ~1.7×
-// the DRAM credit stalls; docs/PERFORMANCE.md).  Try up to
-// PE_PLACEMENT_TRIES (default 8) candidate allocations, each after a
-// PE_PLACEMENT_SKIP_GB (default 8) spacer so it lands in another region;
-// time a few local sweeps on real data (no communication) and keep the
-// fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
-void DeviceSolver::choose_placement() {
-  Range range("pe.placement_search");
-  struct Clock {
-    double& out;
-    clk::time_point t0 = clk::now();
-    ~Clock() { out = secs(t0, clk::now()); }
-  } clock{placement_s_};
-  const double pts = double(blk_.nx) * double(blk_.ny);
-  // Only large blocks: the two-speed placement was measured at 8192² (≈9 %);
-  // at 2400×3200 / 4096² the candidates differ by ≤ 3-7 % while the spacer
-  // allocations cost 0.02-6 s of construction (T_solver) depending on the
-  // allocator state (profiles/r2_ctor_probe.txt).
-  int tries = pts >= 24.0e6 ? 8 : 1;
-  if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
-  double skip_gb = 8.0;
-  if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
-  double fast_tbs = 4.9, max_s = 0.3;
-  if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
-  if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
-  if (tries <= 1) return;
-  // spacers are transient; never let the search take more than 40 % of the
-  // free memory (several solvers may share the device)
-  {
-    size_t free_b = 0, total_b = 0;
-    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
-      const double per_try = skip_gb * double(1ull << 30) + double(sizeof(double) * (2 * xsize_ + wsize_));
-      tries = std::min<int>(tries, std::max(1, int(0.4 * double(free_b) / per_try)));
-    }
-  }
-  if (tries <= 1) return;
-  if (const char* e = std::getenv("PE_PLACEMENT"); e && std::string(e) == "carve") {
-    carve_placement();
-    return;
-  }
-  struct Cand {
-    double *x0, *x1, *w;
-    float ms;
-  };
-  std::vector<Cand> c;
-  std::vector<void*> spacers;
-  c.push_back(Cand{fields_, xalt_, walt_, 0.f});
-  for (int t = 0; t < tries; ++t) {
-    if (t > 0) {
-      void* sp = nullptr;
-      if (skip_gb > 0 && hipMalloc(&sp, size_t(skip_gb * double(1ull << 30))) != hipSuccess) break;
-      if (sp) spacers.push_back(sp);
-      void* a = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
-      if (!a) break;
-      void* b = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
-      if (!b) {
-        field_free(a);
-        break;
-      }
-      void* w = field_try_alloc(sizeof(double) * wsize_, alloc_mode_);
-      if (!w) {
-        field_free(a);
-        field_free(b);
-        break;
-      }
-      c.push_back(Cand{static_cast<double*>(a), static_cast<double*>(b), static_cast<double*>(w), 0.f});
-    }
-    set_fused_fields(c[t].x0, c[t].x1, c[t].w);
-    enqueue_init();
-    dev::launch_S(*kp_, 1, stream_);  // S_0 on real data (local sums only)
-    for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-    for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-    PE_HIP_CHECK(hipEventSynchronize(t1_));
-    PE_HIP_CHECK(hipEventElapsedTime(&c[t].ms, t0_, t1_));
-    // The placements fall into classes (8192²: 0.541-0.547, 0.556-0.562,
-    // 0.59-0.61 and 0.62-0.65 ms per sweep; the bench follows them: 1792 vs
-    // 1745 it/s for the first two, profiles/r2_bench_launch.txt).  A try costs
-    // ≈6 ms (spacer, allocation, 9 sweeps), the best class saves ≈3 % of a
-    // 3.3 s solve: keep the best of all tries, stopping early only at the
-    // best class — the sweep's average 40 B/node streamed at >=
-    // PE_PLACEMENT_FAST_TBS (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
-    // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
-    // 0.56-0.60 ms placements when better ones were a try or two further.)
-    const double tbs = 40.0 * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
-    if (tbs >= fast_tbs) break;
-    // spacer allocations are cheap on fresh memory but can take seconds
-    // when the allocator must clear reused memory (profiles/r2_ctor_probe.txt):
-    // the search is capped at PE_PLACEMENT_MAX_S (0.3 s) of wall time
-    if (secs(clock.t0, clk::now()) > max_s) break;
-  }
-  (void)hipGetLastError();  // clear a failed search allocation
-  size_t best = 0;
-  for (size_t i = 1; i < c.size(); ++i)
-    if (c[i].ms < c[best].ms) best = i;
-  for (size_t i = 0; i < c.size(); ++i)
-    if (i != best) {
-      field_free(c[i].x0);
-      field_free(c[i].x1);
-      field_free(c[i].w);
-    }
-  for (void* sp : spacers) PE_HIP_CHECK(hipFree(sp));
-  set_fused_fields(c[best].x0, c[best].x1, c[best].w);
-  placement_best_ = int(best);
-  placement_ms_.clear();
-  for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
-}
-
-// Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE
-// allocation at x0 = base, x1 = base + X + d, w = base + 2X + 2d for a set of
-// offsets d, each timed like a search candidate — does the sweep's speed
-// depend on the arrays' relative offsets within the same physical memory?
-void DeviceSolver::carve_placement() {
-  static const size_t kD[] = {0, 4096, 65536, 262144, 1 << 20, 2 << 20, 3 << 20, 5 << 20, 7 << 20, 11 << 20, 13 << 20};
-  const size_t X = sizeof(double) * size_t(xsize_), W = sizeof(double) * size_t(wsize_);
-  const size_t dmax = size_t(16) << 20;
-  char* base = nullptr;
-  PE_HIP_CHECK(hipMalloc(&base, 2 * X + W + 2 * dmax + 4096));
-  double *o0 = fields_, *o1 = xalt_, *ow = walt_;
-  placement_ms_.clear();
-  float best = 0.f;
-  size_t bi = 0;
-  for (size_t i = 0; i < sizeof(kD) / sizeof(kD[0]); ++i) {
-    const size_t d = kD[i];
-    set_fused_fields(reinterpret_cast<double*>(base), reinterpret_cast<double*>(base + X + d),
-                     reinterpret_cast<double*>(base + 2 * X + 2 * d));
-    enqueue_init();
-    dev::launch_S(*kp_, 1, stream_);
-    for (int it = 0; it < 2; ++it) dev::launch_S(*kp_, it & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-    for (int it = 0; it < 6; ++it) dev::launch_S(*kp_, it & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-    PE_HIP_CHECK(hipEventSynchronize(t1_));
-    float ms = 0.f;
-    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-    placement_ms_.push_back(ms / 6.0f);
-    if (i == 0 || ms < best) {
-      best = ms;
-      bi = i;
-    }
-  }
-  // keep the separate allocations of the constructor (the carve block is an
-  // experiment); report the best offset's index
-  PE_HIP_CHECK(hipFree(base));
-  set_fused_fields(o0, o1, ow);
-  placement_best_ = int(bi);
-}
 
 DeviceSolver::~DeviceSolver() {
   for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
@@ -1558,112 +915,6 @@ void DeviceSolver::prepare_graphs(int64_t iters) {
   // the capture enqueued nothing: the stream state is unchanged
 }
 
-// ---------------------------------------------------------------------------
-// Checkpoint / resume.  File = header + DevState + field buffers + halo
-// buffers, raw bytes; the header pins everything the byte layout depends on.
-// ---------------------------------------------------------------------------
-namespace {
-struct CkptHeader {
-  char magic[8];
-  int32_t version, M, N, rank, Px, Py, fused, variant, par;
-  int64_t i0, j0, nx, ny, state_bytes, field_bytes, halo_bytes;
-};
-void ck_io(FILE* f, void* host, size_t n, bool write, const std::string& path) {
-  const size_t got = write ? std::fwrite(host, 1, n, f) : std::fread(host, 1, n, f);
-  if (got != n) throw std::runtime_error("checkpoint " + path + ": short " + (write ? "write" : "read"));
-}
-}  // namespace
-
-void DeviceSolver::save_checkpoint(const std::string& path) {
-  Range range("pe.checkpoint");
-  import_halos();  // whole x planes (the halo push keeps halo rows in the receive buffers)
-  PE_HIP_CHECK(hipStreamSynchronize(stream_));
-  std::vector<std::pair<void*, size_t>> bufs;
-  if (fused_) {
-    bufs = {{fields_, sizeof(double) * xsize_}, {xalt_, sizeof(double) * xsize_}, {walt_, sizeof(double) * wsize_}};
-  } else {
-    bufs = {{fields_, sizeof(double) * 4 * blk_.alloc}};
-  }
-  size_t field_bytes = 0;
-  for (auto& b : bufs) field_bytes += b.second;
-  CkptHeader h{};
-  std::memcpy(h.magic, "PECKPT1", 8);
-  h.version = 1;
-  h.M = prob_.M;
-  h.N = prob_.N;
-  h.rank = blk_.rank;
-  h.Px = blk_.Px;
-  h.Py = blk_.Py;
-  h.fused = fused_ ? 1 : 0;
-  h.variant = opt_.variant;
-  h.par = par_;
-  h.i0 = blk_.i0;
-  h.j0 = blk_.j0;
-  h.nx = blk_.nx;
-  h.ny = blk_.ny;
-  h.state_bytes = sizeof(DevState);
-  h.field_bytes = int64_t(field_bytes);
-  h.halo_bytes = int64_t(sizeof(double) * hsize_ * 4);
-  const std::string tmp = path + ".tmp";
-  FILE* f = std::fopen(tmp.c_str(), "wb");
-  if (!f) throw std::runtime_error("checkpoint: cannot open " + tmp);
-  std::vector<char> host(size_t(64) << 20);
-  auto dump = [&](const void* dev, size_t n) {
-    for (size_t o = 0; o < n; o += host.size()) {
-      const size_t m = std::min(host.size(), n - o);
-      PE_HIP_CHECK(hipMemcpy(host.data(), static_cast<const char*>(dev) + o, m, hipMemcpyDeviceToHost));
-      ck_io(f, host.data(), m, true, path);
-    }
-  };
-  ck_io(f, &h, sizeof(h), true, path);
-  dump(st_, sizeof(DevState));
-  for (auto& b : bufs) dump(b.first, b.second);
-  dump(halo_, size_t(h.halo_bytes));
-  std::fclose(f);
-  if (std::rename(tmp.c_str(), path.c_str()) != 0) throw std::runtime_error("checkpoint: cannot rename " + tmp);
-}
-
-void DeviceSolver::load_checkpoint(const std::string& path) {
-  PE_HIP_CHECK(hipStreamSynchronize(stream_));
-  FILE* f = std::fopen(path.c_str(), "rb");
-  if (!f) throw std::runtime_error("resume: cannot open " + path);
-  CkptHeader h{};
-  ck_io(f, &h, sizeof(h), false, path);
-  size_t field_bytes = fused_ ? sizeof(double) * (2 * xsize_ + wsize_) : sizeof(double) * 4 * blk_.alloc;
-  const bool ok = std::memcmp(h.magic, "PECKPT1", 8) == 0 && h.version == 1 && h.M == prob_.M && h.N == prob_.N &&
-                  h.rank == blk_.rank && h.Px == blk_.Px && h.Py == blk_.Py && h.fused == (fused_ ? 1 : 0) &&
-                  h.variant == opt_.variant && h.i0 == blk_.i0 && h.j0 == blk_.j0 && h.nx == blk_.nx &&
-                  h.ny == blk_.ny && h.state_bytes == int64_t(sizeof(DevState)) &&
-                  h.field_bytes == int64_t(field_bytes) && h.halo_bytes == int64_t(sizeof(double) * hsize_ * 4);
-  if (!ok) {
-    std::fclose(f);
-    throw std::runtime_error("resume: " + path + " does not match this problem / block / algorithm");
-  }
-  std::vector<char> host(size_t(64) << 20);
-  auto load = [&](void* dev, size_t n) {
-    for (size_t o = 0; o < n; o += host.size()) {
-      const size_t m = std::min(host.size(), n - o);
-      ck_io(f, host.data(), m, false, path);
-      PE_HIP_CHECK(hipMemcpy(static_cast<char*>(dev) + o, host.data(), m, hipMemcpyHostToDevice));
-    }
-  };
-  load(st_, sizeof(DevState));
-  if (fused_) {
-    load(fields_, sizeof(double) * xsize_);
-    load(xalt_, sizeof(double) * xsize_);
-    load(walt_, sizeof(double) * wsize_);
-  } else {
-    load(fields_, sizeof(double) * 4 * blk_.alloc);
-  }
-  load(halo_, size_t(h.halo_bytes));
-  std::fclose(f);
-  par_ = h.par;
-  PE_HIP_CHECK(hipMemsetAsync(&st_->sig, 0, sizeof(st_->sig), stream_));  // overlap targets restart
-  // halo push: the next sweep (parity par_) reads x[par_ ^ 1]'s halo rows
-  // from the receive buffer
-  if (push_ && fused_) dev::launch_halo_seed(*kp_, par_ ^ 1, stream_);
-  ov_epoch_ = 0;
-}
 
 void DeviceSolver::wait_event(hipEvent_t ev) {
   const auto t0 = clk::now();

@@ -1,0 +1,424 @@
+// Work-item layout of the single-sweep kernel: rows per item, the item
+// lists (cost-aware static LPT layout or per-XCD dynamic queues, boundary
+// items first for the halo push / overlap) and the LDS-resident kernel's
+// tiles (DeviceSolver::set_items / setup_items / setup_resident).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <limits>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include "../hip/kernels.hpp"
+#include "pe/device.hpp"
+#include "solver_internal.hpp"
+
+namespace pe {
+
+using detail::clk;
+using detail::Range;
+using detail::secs;
+using dev::DevState;
+using dev::KParams;
+
+// Items of `ti` rows: counts and the persistent grids sized for them.
+void DeviceSolver::set_items(int ti) {
+  KParams& k = *kp_;
+  k.ti = ti;
+  k.nitems = int(int64_t(k.nstrips) * ((blk_.nx + ti - 1) / ti));
+  // fewest waves that keep every wave's share of the n items equal
+  auto grid_for = [&](int cap, int n) {
+    const int per = (n + cap - 1) / cap;
+    const int waves = (n + per - 1) / per;
+    return std::max(1, (waves + dev::kWPB - 1) / dev::kWPB);
+  };
+  k.nblocks = grid_for(wave_caps_[0], k.nitems);
+  k.nblocks0 = grid_for(wave_caps_[1], k.nitems);
+  k.nslots = k.nitems;
+  static_waves_ = 0;
+}
+
+// Halo/interior overlap (multi-rank single-sweep).  The sweep walks an item
+// list in which, per XCD shard, the boundary items (outputs sent to a
+// neighbour: first / last two owned rows and columns) come first; each bumps
+// st->sig when stored.  A one-wave kernel on a high-priority halo stream waits
+// for the count, then the exchange runs there while the interior items are
+// still being computed.  The sweep keeps its full persistent grid minus
+// `PE_OV_RESERVE` blocks (default 8) left free for the wait / exchange /
+// unpack kernels.  PE_OVERLAP=0 disables.
+//
+// Every dynamic (order 3) sweep walks such lists, overlap or not.  Item cost
+// estimate (from stamps of the sweep, tools/stamp_probe.py): a row of a
+// strip that contains boundary-band nodes (coefficients evaluated from the
+// chord tables) costs ≈ kGenCost plain rows; an item's rows are its own plus
+// the 4 halo rows it re-reads.  Shards are contiguous chunk ranges of equal
+// estimated cost (consecutive chunks stay on one XCD), and each shard lists
+// its boundary items (overlap) first, then its heavy items in decreasing
+// cost, then the rest chunk-major: the sweep's tail is then made of light
+// items, and waves steal from other shards once their own is empty.
+void DeviceSolver::setup_items() {
+  KParams& k = *kp_;
+  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
+  // Overlap only pays when the exchange costs more than what the overlap
+  // itself costs the sweep (boundary-first item order, blocks kept free for
+  // the halo stream: +9-11 µs per iteration on 2-8 ranks with a zero-latency
+  // transport, profiles/r1_overlap_probe_device_decomp.txt).  Auto: measure
+  // the real exchange here (max over ranks, so every rank decides the same)
+  // and overlap when it exceeds PE_OVERLAP_MIN_US (default 12).
+  // PE_OVERLAP=1 / 0 forces it on / off.
+  const char* e = std::getenv("PE_OVERLAP");
+  overlap_ = false;
+  if (fused_ && comm_->size() > 1 && nb && !push_) {
+    if (e) {
+      overlap_ = std::atoi(e) != 0;
+    } else {
+      double min_us = 12.0;
+      if (const char* m = std::getenv("PE_OVERLAP_MIN_US")) min_us = std::atof(m);
+      overlap_ = exchange_us_ > min_us;
+    }
+  }
+  // Lists: dynamic sweeps (order 3), static chunk-major sweeps (order 0:
+  // heavy items split, below) and the overlap; orders 1 / 2 are plain
+  // tuning walks.
+  if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
+  if (ilist_) {  // re-laid out (rows-per-item tuning)
+    PE_HIP_CHECK(hipFree(ilist_));
+    ilist_ = nullptr;
+  }
+  if (overlap_) {
+    ov_reserve_ = 8;
+    // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
+    // order (no boundary-first list)
+    if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
+    if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
+  }
+  const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - (overlap_ ? ov_reserve_ : 0));
+  const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
+  const int nchunks = int((blk_.nx + k.ti - 1) / k.ti);
+  double gen_cost = 3.0;
+  if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
+  const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
+  const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
+  // per-item cost: rows ib-2 .. ie+2, band rows weighted
+  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
+  // Does local row q have a boundary-band node in strip s's 128 loaded
+  // columns?  (The kernel's has_gen on the same row-class table.)
+  auto row_gen = [&](int64_t q, int s) {
+    const int64_t J = -1 + int64_t(s) * dev::kFSW;
+    const int64_t t = q + 1;  // table index of local row q
+    if (t < 0 || t >= rows_tab) return false;
+    const int* r = &rowcls_host_[size_t(t) * 4];
+    const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
+    return lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
+  };
+  auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
+    double c = 0.0;
+    for (int64_t q = ib - 2; q <= ie + 2; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
+    return c;
+  };
+  auto rows_band = [&](int64_t ib, int64_t ie, int s) {
+    for (int64_t q = ib - 2; q <= ie + 2; ++q)
+      if (row_gen(q, s)) return true;
+    return false;
+  };
+  auto item_cost = [&](int ch, int s) {
+    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+    return rows_cost(ib, ie, s);
+  };
+  // {first row | band flag, strip | rows << 20}; the band flag selects the
+  // kernel's coefficient path (rows ib-2 .. ie+2 include a boundary-band row)
+  auto entry = [&](int64_t ib, int64_t rows, int s) {
+    const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
+    return int2{int(ib) | flag, s | int(rows << 20)};
+  };
+  // outputs a neighbour needs: first in the layout under the overlap (they
+  // feed the exchange) and under the halo push (their xGMI stores then
+  // overlap the rest of the sweep instead of ending it)
+  auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
+    const int64_t J = -1 + int64_t(s) * dev::kFSW;
+    const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
+    return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
+           ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
+            (blk_.has(UP) && jhi >= blk_.ny - 1));
+  };
+
+  if (k.order == 0) {
+    // ---- Static sweeps: a longest-processing-time-first layout ----
+    // Every wave walks list positions w, w + W, w + 2W, … (W = the grid's
+    // waves), so the host decides who does what: items are cut where one
+    // would exceed a wave's fair share (band items cost ≈2-3× a plain one;
+    // on small blocks, where each wave gets about one item, the band items
+    // alone were the sweep's tail — profiles/r2_small_before.txt), then
+    // assigned heaviest first to the least-loaded wave, and a wave's k-th
+    // item goes to position k·W + w (empty entries fill the gaps).  Equal
+    // costs keep chunk-major order, so each round of positions still covers
+    // a compact window of rows.  Overlap: boundary items take the first
+    // positions (they run in the first round).
+    struct Piece {
+      int64_t ib, rows;
+      int s;
+      double cost;
+      bool bnd;
+    };
+    const double overhead = 3.0;  // per-item prologue / epilogue, in row steps (stamps)
+    int waves_avail = std::max(dev::kWPB, wave_cap_ - (overlap_ ? ov_reserve_ * dev::kWPB : 0));
+    if (const char* w = std::getenv("PE_WAVES")) waves_avail = std::max(dev::kWPB, std::atoi(w));
+    double total = 0.0;
+    for (int id = 0; id < k.nitems; ++id) total += item_cost(id / k.nstrips, id % k.nstrips) + overhead;
+    // cut only when there are fewer items than waves (small blocks): with
+    // more items than waves the layout balances them, and every cut re-reads
+    // 4 more halo rows (2048²: 96 vs 91 µs per iteration with cuts)
+    const int W0 = std::max(1, std::min(waves_avail, k.nitems));
+    const double share = k.nitems >= waves_avail ? 1e300 : std::max(total / W0, (double(k.ti + 4) + overhead) * 1.15);
+    std::vector<Piece> pcs;
+    for (int ch = 0; ch < nchunks; ++ch)
+      for (int s = 0; s < k.nstrips; ++s) {
+        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+        const int64_t n = ie - ib + 1;
+        const bool bnd = is_boundary(ib, ie, s);
+        int parts = 1;
+        if (split_heavy && !bnd) {
+          for (; 2 * (parts + 1) <= n; ++parts) {  // pieces of >= 2 rows
+            double worst = 0.0;
+            for (int q = 0; q < parts; ++q)
+              worst = std::max(worst, rows_cost(ib + n * q / parts, ib + n * (q + 1) / parts - 1, s) + overhead);
+            if (worst <= share) break;
+          }
+        }
+        for (int q = 0; q < parts; ++q) {
+          const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
+          pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
+        }
+      }
+    const int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
+    std::vector<std::vector<int>> per(static_cast<size_t>(W));
+    std::vector<double> load(static_cast<size_t>(W), 0.0);
+    std::vector<int> order;
+    int nbnd = 0;
+    for (int i = 0; i < int(pcs.size()); ++i) {
+      if (pcs[size_t(i)].bnd) {  // boundary pieces: positions 0, 1, … in order
+        per[size_t(nbnd % W)].push_back(i);
+        load[size_t(nbnd % W)] += pcs[size_t(i)].cost;
+        ++nbnd;
+      } else {
+        order.push_back(i);
+      }
+    }
+    std::stable_sort(order.begin(), order.end(),
+                     [&](int a, int b) { return pcs[size_t(a)].cost > pcs[size_t(b)].cost; });
+    using LW = std::pair<double, int>;
+    std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
+    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
+    for (int i : order) {
+      const LW t = heap.top();
+      heap.pop();
+      per[size_t(t.second)].push_back(i);
+      heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
+    }
+    size_t rounds = 0;
+    for (const auto& v : per) rounds = std::max(rounds, v.size());
+    lay_max_ = 0.0;
+    lay_mean_ = 0.0;
+    for (int w = 0; w < W; ++w) {
+      double l = 0.0;
+      for (int i : per[size_t(w)]) l += pcs[size_t(i)].cost;
+      lay_max_ = std::max(lay_max_, l);
+      lay_mean_ += l / W;
+    }
+    lay_items_ = int(rounds);
+    std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)
+    for (int w = 0; w < W; ++w)
+      for (size_t r = 0; r < per[size_t(w)].size(); ++r) {
+        const Piece& p = pcs[size_t(per[size_t(w)][r])];
+        all[r * size_t(W) + size_t(w)] = entry(p.ib, p.rows, p.s);
+      }
+    static_waves_ = W;
+    nslot_cap_ = std::max<int>(nslot_cap_, int(all.size()));
+    ov_nb_ = nbnd;
+    ov_lnsh_ = 1;
+    ov_lbase_[0] = 0;
+    for (int x = 1; x <= 8; ++x) ov_lbase_[x] = int(all.size());
+    ov_lnb_[0] = nbnd;
+    for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
+    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+    const auto tc = clk::now();
+    upload(ilist_, all.data(), sizeof(int2) * all.size());
+    copy_setup_s_ += secs(tc, clk::now());
+    k.ilist = ilist_;
+    k.lnsh = 1;
+    k.lwaves = W;
+    k.nslots = int(all.size());
+    for (int x = 0; x <= 8; ++x) k.lbase[x] = ov_lbase_[x];
+    for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+    // static list walk: the grid is the one the list was laid out for (plus
+    // the blocks the overlap keeps free for the halo stream)
+    k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
+    if (overlap_) create_halo_stream();
+    return;
+  }
+  lay_max_ = lay_mean_ = 0.0;
+  lay_items_ = 0;
+  std::vector<double> cost(size_t(k.nitems));
+  std::vector<double> ccost(size_t(nchunks) + 1, 0.0);  // prefix sums per chunk
+  for (int ch = 0; ch < nchunks; ++ch) {
+    double cc = 0.0;
+    for (int s = 0; s < k.nstrips; ++s) cc += cost[size_t(ch) * k.nstrips + s] = item_cost(ch, s);
+    ccost[size_t(ch) + 1] = ccost[size_t(ch)] + cc;
+  }
+  const double light = double(k.ti + 4);
+  std::vector<int> cut(size_t(nsh) + 1, 0);
+  for (int x = 1; x < nsh; ++x) {
+    const double target = ccost.back() * x / nsh;
+    int c = cut[size_t(x) - 1];
+    while (c < nchunks && ccost[size_t(c) + 1] <= target) ++c;
+    cut[size_t(x)] = c;
+  }
+  cut[size_t(nsh)] = nchunks;
+  // Tail split (dynamic sweeps, opt-in): the last PE_TAIL_FRAC of every
+  // shard's light items are cut into PE_TAIL_SPLIT shorter items, so the round
+  // of items running when the queues drain is short.  Off by default since the
+  // per-XCD queues: at one placement every extra item costs more than the
+  // shorter drain saves (8192², 18 rows: 545.5 µs per iteration unsplit vs
+  // 550.6 / 552.1 / 556.1 with 5 / 10 / 30 % split; 2 ranks 297.8 vs 307.5 —
+  // profiles/r2_layout.txt).
+  double tail_frac = 0.0;
+  int tail_split = 2;
+  if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
+  if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));
+  std::vector<int2> all;
+  ov_nb_ = 0;
+  ov_lnsh_ = nsh;
+  for (int x = 0; x < nsh; ++x) {
+    std::vector<int> b, heavy, in;
+    for (int ch = cut[size_t(x)]; ch < cut[size_t(x) + 1]; ++ch)
+      for (int s = 0; s < k.nstrips; ++s) {
+        const int id = ch * k.nstrips + s;
+        const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+        if (is_boundary(ib, ie, s)) b.push_back(id);
+        else if (sort_heavy && cost[size_t(id)] > 1.25 * light) heavy.push_back(id);
+        else in.push_back(id);
+      }
+    std::stable_sort(heavy.begin(), heavy.end(), [&](int a, int c) { return cost[size_t(a)] > cost[size_t(c)]; });
+    ov_lbase_[x] = int(all.size());
+    ov_lnb_[x] = int(b.size());
+    ov_nb_ += int(b.size());
+    const size_t nsplit = size_t(tail_frac * double(in.size()) + 0.5);
+    auto push = [&](int id, int parts) {
+      const int ch = id / k.nstrips, s = id % k.nstrips;
+      const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+      const int64_t n = ie - ib + 1;
+      parts = int(std::min<int64_t>(parts, n));
+      for (int q = 0; q < parts; ++q) {
+        const int64_t a0 = ib + n * q / parts, a1 = ib + n * (q + 1) / parts;
+        all.push_back(entry(a0, a1 - a0, s));
+      }
+    };
+    for (int id : b) push(id, 1);
+    for (int id : heavy) push(id, 1);
+    for (size_t i = 0; i < in.size(); ++i) push(in[i], i + nsplit >= in.size() ? tail_split : 1);
+  }
+  ov_lbase_[nsh] = int(all.size());
+  if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
+  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+  const auto tc = clk::now();
+  upload(ilist_, all.data(), sizeof(int2) * all.size());
+  copy_setup_s_ += secs(tc, clk::now());
+  // Every dynamic sweep walks the list (the plain one counts no boundary
+  // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).
+  k.ilist = ilist_;
+  k.lnsh = nsh;
+  k.nslots = int(all.size());
+  for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
+  for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+  if (overlap_) create_halo_stream();
+}
+
+// LDS-resident geometry: tiles of one 124-column strip × R rows (the
+// streaming sweep's strips), one workgroup each, at most one per CU, R ≥ 8
+// where the block allows and ≤ kResMaxRows; the band-coefficient table is
+// sized from the host row classes (the kernel's exact band test).
+void DeviceSolver::setup_resident() {
+  KParams& k = *kp_;
+  resident_ = false;
+  const char* e = std::getenv("PE_RESIDENT");
+  if (e && std::atoi(e) == 0) return;
+  if (!fused_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0) return;
+  const int nx = int(blk_.nx);
+  int cus = 256;
+  {
+    int dev = 0;
+    PE_HIP_CHECK(hipGetDevice(&dev));
+    PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+  }
+  const int nstrips = k.nstrips;
+  if (nstrips > cus) return;
+  const int ntr = std::max(1, std::min(cus / nstrips, nx / 8));
+  if (nx < 2 * ntr) return;
+  std::vector<int> rs(size_t(ntr) + 1);
+  for (int t = 0; t <= ntr; ++t) rs[size_t(t)] = 1 + int(int64_t(t) * nx / ntr);
+  int rcap = 0;
+  for (int t = 0; t < ntr; ++t) rcap = std::max(rcap, rs[size_t(t) + 1] - rs[size_t(t)]);
+  if (rcap > dev::kResMaxRows) return;
+  // band nodes per tile region (rows I0-2 .. I0+R+1, columns J0-2 .. J0+125)
+  const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
+  int nb_max = 0;
+  for (int t = 0; t < ntr; ++t)
+    for (int sx = 0; sx < nstrips; ++sx) {
+      int nb = 0;
+      const int J0 = 1 + dev::kFSW * sx;
+      for (int q = rs[size_t(t)] - 2; q < rs[size_t(t) + 1] + 2; ++q) {
+        if (q + 1 < 0 || q + 1 >= rows_tab) continue;
+        const int* r = &rowcls_host_[size_t(q + 1) * 4];
+        for (int c = J0 - 2; c < J0 + 126; ++c)
+          if (c >= r[2] && c <= r[3] && !(c >= r[0] && c <= r[1])) ++nb;
+      }
+      nb_max = std::max(nb_max, nb);
+    }
+  const int nbcap = nb_max + 8;
+  const size_t lds = dev::resident_lds_bytes(rcap, nbcap);
+  if (lds > 163840) return;
+  const int per_cu = dev::resident_max_blocks_per_cu(lds);
+  const int nwg = ntr * nstrips;
+  if (per_cu < 1 || nwg > per_cu * cus) return;
+  rp_ = std::make_unique<dev::ResParams>();
+  dev::ResParams& r = *rp_;
+  std::memset(&r, 0, sizeof(r));
+  r.nstrips = nstrips;
+  r.ntr = ntr;
+  r.nwg = nwg;
+  r.rcap = rcap;
+  r.nbcap = nbcap;
+  r.lds_bytes = unsigned(lds);
+  r.timeout_ticks = 200000000LL;  // 2 s per barrier wait
+  if (const char* t = std::getenv("PE_RES_TIMEOUT_S")) r.timeout_ticks = (long long)(std::atof(t) * 1e8);
+  PE_HIP_CHECK(hipMalloc(&res_rowstart_, sizeof(int) * rs.size()));
+  upload(res_rowstart_, rs.data(), sizeof(int) * rs.size());
+  const size_t nedge = size_t(2) * size_t(nwg) * dev::kResEdge, npart = size_t(2) * size_t(nwg) * 8;
+  PE_HIP_CHECK(hipMalloc(&res_buf_, sizeof(double) * (nedge + npart)));
+  // stream-ordered: a null-stream operation would create that stream's
+  // hardware queue (≈10 ms inside T_solver in a fresh process, profiles/r2_ctor_phases.txt)
+  PE_HIP_CHECK(hipMemsetAsync(res_buf_, 0, sizeof(double) * (nedge + npart), stream_));
+  PE_HIP_CHECK(hipMalloc(&res_ctr_, sizeof(unsigned) * 8 * 32));
+  if (const char* t = std::getenv("PE_RES_STAMPS"); t && std::atoi(t) == 1) {
+    nstamps_ = size_t(nwg) * dev::kResStampIters * 8;
+    PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
+    PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
+    r.stamps = stamps_;
+  }
+  r.rowstart = res_rowstart_;
+  r.edges = res_buf_;
+  r.partials = res_buf_ + nedge;
+  r.ctr = res_ctr_;
+  resident_ = true;
+}
+
+}  // namespace pe

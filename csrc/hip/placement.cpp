@@ -1,0 +1,289 @@
+// Memory placement of the solver fields: the allocation modes (plain,
+// physically contiguous, shuffled physical chunks) and the placement
+// search that picks, among a few candidate allocations, the one the sweep
+// streams fastest from (DeviceSolver::choose_placement / carve_placement).
+#include <hip/hip_runtime_api.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <limits>
+#include <mutex>
+#include <queue>
+#include <string>
+#include <vector>
+
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include "../hip/kernels.hpp"
+#include "pe/device.hpp"
+#include "solver_internal.hpp"
+
+namespace pe {
+
+namespace detail {
+// Field allocation.  PE_MALLOC=1 requests physically contiguous memory
+// (hipDeviceMallocContiguous); PE_MALLOC=2 builds the range from
+// PE_VMM_CHUNK_MB-sized physical chunks (default 2) mapped into one virtual
+// range in a shuffled order (virtual memory API) — experiments on the
+// allocation-dependent speed of the streaming sweep (docs/PERFORMANCE.md).
+namespace {
+struct VmmRange {
+  size_t size;
+  std::vector<hipMemGenericAllocationHandle_t> h;
+};
+std::mutex g_vmm_mu;
+std::map<void*, VmmRange> g_vmm;
+
+void* vmm_alloc_shuffled(size_t bytes) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  hipMemAllocationProp prop{};
+  prop.type = hipMemAllocationTypePinned;
+  prop.location.type = hipMemLocationTypeDevice;
+  prop.location.id = dev;
+  size_t gran = 0;
+  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || gran == 0)
+    return nullptr;
+  size_t chunk = size_t(2) << 20;
+  if (const char* e = std::getenv("PE_VMM_CHUNK_MB")) chunk = size_t(std::max(1, std::atoi(e))) << 20;
+  chunk = (chunk + gran - 1) / gran * gran;
+  const size_t n = (bytes + chunk - 1) / chunk, size = n * chunk;
+  void* va = nullptr;
+  if (hipMemAddressReserve(&va, size, chunk, nullptr, 0) != hipSuccess) return nullptr;
+  VmmRange r{size, std::vector<hipMemGenericAllocationHandle_t>(n)};
+  for (size_t i = 0; i < n; ++i)
+    if (hipMemCreate(&r.h[i], chunk, &prop, 0) != hipSuccess) {
+      for (size_t j = 0; j < i; ++j) (void)hipMemRelease(r.h[j]);
+      (void)hipMemAddressFree(va, size);
+      return nullptr;
+    }
+  // chunk i of the range ← physical chunk perm[i] (fixed-seed shuffle)
+  std::vector<size_t> perm(n);
+  for (size_t i = 0; i < n; ++i) perm[i] = i;
+  unsigned long long x = 0x9E3779B97F4A7C15ull;
+  for (size_t i = n; i > 1; --i) {
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    std::swap(perm[i - 1], perm[size_t(x % i)]);
+  }
+  for (size_t i = 0; i < n; ++i)
+    PE_HIP_CHECK(hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, r.h[perm[i]], 0));
+  hipMemAccessDesc acc{};
+  acc.location.type = hipMemLocationTypeDevice;
+  acc.location.id = dev;
+  acc.flags = hipMemAccessFlagsProtReadWrite;
+  PE_HIP_CHECK(hipMemSetAccess(va, size, &acc, 1));
+  std::lock_guard<std::mutex> g(g_vmm_mu);
+  g_vmm.emplace(va, std::move(r));
+  return va;
+}
+}  // namespace
+
+// mode: 0 hipMalloc, 1 physically contiguous, 2 shuffled physical chunks;
+// PE_MALLOC overrides.  nullptr when the device is out of memory.
+void* field_try_alloc(size_t bytes, int mode) {
+  void* p = nullptr;
+  if (const char* e = std::getenv("PE_MALLOC")) mode = std::atoi(e);
+  if (mode == 2) {
+    if (void* v = vmm_alloc_shuffled(bytes)) return v;
+    (void)hipGetLastError();
+    mode = 0;  // no virtual memory API: plain allocation
+  }
+  const hipError_t r = mode == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) : hipMalloc(&p, bytes);
+  if (r != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  return p;
+}
+
+void* field_alloc(size_t bytes, int mode) {
+  void* p = field_try_alloc(bytes, mode);
+  if (!p) PE_HIP_CHECK(hipErrorOutOfMemory);
+  return p;
+}
+
+void field_free(void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> g(g_vmm_mu);
+    auto it = g_vmm.find(p);
+    if (it != g_vmm.end()) {
+      (void)hipDeviceSynchronize();
+      (void)hipMemUnmap(p, it->second.size);
+      for (auto h : it->second.h) (void)hipMemRelease(h);
+      (void)hipMemAddressFree(p, it->second.size);
+      g_vmm.erase(it);
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+}  // namespace detail
+
+using detail::clk;
+using detail::field_free;
+using detail::field_try_alloc;
+using detail::Range;
+using detail::secs;
+using dev::KParams;
+
+// Memory-placement autotune (single-sweep, large blocks).  The same sweep
+// runs at two distinct speeds depending on which physical memory its arrays
+// land in (8192²: ≈1380 vs ≈1510 it/s; stable per allocation; consecutive
+// allocations come in slow and fast runs of several GB; no dependence on
+// row padding, virtual address or TLB misses — the slow placements show ~1.7×
+// the DRAM credit stalls; docs/PERFORMANCE.md).  Try up to
+// PE_PLACEMENT_TRIES (default 8) candidate allocations, each after a
+// PE_PLACEMENT_SKIP_GB (default 8) spacer so it lands in another region;
+// time a few local sweeps on real data (no communication) and keep the
+// fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
+void DeviceSolver::choose_placement() {
+  Range range("pe.placement_search");
+  struct Clock {
+    double& out;
+    clk::time_point t0 = clk::now();
+    ~Clock() { out = secs(t0, clk::now()); }
+  } clock{placement_s_};
+  const double pts = double(blk_.nx) * double(blk_.ny);
+  // Only large blocks: the two-speed placement was measured at 8192² (≈9 %);
+  // at 2400×3200 / 4096² the candidates differ by ≤ 3-7 % while the spacer
+  // allocations cost 0.02-6 s of construction (T_solver) depending on the
+  // allocator state (profiles/r2_ctor_probe.txt).
+  int tries = pts >= 24.0e6 ? 8 : 1;
+  if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
+  double skip_gb = 8.0;
+  if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
+  double fast_tbs = 4.9, max_s = 0.3;
+  if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
+  if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
+  if (tries <= 1) return;
+  // spacers are transient; never let the search take more than 40 % of the
+  // free memory (several solvers may share the device)
+  {
+    size_t free_b = 0, total_b = 0;
+    if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
+      const double per_try = skip_gb * double(1ull << 30) + double(sizeof(double) * (2 * xsize_ + wsize_));
+      tries = std::min<int>(tries, std::max(1, int(0.4 * double(free_b) / per_try)));
+    }
+  }
+  if (tries <= 1) return;
+  if (const char* e = std::getenv("PE_PLACEMENT"); e && std::string(e) == "carve") {
+    carve_placement();
+    return;
+  }
+  struct Cand {
+    double *x0, *x1, *w;
+    float ms;
+  };
+  std::vector<Cand> c;
+  std::vector<void*> spacers;
+  c.push_back(Cand{fields_, xalt_, walt_, 0.f});
+  for (int t = 0; t < tries; ++t) {
+    if (t > 0) {
+      void* sp = nullptr;
+      if (skip_gb > 0 && hipMalloc(&sp, size_t(skip_gb * double(1ull << 30))) != hipSuccess) break;
+      if (sp) spacers.push_back(sp);
+      void* a = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
+      if (!a) break;
+      void* b = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
+      if (!b) {
+        field_free(a);
+        break;
+      }
+      void* w = field_try_alloc(sizeof(double) * wsize_, alloc_mode_);
+      if (!w) {
+        field_free(a);
+        field_free(b);
+        break;
+      }
+      c.push_back(Cand{static_cast<double*>(a), static_cast<double*>(b), static_cast<double*>(w), 0.f});
+    }
+    set_fused_fields(c[t].x0, c[t].x1, c[t].w);
+    enqueue_init();
+    dev::launch_S(*kp_, 1, stream_);  // S_0 on real data (local sums only)
+    for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+    for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+    PE_HIP_CHECK(hipEventSynchronize(t1_));
+    PE_HIP_CHECK(hipEventElapsedTime(&c[t].ms, t0_, t1_));
+    // The placements fall into classes (8192²: 0.541-0.547, 0.556-0.562,
+    // 0.59-0.61 and 0.62-0.65 ms per sweep; the bench follows them: 1792 vs
+    // 1745 it/s for the first two, profiles/r2_bench_launch.txt).  A try costs
+    // ≈6 ms (spacer, allocation, 9 sweeps), the best class saves ≈3 % of a
+    // 3.3 s solve: keep the best of all tries, stopping early only at the
+    // best class — the sweep's average 40 B/node streamed at >=
+    // PE_PLACEMENT_FAST_TBS (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
+    // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
+    // 0.56-0.60 ms placements when better ones were a try or two further.)
+    const double tbs = 40.0 * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
+    if (tbs >= fast_tbs) break;
+    // spacer allocations are cheap on fresh memory but can take seconds
+    // when the allocator must clear reused memory (profiles/r2_ctor_probe.txt):
+    // the search is capped at PE_PLACEMENT_MAX_S (0.3 s) of wall time
+    if (secs(clock.t0, clk::now()) > max_s) break;
+  }
+  (void)hipGetLastError();  // clear a failed search allocation
+  size_t best = 0;
+  for (size_t i = 1; i < c.size(); ++i)
+    if (c[i].ms < c[best].ms) best = i;
+  for (size_t i = 0; i < c.size(); ++i)
+    if (i != best) {
+      field_free(c[i].x0);
+      field_free(c[i].x1);
+      field_free(c[i].w);
+    }
+  for (void* sp : spacers) PE_HIP_CHECK(hipFree(sp));
+  set_fused_fields(c[best].x0, c[best].x1, c[best].w);
+  placement_best_ = int(best);
+  placement_ms_.clear();
+  for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
+}
+
+// Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE
+// allocation at x0 = base, x1 = base + X + d, w = base + 2X + 2d for a set of
+// offsets d, each timed like a search candidate — does the sweep's speed
+// depend on the arrays' relative offsets within the same physical memory?
+void DeviceSolver::carve_placement() {
+  static const size_t kD[] = {0, 4096, 65536, 262144, 1 << 20, 2 << 20, 3 << 20, 5 << 20, 7 << 20, 11 << 20, 13 << 20};
+  const size_t X = sizeof(double) * size_t(xsize_), W = sizeof(double) * size_t(wsize_);
+  const size_t dmax = size_t(16) << 20;
+  char* base = nullptr;
+  PE_HIP_CHECK(hipMalloc(&base, 2 * X + W + 2 * dmax + 4096));
+  double *o0 = fields_, *o1 = xalt_, *ow = walt_;
+  placement_ms_.clear();
+  float best = 0.f;
+  size_t bi = 0;
+  for (size_t i = 0; i < sizeof(kD) / sizeof(kD[0]); ++i) {
+    const size_t d = kD[i];
+    set_fused_fields(reinterpret_cast<double*>(base), reinterpret_cast<double*>(base + X + d),
+                     reinterpret_cast<double*>(base + 2 * X + 2 * d));
+    enqueue_init();
+    dev::launch_S(*kp_, 1, stream_);
+    for (int it = 0; it < 2; ++it) dev::launch_S(*kp_, it & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+    for (int it = 0; it < 6; ++it) dev::launch_S(*kp_, it & 1, stream_);
+    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+    PE_HIP_CHECK(hipEventSynchronize(t1_));
+    float ms = 0.f;
+    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+    placement_ms_.push_back(ms / 6.0f);
+    if (i == 0 || ms < best) {
+      best = ms;
+      bi = i;
+    }
+  }
+  // keep the separate allocations of the constructor (the carve block is an
+  // experiment); report the best offset's index
+  PE_HIP_CHECK(hipFree(base));
+  set_fused_fields(o0, o1, ow);
+  placement_best_ = int(bi);
+}
+
+}  // namespace pe
