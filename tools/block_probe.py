@@ -3,6 +3,7 @@ decomposition of 8192² (timing-only transport with zero delays, overlap off,
 eager) under a list of kernel configurations.
 
     PROBE_CFG=8:aspect,4:aspect PROBE_ENV="PE_TI=8 PE_ORDER=0;PE_TI=16 PE_ORDER=3" python tools/block_probe.py
+    PROBE_RANKS=all (every rank's block in turn; default: rank P//2)
 """
 import os
 import sys
@@ -20,28 +21,31 @@ iters = int(os.environ.get("PROBE_ITERS", "400"))
 GM, GN = (int(v) for v in os.environ.get("PROBE_GRID", "8192x8192").split("x"))
 prob = pe.EllipseProblem(GM, GN)
 os.environ["PE_OVERLAP"] = "0"
+# PROBE_RANKS: "mid" (default, rank P//2), "all", or a comma list
+rsel = os.environ.get("PROBE_RANKS", "mid")
 for P, spec in configs:
     g = D.grid(P, GM, GN, spec)
-    rank = P // 2
-    blk = nat.decompose(GM, GN, g, rank)
-    for env in envs:
-        kv = dict(x.split("=") for x in env.split()) if env else {}
-        saved = {k: os.environ.get(k) for k in kv}
-        os.environ.update(kv)
-        opt = nat.SolveOptions()
-        opt.check_tol = False
-        comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
-        s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
-        s.reset()
-        s.time_iterations(20, False)
-        dt = s.time_iterations(iters, False)
-        tune = " ".join(f"{x * 1e3:.1f}" for x in s.ti_tuning_ms)
-        print(f"P={P} {g.Px}x{g.Py} block {blk.nx}x{blk.ny} [{env or 'default'}]: {dt / iters * 1e6:7.1f} us/iter "
-              f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)  ti {s.ti}" + (f"  tuning us/sweep [{tune}]" if tune else ""),
-              flush=True)
-        del s, comm
-        for k, v in saved.items():
-            if v is None:
-                os.environ.pop(k, None)
-            else:
-                os.environ[k] = v
+    ranks = [P // 2] if rsel == "mid" else list(range(P)) if rsel == "all" else [int(r) for r in rsel.split(",")]
+    for rank in ranks:
+        blk = nat.decompose(GM, GN, g, rank)
+        for env in envs:
+            kv = dict(x.split("=") for x in env.split()) if env else {}
+            saved = {k: os.environ.get(k) for k in kv}
+            os.environ.update(kv)
+            opt = nat.SolveOptions()
+            opt.check_tol = False
+            comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
+            s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
+            s.reset()
+            s.time_iterations(20, False)
+            dt = s.time_iterations(iters, False)
+            tune = " ".join(f"{x * 1e3:.1f}" for x in s.ti_tuning_ms)
+            print(f"P={P} {g.Px}x{g.Py} rank {rank} block {blk.nx}x{blk.ny} [{env or 'default'}]: {dt / iters * 1e6:7.1f} us/iter "
+                  f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)  ti {s.ti}" + (f"  tuning us/sweep [{tune}]" if tune else ""),
+                  flush=True)
+            del s, comm
+            for k, v in saved.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
