@@ -199,6 +199,63 @@ void DeviceSolver::setup_items() {
           pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
         }
       }
+    // PE_SEGMENTS=1 (experiment): the segment layout below
+    if (const char* sg = std::getenv("PE_SEGMENTS"); sg && std::atoi(sg) == 1) {
+      // Segment layout: one tall item per wave.  Each strip's rows are cut
+      // into segments of equal estimated cost, and the strips' segment
+      // counts are dealt (largest remaining segment cost first) so that the
+      // heaviest segment is as light as possible.  An item re-reads its 4
+      // halo rows; at 24 rows that is +17 % row reads, ≈ the +21 % excess
+      // DRAM reads the counters show (profiles/r2_head_profile.txt), and a
+      // segment of a few hundred rows re-reads them once.
+      pcs.clear();
+      const int64_t nx = blk_.nx;
+      const int ns = k.nstrips;
+      const int Wt = std::max(dev::kWPB, (waves_avail / dev::kWPB) * dev::kWPB);
+      std::vector<std::vector<double>> pre(static_cast<size_t>(ns));  // cost prefix over rows 1..q
+      std::vector<double> C(static_cast<size_t>(ns));
+      double sumC = 0.0;
+      for (int s = 0; s < ns; ++s) {
+        auto& p = pre[size_t(s)];
+        p.assign(size_t(nx) + 1, 0.0);
+        for (int64_t q = 1; q <= nx; ++q) p[size_t(q)] = p[size_t(q - 1)] + (row_gen(q, s) ? gen_cost : 1.0);
+        C[size_t(s)] = p[size_t(nx)];
+        sumC += C[size_t(s)];
+      }
+      // at most 1500 rows (the list entry's row field), at least 4 per segment
+      const int n_min = int((nx + 1499) / 1500), n_max = std::max<int>(1, int(nx / 4));
+      std::vector<int> n(static_cast<size_t>(ns));
+      int tot = 0;
+      using CS = std::pair<double, int>;
+      std::priority_queue<CS> h;
+      for (int s = 0; s < ns; ++s) {
+        n[size_t(s)] = std::min(n_max, std::max(n_min, int(std::floor(C[size_t(s)] * Wt / sumC))));
+        tot += n[size_t(s)];
+        h.push(CS{C[size_t(s)] / n[size_t(s)], s});
+      }
+      while (tot < Wt && !h.empty()) {
+        const int s = h.top().second;
+        h.pop();
+        if (n[size_t(s)] >= n_max) continue;
+        ++n[size_t(s)];
+        ++tot;
+        h.push(CS{C[size_t(s)] / n[size_t(s)], s});
+      }
+      for (int s = 0; s < ns; ++s) {
+        const auto& p = pre[size_t(s)];
+        int64_t a0 = 1;
+        for (int q = 1; q <= n[size_t(s)]; ++q) {
+          int64_t a1 = nx + 1;
+          if (q < n[size_t(s)]) {
+            const double target = C[size_t(s)] * q / n[size_t(s)];
+            a1 = int64_t(std::lower_bound(p.begin() + 1, p.end(), target) - p.begin()) + 1;
+            a1 = std::min<int64_t>(std::max<int64_t>(a1, a0 + 4), nx + 1 - 4 * (n[size_t(s)] - q));
+          }
+          pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, is_boundary(a0, a1 - 1, s)});
+          a0 = a1;
+        }
+      }
+    }
     const int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
     std::vector<std::vector<int>> per(static_cast<size_t>(W));
     std::vector<double> load(static_cast<size_t>(W), 0.0);
