@@ -104,7 +104,14 @@ void DeviceSolver::setup_items() {
   const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - (overlap_ ? ov_reserve_ : 0));
   const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
   const int nchunks = int((blk_.nx + k.ti - 1) / k.ti);
-  double gen_cost = 3.0;
+  // Cost of a boundary-band row in plain rows (item costs of the layouts).
+  // Since the band coefficients are evaluated once per row (LDS ring) a band
+  // row costs less than the round-1 weight of 3: blocks below 2²⁴ nodes lay
+  // out better at 2 (8-rank 8192² block 84.2-85.1 vs 87.3-87.8 µs per
+  // iteration, 4-rank 155 vs 160, 2400×3200 77.9-79.3 vs 79.5-80.3; 1 is
+  // worse everywhere); larger blocks see no difference above the placement
+  // noise and keep 3 (profiles/r2_gencost.txt).  PE_GEN_COST overrides.
+  double gen_cost = double(blk_.nx) * double(blk_.ny) >= double(1 << 24) ? 3.0 : 2.0;
   if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
   const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
   const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
