@@ -155,7 +155,11 @@ void DeviceSolver::choose_placement() {
   // at 2400×3200 / 4096² the candidates differ by ≤ 3-7 % while the spacer
   // allocations cost 0.02-6 s of construction (T_solver) depending on the
   // allocator state (profiles/r2_ctor_probe.txt).
-  int tries = pts >= 24.0e6 ? 8 : 1;
+  // 12 tries (the 40 % memory cap below allows 11 at 8192²): a box whose
+  // first 8 held no best-class placement ran 1800 vs 1843 it/s
+  // (profiles/r2_validate_s4b.txt); a try costs ≈6 ms, and the search stops
+  // at the first best-class candidate.
+  int tries = pts >= 24.0e6 ? 12 : 1;
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
   double skip_gb = 8.0;
   if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
