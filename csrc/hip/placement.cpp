@@ -157,8 +157,10 @@ void DeviceSolver::choose_placement() {
   // allocator state (profiles/r2_ctor_probe.txt).
   // 12 tries (the 40 % memory cap below allows 11 at 8192²): a box whose
   // first 8 held no best-class placement ran 1800 vs 1843 it/s
-  // (profiles/r2_validate_s4b.txt); a try costs ≈6 ms, and the search stops
-  // at the first best-class candidate.
+  // (profiles/r2_validate_s4b.txt), and the final validation's 2000-step
+  // process found its best-class candidate at the 9th try (1838 it/s,
+  // profiles/r2_validate_final.txt); a try costs ≈6 ms, and the search
+  // stops at the first best-class candidate.
   int tries = pts >= 24.0e6 ? 12 : 1;
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
   double skip_gb = 8.0;
