@@ -170,12 +170,14 @@ void DeviceSolver::choose_placement() {
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return;
   // spacers are transient; never let the search take more than 40 % of the
-  // free memory (several solvers may share the device)
+  // free memory (several solvers may share the device; PE_PLACEMENT_MEM_FRAC)
   {
+    double frac = 0.4;
+    if (const char* e = std::getenv("PE_PLACEMENT_MEM_FRAC")) frac = std::min(0.9, std::max(0.0, std::atof(e)));
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
       const double per_try = skip_gb * double(1ull << 30) + double(sizeof(double) * (2 * xsize_ + wsize_));
-      tries = std::min<int>(tries, std::max(1, int(0.4 * double(free_b) / per_try)));
+      tries = std::min<int>(tries, std::max(1, int(frac * double(free_b) / per_try)));
     }
   }
   if (tries <= 1) return;
