@@ -7,20 +7,37 @@ Poisson problem (BASELINE.json: "PCG iters/sec + T_solver, 8192x8192 grid at
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
         --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
 
+Launch: under torchrun (WORLD_SIZE set) this process is one rank and
+`--gpus` must equal WORLD_SIZE.  Without a launcher, `--gpus N > 1` starts
+the N ranks itself: it checks (without initialising HIP) that N GPUs are
+visible — fewer is an error, never a silent 1-rank run — and runs
+`torch.distributed.run --nproc-per-node N bench.py …` as a child process,
+relaying rank 0's JSON line and returning the job's exit status (the
+reference's stage 4 runs as N MPI ranks on N GPUs,
+stage4-mpi+cuda/poisson_mpi_cuda2.cu:986-990).
+
 A *step* is one full PCG iteration of the global solve on N GPUs (the
 single-sweep kernel with its 7 sums summed over ranks inside the sweep over
 xGMI P2P, and the halo rows — row-slab blocks — pushed by the same sweep into
-the neighbours' receive buffers, or exchanged through RCCL otherwise).  The timed region runs exactly K steps from the start of a fresh
-solve (w⁰ = 0, as the reference) with the convergence test switched off so
-every step does full work; it is bracketed by a barrier + device synchronise
-on both sides and the max over ranks is reported (each rank's clock stops at
-its closing device synchronise, before the closing CPU barrier: the ranks are
-coupled every iteration by the in-sweep sums, so the max over ranks is the
-job's time, without the gloo barrier's ~0.1-0.3 ms, which at 8 ranks would be
-≈10 % of a 20-step window).  `value` = job-wide PCG
-iterations/s (the grid is fixed → strong scaling).  Outside the timed region
-the script also runs one complete solve to convergence and reports T_solver,
-its iteration count and the L2 error against the analytic solution.
+the neighbours' receive buffers, or exchanged through RCCL otherwise).  The
+timed region runs exactly K steps from the start of a fresh solve (w⁰ = 0, as
+the reference) with the convergence test switched off so every step does full
+work; it is bracketed by a barrier + device synchronise on both sides and the
+max over ranks is reported (each rank's clock stops at its closing device
+synchronise, before the closing CPU barrier: the ranks are coupled every
+iteration by the in-sweep sums, so the max over ranks is the job's time,
+without the gloo barrier's ~0.1-0.3 ms, which at 8 ranks would be ≈10 % of a
+20-step window).  `value` = job-wide PCG iterations/s (the grid is fixed →
+strong scaling).  Outside the timed region the script also runs one complete
+solve to convergence (w⁰ = 0: T_solver, iterations, L2 error against the
+analytic solution, timer breakdown incl. the cross-rank wait) and one with
+the BASELINE's random-init w⁰ (`random_init`; the reference has no random
+init, so its iteration count is parity-unpinned).
+
+Every multi-rank wait is bounded: PE_P2P_TIMEOUT_S (default 30 s here) on
+the in-sweep cross-rank sums, PE_WATCHDOG_S (default 60 s here) on every host
+wait of the timed region and the solves (the communicator is aborted and the
+rank exits non-zero; torchrun then ends the job).
 
 vs_baseline: the reference never ran 8192²; BASELINE.md §1b extrapolates one
 P100 to ≈270 s for its 5889 iterations = 21.8 iterations/s, which is the
@@ -32,42 +49,121 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import signal
+import socket
+import subprocess
 import sys
 import time
-
-import torch
 
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, REPO)
 
-from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem, native  # noqa: E402
-from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D  # noqa: E402
-from poisson_ellipse_openmp_mpi_cuda_amd.parallel import dist as PD  # noqa: E402
-
 P100_ITERS_PER_S_8192 = 5889 / 270.0  # BASELINE.md §1b extrapolation (1× P100)
 
 
-def main() -> int:
+def parse_args(argv):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
     ap.add_argument("--grid", type=int, nargs="+", default=[8192, 8192])
     ap.add_argument("--decomp", default="device", help="device | aspect | reference | rows | cols | <Px>x<Py>")
-    ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solve")
+    ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solves")
+    ap.add_argument("--no-random-solve", action="store_true", help="skip the (untimed) random-init solve")
+    ap.add_argument("--seed", type=int, default=1234, help="random-init w0 seed")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused"))
     ap.add_argument("--launch", default="graph", choices=("graph", "eager"),
                     help="timed steps replayed from instantiated hipGraphs (default) or launched eagerly")
-    a = ap.parse_args()
-    M, N = (a.grid[0], a.grid[-1])
+    return ap.parse_args(argv)
 
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _visible_gpus() -> int:
+    """GPUs this process could open, without initialising HIP in it (the ranks
+    are separate processes; torch.cuda.device_count() does not initialise the
+    device on this image)."""
+    import torch
+
+    return int(torch.cuda.device_count())
+
+
+def launch_ranks(a, argv) -> int:
+    """Parent of an N-rank run started without a launcher."""
+    n = _visible_gpus()
+    shared = os.environ.get("PE_COMM") == "host"  # test transport: ranks may share one GPU
+    if n < 1 or (n < a.gpus and not shared):
+        print(f"[bench] --gpus {a.gpus} needs {a.gpus} visible GPUs, this node has {n}", file=sys.stderr)
+        return 2
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(a.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__), *argv]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+
+    def _die_with_parent():  # the launcher never outlives this process
+        try:
+            import ctypes
+
+            ctypes.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+        except OSError:
+            pass
+
+    p = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, start_new_session=True,
+                         preexec_fn=_die_with_parent)
+
+    def _forward(sig, _frame):
+        try:
+            os.killpg(p.pid, sig)
+        except ProcessLookupError:
+            pass
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, _forward)
+    assert p.stdout is not None
+    for line in p.stdout:  # rank 0's JSON line → stdout; anything else → stderr
+        (sys.stdout if line.startswith("{") else sys.stderr).write(line)
+        sys.stdout.flush()
+    rc = p.wait()
+    if rc != 0:
+        print(f"[bench] {a.gpus}-rank job failed (exit {rc})", file=sys.stderr)
+    return rc
+
+
+def main(argv=None) -> int:
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse_args(argv)
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        return launch_ranks(a, argv)
+
+    # bounded multi-rank waits (read by the comm / solver constructors)
+    os.environ.setdefault("PE_P2P_TIMEOUT_S", "30")
+    os.environ.setdefault("PE_WATCHDOG_S", "60")
+
+    import torch
+
+    from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem, native
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import dist as PD
+
+    M, N = (a.grid[0], a.grid[-1])
     rank, world, local = PD.env_rank_world()
     if world != a.gpus:
-        print(f"[bench] warning: --gpus {a.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+        print(f"[bench] --gpus {a.gpus} but the launcher started WORLD_SIZE={world} ranks", file=sys.stderr)
+        return 2
     nat = native()
-    if nat.device_count() < 1:
+    ndev = nat.device_count()
+    if ndev < 1:
         print("[bench] no HIP device visible", file=sys.stderr)
+        return 2
+    if world > ndev and os.environ.get("PE_COMM") != "host":
+        print(f"[bench] {world} ranks but only {ndev} GPUs visible (one GPU per rank)", file=sys.stderr)
         return 2
     ctx = None
     comm = None
@@ -78,6 +174,9 @@ def main() -> int:
 
         cpu_group = dist.new_group(backend="gloo")
         comm = PD.rccl_comm(ctx)
+        if comm.size != world:
+            print(f"[bench] communicator has {comm.size} ranks, WORLD_SIZE={world}", file=sys.stderr)
+            return 2
     else:
         nat.set_device(0)
     torch.cuda.set_device(local % max(1, torch.cuda.device_count()))
@@ -105,6 +204,22 @@ def main() -> int:
         t = torch.tensor([x], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX, group=cpu_group)
         return float(t[0])
+
+    def gather(obj):
+        if world == 1:
+            return [obj]
+        import torch.distributed as dist
+
+        out = [None] * world
+        dist.all_gather_object(out, obj, group=cpu_group)
+        return out
+
+    dev = nat.current_device()
+    me = {"rank": rank, "local_rank": local, "device": dev, "pci_bus_id": nat.device_pci_bus_id(dev),
+          "block": [blk.nx, blk.ny],
+          "placement_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
+          "placement_chosen": solver.placement_choice, "construct_s": round(solver.construct_s, 3)}
+    ranks_info = gather(me)
 
     # warmup: first-touch / RCCL connections, then instantiate every chunk
     # graph the timed run will launch (no capture inside the timed region)
@@ -139,12 +254,25 @@ def main() -> int:
         res = solver.solve()
         tm = res.timers
         extra = dict(t_solver_s=maxval(tm["solver"]), t_setup_s=maxval(tm["setup"]), t_iterate_s=maxval(tm["iterate"]),
-                     t_breakdown_s={k: maxval(tm[k]) for k in ("gpu", "dot", "halo", "reduce", "copy")},
+                     t_breakdown_s={k: maxval(tm[k]) for k in ("gpu", "dot", "halo", "reduce", "wait", "copy")},
                      iters_converged=int(res.iters), converged=bool(res.converged),
                      l2_err=float(res.l2_err), max_err=float(res.max_err),
                      solve_iters_per_s=float(res.iters) / maxval(tm["iterate"]))
+        if not a.no_random_solve:
+            # BASELINE's "random-init w0": same solver, w0 = amp·hash(global
+            # node, seed) (decomposition-independent); T_solver here has no
+            # construction in it (counted once, by the first solve)
+            solver.set_init(nat.Init.Random, a.seed, 0.05)
+            barrier()
+            rr = solver.solve()
+            solver.set_init(nat.Init.Zero, a.seed, 0.05)
+            extra["random_init"] = dict(seed=a.seed, amp=0.05, iters=int(rr.iters), converged=bool(rr.converged),
+                                        t_solver_s=maxval(rr.timers["solver"]),
+                                        t_iterate_s=maxval(rr.timers["iterate"]), l2_err=float(rr.l2_err),
+                                        parity="unpinned vs reference (the reference has only w0 = 0)")
 
     ips = a.steps / dt
+    pcis = sorted({r["pci_bus_id"] for r in ranks_info})
     out = {
         "metric": "pcg_iters_per_sec_8192x8192" if (M, N) == (8192, 8192) else f"pcg_iters_per_sec_{M}x{N}",
         "value": ips,
@@ -172,6 +300,9 @@ def main() -> int:
             "algo": "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else "classic (2 kernels, 2 allreduces / iter)",
             "decomposition": {"spec": a.decomp, "Px": blk.Px, "Py": blk.Py, "block": [blk.nx, blk.ny]},
             "transport": comm.name if comm is not None else "none",
+            "comm_ranks": comm.size if comm is not None else 1,
+            "distinct_gpus": len(pcis),
+            "ranks": ranks_info,
             "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
             "halo": ("in-sweep xGMI push (graph-captured)" if solver.halo_push else
                      ("exchange: " + comm.name)) if world > 1 else "none",
@@ -184,7 +315,8 @@ def main() -> int:
             "chunk": solver.chunk,
             "launch": a.launch,
             "placement": {"candidates_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
-                          "chosen": solver.placement_choice, "search_s": round(solver.placement_s, 3)},
+                          "chosen": solver.placement_choice, "search_s": round(solver.placement_s, 3),
+                          "job_ms_per_sweep": round(solver.placement_job_ms, 4)},
             "construct_s": round(solver.construct_s, 3),
         },
         "valid": valid,

@@ -30,6 +30,7 @@ py::dict timers_dict(const Timers& t) {
   d["iterate"] = t.iterate;
   d["construct"] = t.construct;
   d["sampled"] = t.sampled;
+  d["wait"] = t.wait;
   d["dot_fused"] = t.dot_fused;
   return d;
 }
@@ -169,6 +170,7 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("Py", &SolveResult::Py)
       .def_readonly("backend", &SolveResult::backend)
       .def_readonly("algo", &SolveResult::algo)
+      .def_readonly("resident_fallback", &SolveResult::resident_fallback)
       .def_property_readonly("timers", [](const SolveResult& r) { return timers_dict(r.t); });
 
   m.def("format_result_legacy", &format_result_legacy);
@@ -259,6 +261,8 @@ PYBIND11_MODULE(_native, m) {
   m.def("device_count", &device_count);
   m.def("set_device", &set_device);
   m.def("device_name", &device_name);
+  m.def("current_device", &current_device);
+  m.def("device_pci_bus_id", &device_pci_bus_id, py::arg("dev"));
   m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
 
   py::class_<CommHandle>(m, "DeviceComm")
@@ -380,6 +384,7 @@ PYBIND11_MODULE(_native, m) {
            },
            py::arg("iters"), py::arg("use_graph") = true)
       .def("set_check_tol", &DeviceSolver::set_check_tol, py::arg("on"))
+      .def("set_init", &DeviceSolver::set_init, py::arg("init"), py::arg("seed") = 1234, py::arg("amp") = 0.05)
       .def("relayout", &DeviceSolver::relayout, py::arg("ti"), py::arg("order") = -1)
       .def("prepare_graphs",
            [](DeviceSolver& s, int64_t n) {
@@ -419,6 +424,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("resident", &DeviceSolver::resident)
+      .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def_property_readonly("halo_push", &DeviceSolver::halo_push,
                              "halo rows pushed by the sweep over xGMI (no exchange call; graph-capturable)")
@@ -428,6 +434,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("placement_ms", &DeviceSolver::placement_ms)
       .def_property_readonly("placement_choice", &DeviceSolver::placement_choice)
       .def_property_readonly("placement_s", &DeviceSolver::placement_seconds)
+      .def_property_readonly("placement_job_ms", &DeviceSolver::placement_job_ms)
       .def_property_readonly("construct_s", &DeviceSolver::construct_seconds)
       .def_property_readonly("exchange_us", &DeviceSolver::exchange_us)
       .def_property_readonly("ti_tuning_ms", &DeviceSolver::ti_tuning_ms)

@@ -38,13 +38,14 @@ std::string format_result_legacy(const Problem& P, const SolveResult& r, int nra
   } else {  // stage4 (GPU)
     // Labels verbatim (parity); values are the device solver's honest
     // categories: "GPU compute" = every compute kernel, "MPI halo exchange"
-    // = exchange + allreduce launches (the reference lumps them, :870-873),
+    // = exchange + allreduce launches + the in-sweep cross-rank wait (the
+    // reference lumps halo and allreduces, :870-873, :891-895, :924-928),
     // the preconditioner runs inside the sweep kernel (no separate time),
     // the dot products are the reduction kernel unless fused into the sweep.
     std::ostringstream t;
     t << "   GPU compute time (Ap + D^{-1}r, max over ranks) ~ " << r.t.gpu << " s\n";
     t << "   Host<->Device copy time (max over ranks)        ~ " << r.t.copy << " s\n";
-    t << "   MPI halo exchange time (max over ranks)         ~ " << (r.t.halo + r.t.reduce) << " s\n";
+    t << "   MPI halo exchange time (max over ranks)         ~ " << (r.t.halo + r.t.reduce + r.t.wait) << " s\n";
     t << "   Preconditioner CPU part time (max over ranks)   ~ n/a (fused into the GPU sweep)\n";
     if (r.t.dot_fused)
       t << "   Dot products time (max over ranks)              ~ n/a (fused into the GPU sweep)\n";

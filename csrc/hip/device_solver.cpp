@@ -17,6 +17,7 @@
 #include <chrono>
 #include <cmath>
 #include <cstdio>
+#include <cstddef>
 #include <cstring>
 #include <deque>
 #include <map>
@@ -134,6 +135,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   std::memset(hst_, 0, sizeof(DevState) * 2);
   PE_HIP_CHECK(hipEventCreateWithFlags(&ev_[0], hipEventDisableTiming));
   PE_HIP_CHECK(hipEventCreateWithFlags(&ev_[1], hipEventDisableTiming));
+  PE_HIP_CHECK(hipEventCreateWithFlags(&ev_sync_, hipEventDisableTiming));
   PE_HIP_CHECK(hipEventCreate(&t0_));
   PE_HIP_CHECK(hipEventCreate(&t1_));
 
@@ -180,10 +182,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (const char* e = std::getenv("PE_FAULT_INJECT")) {
     const std::string f = e;
     if (f.rfind("nan@iter:", 0) == 0) k.fault_iter = std::atoll(f.c_str() + 9);
+    if (f.rfind("zero@iter:", 0) == 0) k.fault_zero = std::atoll(f.c_str() + 10);
     if (f == "stall") fault_stall_ = true;
     // stall@rank:R — only rank R hangs (its watchdog fires and aborts the
     // communicator; the peers then see the transport fail, not a hang)
     if (f.rfind("stall@rank:", 0) == 0 && std::atoi(f.c_str() + 11) == blk_.rank) fault_stall_ = true;
+    // slow@rank:R,us:X — rank R's sweeps idle X µs before their cross-rank
+    // sum (the peers' T_MPI must show it: iterations × X)
+    if (f.rfind("slow@rank:", 0) == 0 && std::atoi(f.c_str() + 10) == blk_.rank) {
+      const size_t u = f.find("us:");
+      k.slow_ticks = u == std::string::npos ? 0 : (long long)(std::atof(f.c_str() + u + 3) * 100.0);
+    }
   }
   if (const char* e = std::getenv("PE_WATCHDOG_S")) watchdog_s_ = std::atof(e);
   if (opt_.keep_history) {  // per-iteration ‖Δw‖ on the device (capped at 2²⁴ iterations)
@@ -352,7 +361,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // separate allreduce launch.
   if (fused_ && comm_->size() > 1 && comm_->peer_sum()) {
     const char* e = std::getenv("PE_XR");
-    if (!(e && std::atoi(e) == 0)) k.xr = *comm_->peer_sum();
+    if (!(e && std::atoi(e) == 0)) {
+      k.xr = *comm_->peer_sum();
+      k.xr.wait_acc = &st_->xr_wait;  // T_MPI of the in-sweep sum (DevState::xr_wait, xr_n)
+    }
   }
   // In-kernel item-sum fold for dynamic sweeps, opt-in (PE_FOLD=1): it saves
   // the reduction kernel (≈10 µs + a launch gap per iteration at 8192²) but
@@ -395,6 +407,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   int c = int(0.5e-3 / t_iter);
   c = std::max(8, std::min(128, c));
   c += c & 1;
+  stream_chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   mark("tuning+rest");
@@ -498,11 +511,21 @@ void DeviceSolver::setup_halo_push() {
 
 void DeviceSolver::relayout(int ti, int order) {
   if (!fused_ || resident_) return;
-  if (order == 0 || order == 3) kp_->order = order;  // static LPT list / dynamic per-XCD queue
+  ti = std::max(2, std::min(ti, 64));
+  const int ord = (order == 0 || order == 3) ? order : kp_->order;  // static LPT list / dynamic per-XCD queue
+  // the item-sum slots and the fold buffer were sized at construction: a
+  // layout that needs more is refused before anything changes
+  const int64_t nitems = int64_t(kp_->nstrips) * ((blk_.nx + ti - 1) / ti);
+  const int64_t need = (ord == 0 ? ti + 1 : 2) * nitems + 64;
+  if (need > nslot_cap_ || (kp_->fold && ord != 3))
+    throw std::invalid_argument("relayout: " + std::to_string(ti) + " rows per item (order " + std::to_string(ord) +
+                                ") needs " + std::to_string(need) + " item-sum slots, " + std::to_string(nslot_cap_) +
+                                " allocated");
+  kp_->order = ord;
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
   for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));
   graphs_.clear();
-  set_items(std::max(2, std::min(ti, 64)));
+  set_items(ti);
   setup_items();
 }
 
@@ -511,6 +534,12 @@ void DeviceSolver::set_check_tol(bool on) {
   kp_->check_tol = on ? 1 : 0;
   for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured with the old parameters
   graphs_.clear();
+}
+
+void DeviceSolver::set_init(Init init, uint64_t seed, double amp) {
+  opt_.init = init;
+  opt_.seed = seed;
+  opt_.init_amp = amp;
 }
 
 void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
@@ -561,6 +590,7 @@ DeviceSolver::~DeviceSolver() {
   for (auto& g : graphs_) (void)hipGraphExecDestroy(g.second);
   (void)hipEventDestroy(ev_[0]);
   (void)hipEventDestroy(ev_[1]);
+  (void)hipEventDestroy(ev_sync_);
   (void)hipEventDestroy(t0_);
   (void)hipEventDestroy(t1_);
   for (const PhaseRec& r : recs_) {
@@ -932,7 +962,9 @@ void DeviceSolver::wait_event(hipEvent_t ev) {
       throw std::runtime_error("watchdog: device made no progress for " + std::to_string(watchdog_s_) +
                                " s (communicator aborted)");
     }
-    std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // spin for the first 2 ms (a bench's closing wait stays exact), then poll
+    if (secs(t0, clk::now()) > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    else std::this_thread::yield();
   }
 }
 
@@ -945,7 +977,14 @@ void DeviceSolver::read_state(DevState* out) {
   PE_HIP_CHECK(hipStreamSynchronize(stream_));
 }
 
-void DeviceSolver::synchronize() { PE_HIP_CHECK(hipStreamSynchronize(stream_)); }
+void DeviceSolver::synchronize() {
+  if (watchdog_s_ <= 0 && !fault_stall_) {
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    return;
+  }
+  PE_HIP_CHECK(hipEventRecord(ev_sync_, stream_));
+  wait_event(ev_sync_);
+}
 
 void DeviceSolver::reset() {
   par_ = 0;
@@ -1047,6 +1086,7 @@ SolveResult DeviceSolver::solve() {
   std::deque<Flight> inflight;
   int64_t nchunk = 0;
   bool stop = false;
+  bool res_abort = false;  // a resident launch's grid barrier timed out (status 5)
   for (;;) {
     while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
       const bool sample = sample_every > 0 && nchunk % sample_every == 0;
@@ -1075,6 +1115,33 @@ SolveResult DeviceSolver::solve() {
         while (next_ck <= enq) next_ck += ck_every;
         continue;
       }
+      if (res_abort) {
+        // Resident fallback: the aborted launch wrote nothing back (and the
+        // chunk after it saw `done` and did nothing), so the device holds the
+        // state from before it.  Clear the abort, switch this solver to the
+        // streaming sweep and continue from that iteration.
+        res_abort = false;
+        DevState s0;
+        read_state(&s0);
+        if (s0.status == 5) {
+          std::fprintf(stderr, "[pe] rank %d: resident kernel barrier timed out at iteration %lld; "
+                               "continuing with the streaming sweep\n", blk_.rank, (long long)s0.iter);
+          PE_HIP_CHECK(hipMemsetAsync(reinterpret_cast<char*>(st_) + offsetof(DevState, done), 0, 2 * sizeof(int),
+                                      stream_));
+          resident_ = false;
+          resident_fallback_ = true;
+          chunk_ = stream_chunk_;
+          par_ = int(s0.iter & 1);
+          enq = s0.iter;
+          // the drained records: keep the samples of the iterations that ran
+          harvest(recs_.size());
+          samples_.erase(std::remove_if(samples_.begin(), samples_.end(),
+                                        [&](const PhaseSample& x) { return x.iter >= s0.iter; }),
+                         samples_.end());
+          stop = false;
+          continue;
+        }
+      }
       break;
     }
     const Flight f = inflight.front();
@@ -1084,7 +1151,10 @@ SolveResult DeviceSolver::solve() {
     const size_t done_recs = std::min(f.nrec, recs_.size());
     harvest(done_recs);
     for (Flight& g : inflight) g.nrec -= std::min(g.nrec, done_recs);
-    if (hst_[f.slot].done) stop = true;
+    if (hst_[f.slot].done) {
+      stop = true;
+      if (hst_[f.slot].status == 5 && resident_) res_abort = true;
+    }
     if (opt_.log_every > 0 && blk_.rank == 0 && hst_[f.slot].iter >= next_log) {  // chunk-granular progress log
       std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[f.slot].iter,
                    hst_[f.slot].last_diff, hst_[f.slot].rz_cur);
@@ -1111,7 +1181,9 @@ SolveResult DeviceSolver::solve() {
   res.converged = hs.status == 1;
   res.breakdown = hs.status == 2;
   res.nonfinite = hs.status == 4;
-  if (hs.status == 5) throw std::runtime_error("single-sweep: boundary partials never arrived (internal error)");
+  res.resident_fallback = resident_fallback_;
+  if (resident_fallback_) res.algo = "fused (resident fallback)";
+  if (hs.status == 5) throw std::runtime_error("single-sweep: internal error (status 5: a grid barrier or item sums never completed)");
   res.last_diff = hs.last_diff;
   if (hist_ && hs.iter > 0) {
     res.history.resize(size_t(std::min<long long>(hs.iter, kp_->hist_n)));
@@ -1153,14 +1225,18 @@ SolveResult DeviceSolver::solve() {
     res.t.reduce = sum[kPhReduce] * scale;
     res.t.copy = copy_s + (ncopy > 0 ? sum[kPhCopy] * double(chunks_run) / double(ncopy) : 0.0);
     res.t.sampled = double(nit);
+    // in-sweep cross-rank sum: the final blocks' wait for the peers' flags
+    // (ticks of the 100 MHz s_memrealtime clock)
+    res.t.wait = double(hs.xr_wait) * 1e-8;
     res.t.dot_fused = !(fused_ && kp_->order == 3 && !kp_->fold);
     if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
   }
   res.t.solver = construct + secs(t_start, clk::now());
   // Timers: max over ranks (reference MPI_Reduce(MAX), :962-966).
   double tv[10] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate,
-                   res.t.dot, res.t.construct, 0};
+                   res.t.dot, res.t.construct, res.t.wait};
   comm_->host_max(tv, 10, stream_);
+  res.t.wait = tv[9];
   res.t.gpu = tv[0];
   res.t.copy = tv[1];
   res.t.halo = tv[2];

@@ -131,12 +131,19 @@ __device__ __forceinline__ double2 ldw(const double* p) {
 // Pointwise w += a1·p_{k-1} + a2·p_k over the owned nodes (rare paths:
 // convergence / iteration cap in a deferring sweep, breakdown, host flush).
 // p_k = zc·D⁻¹r_{k-1} + β p_{k-1} from the input buffer xin.
+// (1/D from the march's own division-free coefficient path, cset_rc, so p_k
+// has the bits the sweep would have produced.)
 __device__ void w_pointwise(const KParams& k, const double* xin, double a1, double a2, double zc, double beta) {
   const int64_t n = k.nx * k.ny;
   for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * blockDim.x) {
     const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
     const double r = xin[li * k.pitch + lj], pold = xin[li * k.pitch + k.poff + lj];
-    const double pk = zc * (r * cset_mem<false>(k, li, lj).d) + beta * pold;
+    const int* rc = k.rowcls + (li + 1) * 4;
+    const double* ctr = k.colT + (li + 1) * 4;
+    const double* tv = k.rowT + (lj + 1) * 4;
+    const double d = cset_rc(k, RowCls{rc[0], rc[1], rc[2], rc[3]}, CT{ctr[0], ctr[4], ctr[1], ctr[2]}, lj,
+                             TV{tv[0], tv[1], tv[2], tv[6]}).d;
+    const double pk = zc * (r * d) + beta * pold;
     double& w = k.w[li * k.wpitch + lj];
     w = w + a1 * pold + a2 * pk;
   }
@@ -182,8 +189,11 @@ template <int WM>
 __device__ __forceinline__ Term sweep_term(const KParams& k, const Scal& c) {
   Term t{false, false, false, false};
   if (c.first) return t;
-  t.bad = !isfinite(c.den) || !isfinite(c.g) || !isfinite(c.diff);
-  t.brk = t.bad || fabs(c.den) < 1e-15;
+  // breakdown first (reference :413 tests |den| before α exists); a
+  // non-finite ‖Δw‖ only matters when α was formed
+  const bool tiny = fabs(c.den) < 1e-15;
+  t.bad = !isfinite(c.den) || !isfinite(c.g) || (!tiny && !isfinite(c.diff));
+  t.brk = t.bad || tiny;
   t.conv = k.check_tol && c.diff < k.tol;
   t.last = !t.brk && WM == 0 && (t.conv || c.kiter >= k.max_iter);
   return t;
@@ -217,6 +227,8 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
 #pragma unroll
   for (int n = 0; n < 7; ++n) st->fs[par][n] = t[n];
   if (k.fault_iter > 0 && c.kiter == k.fault_iter) st->fs[par][1] = __builtin_nan("");  // PE_FAULT_INJECT=nan@iter:K
+  if (k.fault_zero > 0 && c.kiter == k.fault_zero)  // PE_FAULT_INJECT=zero@iter:K: den of the next sweep = 0
+    st->fs[par][1] = st->fs[par][2] = st->fs[par][3] = 0.0;
   st->wpend = WM == 0 ? 1 : 0;
   st->wpar = par;
   if (c.first) {
@@ -245,6 +257,13 @@ __device__ __forceinline__ void sweep_finalize(const KParams& k, DevState* st, i
 // sums t are valid in thread 0): with a P2P transport (k.xr) the 7 sums are
 // summed over ranks right here (peer_sum.hpp) — the iteration then needs no
 // allreduce launch — then thread 0 updates the state.
+__device__ __forceinline__ void slow_inject(const KParams& k) {
+  if (k.slow_ticks > 0) {  // PE_FAULT_INJECT=slow@rank (test hook): idle before the cross-rank sum
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < k.slow_ticks) __builtin_amdgcn_s_sleep(2);
+  }
+}
+
 template <int WM>
 __device__ __forceinline__ void finalize_block(const KParams& k, DevState* st, int par, const Scal& sc,
                                                double (&t)[7]) {
@@ -252,6 +271,7 @@ __device__ __forceinline__ void finalize_block(const KParams& k, DevState* st, i
   __shared__ unsigned long long sseq;
   __shared__ int sok;
   if (k.xr.peers) {
+    if (threadIdx.x == 0) slow_inject(k);
     if (threadIdx.x == 0)
 #pragma unroll
       for (int n = 0; n < 7; ++n) v[n] = t[n];
@@ -267,7 +287,10 @@ __device__ __forceinline__ void finalize_block(const KParams& k, DevState* st, i
 template <int WM>
 __device__ __forceinline__ void finalize_wave(const KParams& k, DevState* st, int par, const Scal& sc,
                                               double (&t)[7]) {
-  if (k.xr.peers) peer_sum_wave(k.xr, t, 7);
+  if (k.xr.peers) {
+    slow_inject(k);
+    peer_sum_wave(k.xr, t, 7);
+  }
   if ((threadIdx.x & 63) == 0) sweep_finalize<WM>(k, st, par, sc, t);
 }
 
@@ -540,9 +563,12 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       } else {
         w_pointwise(k, k.x[par ^ 1], 0.0, alpha, zc, beta);
       }
-      if ((!persum || FOLD) && arrive_last(&st->ticket[0], gridDim.x, &sflag) && threadIdx.x == 0) {
+      // A wave reaches this point after its first item's prologue or after
+      // an empty walk — different program points within one workgroup — so
+      // the hand-off counts waves (no workgroup barrier on this path).
+      if ((!persum || FOLD) && arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
         sweep_terminal(k, st, sc, tm);
-        __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return true;
     }

@@ -453,6 +453,7 @@ void DeviceSolver::setup_resident() {
   const int per_cu = dev::resident_max_blocks_per_cu(lds);
   const int nwg = ntr * nstrips;
   if (per_cu < 1 || nwg > per_cu * cus) return;
+  if (nwg > dev::kResMaxTiles) return;  // the kernel's sum gather covers 256 tiles (parts with > 256 CUs)
   rp_ = std::make_unique<dev::ResParams>();
   dev::ResParams& r = *rp_;
   std::memset(&r, 0, sizeof(r));
@@ -482,6 +483,8 @@ void DeviceSolver::setup_resident() {
   r.edges = res_buf_;
   r.partials = res_buf_ + nedge;
   r.ctr = res_ctr_;
+  r.fault_wg = -1;
+  if (const char* f = std::getenv("PE_FAULT_INJECT"); f && std::string(f) == "resbarrier") r.fault_wg = nwg - 1;
   resident_ = true;
 }
 

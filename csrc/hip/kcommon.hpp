@@ -188,11 +188,33 @@ __device__ __forceinline__ bool arrive_last(unsigned* ticket, unsigned nblocks, 
   return *sflag != 0;
 }
 
+// Wave-level form of arrive_last for paths that waves of one workgroup reach
+// at different program points (no workgroup barrier): every wave of the grid
+// drains and releases its stores, then lane 0 takes a ticket counted against
+// all `nwaves` waves; true (wave-uniform) in the wave that arrives last, after
+// its acquire.
+__device__ __forceinline__ bool arrive_last_wave(unsigned* ticket, unsigned nwaves) {
+  int last = 0;
+  if ((threadIdx.x & 63) == 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = (t == nwaves - 1);
+    if (last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
+  return __builtin_amdgcn_readfirstlane(last) != 0;
+}
+
 // Write-through form of arrive_last for a block's N partial sums (thread 0
 // holds them): stored `sc1` (relaxed agent-scope atomic stores), drained,
 // then the ticket — no per-block L2 write-back (`buffer_wbl2`, ≈1.7-6.5 µs
 // on a dirty L2, paid by every block of the grid); the last arriver does
-// the agent acquire before reading (MI355X_MICROARCH.md, visibility recipe R1).
+// the agent acquire before reading (the image's CDNA4 guide,
+// /opt/skills/guides/MI355X_MICROARCH.md — not part of this repo — visibility recipe R1).
 template <int N>
 __device__ __forceinline__ bool publish_last(double* dst, const double (&v)[N], unsigned* ticket, unsigned nblocks,
                                              int* sflag) {

@@ -35,8 +35,9 @@ struct DevState {
   long long iter;    // completed iterations
   int done;          // 1 → every later kernel is a no-op
   int status;        // 0 running, 1 converged, 2 breakdown, 3 iteration cap, 4 non-finite scalars, 5 internal
-  unsigned ticket[4];
-  unsigned pad[4];
+  unsigned ticket[5];  // last-arriver tickets: [0] sweep / F, [1] reduction / G, [2] init, [3] error,
+                       // [4] single-sweep terminal path (counts waves)
+  unsigned pad[3];
   // Single-sweep (fused) PCG: the 7 local/global sums of sweep k live in
   // fs[k & 1] = {(r,z), (z,Az), (z,s), (p,s), (z,z), (z,p), (p,p)}, unweighted.
   double fs[2][8];
@@ -47,6 +48,13 @@ struct DevState {
   int pad2;
   unsigned qhead[8][16];  // single-sweep work queue heads, one 64-B line per XCD shard
   unsigned long long sig;  // overlap: boundary items stored, cumulative over the solve's sweeps
+  // In-sweep cross-rank sum (KParams::xr): s_memrealtime ticks (100 MHz) the
+  // final block spent waiting for the peers' flags, summed over the solve's
+  // sweeps, and the number of such waits — the T_MPI of the default
+  // multi-rank path (the halo push's delivery is signalled by the same flags,
+  // so its wait is inside this one).
+  unsigned long long xr_wait;
+  unsigned long long xr_n;
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
@@ -59,6 +67,9 @@ struct PeerSum {
   unsigned long long* seq;
   int me, P;
   long long timeout_ticks;
+  // non-null: the ticks spent waiting for the peers' flags are added here
+  // (and one count at wait_acc[1]) — DevState::xr_wait of the solver
+  unsigned long long* wait_acc;
 };
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
@@ -105,6 +116,7 @@ struct KParams {
   double* itemsum;               // dynamic single-sweep: per-item sums [nslots][8]
   int nslots;                    // item-sum slots: list entries (listed walk) or nitems
   long long fault_iter;          // > 0: poison the reduced sums after this iteration (PE_FAULT_INJECT=nan@iter:K)
+  long long fault_zero;          // > 0: zero the (p, A p) sums after this iteration → breakdown (zero@iter:K)
   double* hist;                  // keep_history: ‖Δw‖ of iteration k at hist[k-1] (k ≤ hist_n)
   long long hist_n;
   // Item lists (dynamic sweeps, setup_items): entries {first row, strip |
@@ -153,6 +165,9 @@ struct KParams {
   unsigned* gcnt;
   unsigned* xcnt;
   double* gsum;
+  // PE_FAULT_INJECT=slow@rank:R,us:X — this rank's final reduction block
+  // idles X µs (in ticks) before the cross-rank sum (T_MPI test hook)
+  long long slow_ticks;
 };
 constexpr int kFoldGroup = 64;
 
@@ -182,7 +197,8 @@ struct ResParams {
   const int* rowstart;               // ntr+1: first local row of band tr (rowstart[ntr] = nx + 1)
   double* edges;                     // [2][nwg][kResEdge]
   double* partials;                  // [2][nwg][8]
-  unsigned* ctr;                     // [8][32] barrier counters (zeroed before every launch)
+  unsigned* ctr;                     // [8][32] barrier counters (zeroed before every launch);
+                                     // ctr[16]: workgroups past their entry state reads
   int niter;                         // iterations of this launch
   int par0;                          // parity of its first iteration
   long long timeout_ticks;           // barrier wait limit (s_memrealtime ticks, 100 MHz)
@@ -190,8 +206,13 @@ struct ResParams {
   // PE_RES_STAMPS=1 diagnostic: s_memrealtime of every workgroup at 8 points
   // of its first kResStampIters iterations, [nwg][kResStampIters][8] (null: off)
   unsigned long long* stamps;
+  // PE_FAULT_INJECT=resbarrier: this workgroup never arrives at the first
+  // grid barrier (-1: none) — the barrier times out, the launch aborts with
+  // status 5 and the solver must fall back to the streaming sweep
+  int fault_wg;
 };
 constexpr int kResStampIters = 64;
+constexpr int kResMaxTiles = 256;  // the per-iteration sum gather reads ≤ 4 × 64 tile partials
 size_t resident_lds_bytes(int rcap, int nbcap);
 // Launch n iterations (the caller zeroes rp.ctr on the same stream first).
 void launch_resident(const KParams& k, const ResParams& rp, hipStream_t s);

@@ -25,13 +25,17 @@
 namespace pe {
 namespace dev {
 
+// The wait (from this rank's flag release to the last peer's flag) is
+// accumulated into ps.wait_acc when set: the cross-rank part of T_MPI.
 __device__ __forceinline__ void peer_sum_block(const PeerSum& ps, double* v, int n, unsigned long long* sseq,
                                                int* sok) {
+  unsigned long long tw = 0;
   if (threadIdx.x == 0) {
     const unsigned long long q = *ps.seq + 1;
     *ps.seq = q;
     *sseq = q;
     *sok = 1;
+    tw = __builtin_amdgcn_s_memrealtime();
   }
   __syncthreads();
   const unsigned long long seq = *sseq;
@@ -54,6 +58,10 @@ __device__ __forceinline__ void peer_sum_block(const PeerSum& ps, double* v, int
     }
   }
   __syncthreads();
+  if (threadIdx.x == 0 && ps.wait_acc) {
+    ps.wait_acc[0] += __builtin_amdgcn_s_memrealtime() - tw;
+    ps.wait_acc[1] += 1;
+  }
   if (t < n) {
     double s = 0.0;
     for (int r = 0; r < ps.P; ++r)
@@ -79,6 +87,7 @@ __device__ __forceinline__ void peer_sum_wave(const PeerSum& ps, double* v, int 
       ((unsigned long long)__builtin_amdgcn_readfirstlane(int(q >> 32)) << 32);
   const size_t set = size_t(q & 1);
   int ok = 1;
+  const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
   if (lane < ps.P) {
     double* dst = ps.peers[lane] + (set * size_t(ps.P) + size_t(ps.me)) * kP2PSlot;
     for (int i = 0; i < n; ++i) dst[i] = v[i];
@@ -96,6 +105,10 @@ __device__ __forceinline__ void peer_sum_wave(const PeerSum& ps, double* v, int 
     }
   }
   const bool all_ok = __ballot(ok == 0) == 0ull;
+  if (lane == 0 && ps.wait_acc) {
+    ps.wait_acc[0] += __builtin_amdgcn_s_memrealtime() - tw;
+    ps.wait_acc[1] += 1;
+  }
   double s = 0.0;
   if (lane < n)
     for (int r = 0; r < ps.P; ++r)

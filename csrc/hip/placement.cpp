@@ -143,13 +143,41 @@ using dev::KParams;
 // PE_PLACEMENT_SKIP_GB (default 8) spacer so it lands in another region;
 // time a few local sweeps on real data (no communication) and keep the
 // fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
+//
+// Multi-rank jobs: the in-sweep sums couple the ranks every iteration, so the
+// job runs at its slowest rank's placement.  After the local searches the
+// ranks agree (max-allreduce) whether any of them missed the best class;
+// if so, those ranks search once more (same 0.3 s cap, past the memory the
+// first round tried) while the others wait at the next collective, and the
+// job's max ms/sweep is recorded (bench.py reports it with every rank's
+// candidates).  Every rank makes the same collective calls whatever its
+// local search did (job-wide MAX semantics of the reference's timer
+// reduction, poisson_mpi_cuda2.cu:962-966).
 void DeviceSolver::choose_placement() {
+  const double t_all = placement_s_;
+  const auto t0 = clk::now();
+  const bool fast = placement_search(false);
+  if (comm_->size() > 1) {
+    double v[1] = {(!placement_ms_.empty() && !fast) ? 1.0 : 0.0};
+    comm_->host_max(v, 1, stream_);
+    if (v[0] > 0.0 && !placement_ms_.empty() && !fast) placement_search(true);
+    double m[1] = {placement_ms_.empty() ? 0.0 : double(placement_ms_[size_t(placement_best_)])};
+    comm_->host_max(m, 1, stream_);
+    placement_job_ms_ = m[0];
+  } else if (!placement_ms_.empty()) {
+    placement_job_ms_ = placement_ms_[size_t(placement_best_)];
+  }
+  placement_s_ = t_all + secs(t0, clk::now());
+}
+
+bool DeviceSolver::placement_search(bool retry) {
   Range range("pe.placement_search");
+  double search_s = 0;
   struct Clock {
     double& out;
     clk::time_point t0 = clk::now();
     ~Clock() { out = secs(t0, clk::now()); }
-  } clock{placement_s_};
+  } clock{search_s};
   const double pts = double(blk_.nx) * double(blk_.ny);
   // Only large blocks: the two-speed placement was measured at 8192² (≈9 %);
   // at 2400×3200 / 4096² the candidates differ by ≤ 3-7 % while the spacer
@@ -162,13 +190,14 @@ void DeviceSolver::choose_placement() {
   // profiles/r2_validate_final.txt); a try costs ≈6 ms, and the search
   // stops at the first best-class candidate.
   int tries = pts >= 24.0e6 ? 12 : 1;
+  if (retry) tries = std::max(1, tries / 2 + 1);  // the kept candidate + half a round
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
   double skip_gb = 8.0;
   if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
   double fast_tbs = 4.9, max_s = 0.3;
   if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
-  if (tries <= 1) return;
+  if (tries <= 1) return true;
   // spacers are transient; never let the search take more than 40 % of the
   // free memory (several solvers may share the device; PE_PLACEMENT_MEM_FRAC)
   {
@@ -180,10 +209,10 @@ void DeviceSolver::choose_placement() {
       tries = std::min<int>(tries, std::max(1, int(frac * double(free_b) / per_try)));
     }
   }
-  if (tries <= 1) return;
+  if (tries <= 1) return true;
   if (const char* e = std::getenv("PE_PLACEMENT"); e && std::string(e) == "carve") {
     carve_placement();
-    return;
+    return true;
   }
   struct Cand {
     double *x0, *x1, *w;
@@ -192,6 +221,16 @@ void DeviceSolver::choose_placement() {
   std::vector<Cand> c;
   std::vector<void*> spacers;
   c.push_back(Cand{fields_, xalt_, walt_, 0.f});
+  // a retry first steps past the memory the first round tried (its spacers
+  // and candidates were freed: the allocator would hand them out again)
+  const size_t n_first = placement_ms_.size();
+  if (retry && skip_gb > 0) {
+    const double gb = double(n_first) * (skip_gb + double(sizeof(double) * (2 * xsize_ + wsize_)) / double(1ull << 30));
+    void* sp = nullptr;
+    if (hipMalloc(&sp, size_t(gb * double(1ull << 30))) == hipSuccess) spacers.push_back(sp);
+    else (void)hipGetLastError();
+  }
+  bool fast = false;
   for (int t = 0; t < tries; ++t) {
     if (t > 0) {
       void* sp = nullptr;
@@ -231,7 +270,10 @@ void DeviceSolver::choose_placement() {
     // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
     // 0.56-0.60 ms placements when better ones were a try or two further.)
     const double tbs = 40.0 * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
-    if (tbs >= fast_tbs) break;
+    if (tbs >= fast_tbs) {
+      fast = true;
+      break;
+    }
     // spacer allocations are cheap on fresh memory but can take seconds
     // when the allocator must clear reused memory (profiles/r2_ctor_probe.txt):
     // the search is capped at PE_PLACEMENT_MAX_S (0.3 s) of wall time
@@ -249,9 +291,11 @@ void DeviceSolver::choose_placement() {
     }
   for (void* sp : spacers) PE_HIP_CHECK(hipFree(sp));
   set_fused_fields(c[best].x0, c[best].x1, c[best].w);
-  placement_best_ = int(best);
-  placement_ms_.clear();
+  if (!retry) placement_ms_.clear();
+  // a retry appends its candidates (its first is the first round's pick, re-timed)
+  placement_best_ = int(placement_ms_.size() + best);
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
+  return fast || 40.0 * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
 }
 
 // Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE

@@ -26,7 +26,8 @@
 //   →  7 partial sums published, ONE grid barrier, then every workgroup reads
 //      the ring 2 of r from its 8 neighbours and ALL partial sums, and adds
 //      them in a fixed order (the same bits everywhere: deterministic).
-// Hand-off protocol (MI355X_MICROARCH.md, "Valid forms" row 1): every
+// Hand-off protocol (the image's CDNA4 guide /opt/skills/guides/MI355X_MICROARCH.md,
+// not part of this repo: "Valid forms" row 1): every
 // published value is stored `sc1` (relaxed agent-scope atomic store), each
 // storing wave drains `vmcnt(0)`, a workgroup barrier, ONE lane adds to a
 // per-XCD-sharded counter; consumers poll with `sc1` loads, barrier, and read
@@ -114,7 +115,6 @@ __device__ __forceinline__ double wave_sum63(double v) {
 __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
   extern __shared__ double lds_raw[];
   DevState* st = k.st;
-  if (st->done) return;  // uniform: the solve has ended
   const int tid = int(threadIdx.x), lane = tid & 63, wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wg = int(blockIdx.x);
   const int tr = wg / rp.nstrips, s = wg - tr * rp.nstrips;
@@ -136,6 +136,7 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
   const Coef cf{k.inv_eps, k.ih1sq, k.ih2sq, band, rp.nbcap};
 
   // ---- state of the previous iteration (fused.hip's DevState) ----
+  const int done0 = st->done;
   const int wpend = st->wpend;
   const double alpha_st = st->alpha;
   double gprev = st->gprev;
@@ -144,7 +145,23 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
 #pragma unroll
   for (int n = 0; n < 7; ++n) S[n] = st->fs[rp.par0 ^ 1][n];
   if (tid == 0) misc[0] = misc[1] = misc[2] = 0;
+  // every thread's state reads have returned before this workgroup counts
+  // itself in: workgroup 0 writes a terminal state of the launch's FIRST
+  // iteration only once all workgroups are counted (none can then read a
+  // half-written state or a premature `done`)
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
+  if (done0) return;  // uniform: the solve has ended
+  if (tid == 0) __hip_atomic_fetch_add(rp.ctr + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // the terminal write of iteration 0 (workgroup 0, thread 0): wait for every
+  // workgroup's entry (co-resident grid; the barrier timeout bounds it)
+  auto entered_all = [&]() {
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(rp.ctr + 16, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < unsigned(rp.nwg)) {
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > rp.timeout_ticks) break;
+      __builtin_amdgcn_s_sleep(1);
+    }
+  };
 
   // ---- load the region, evaluate the coefficient codes ----
   const int c0 = J0 - 2 + 2 * lane;  // this lane's column pair (c0, c0+1) = region columns 2·lane, 2·lane+1
@@ -239,12 +256,14 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
     alpha = g / den;
     const double pn2 = fmax(S[4] + 2.0 * beta * S[5] + beta * beta * S[6], 0.0);
     diff = k.weighted ? fabs(alpha) * sqrt(pn2 * hh) : fabs(alpha) * sqrt(pn2);
-    const bool bad = !isfinite(den) || !isfinite(g) || !isfinite(diff);
-    const bool brk = bad || fabs(den) < 1e-15;
+    const bool tiny = fabs(den) < 1e-15;  // breakdown before α (reference :413)
+    const bool bad = !isfinite(den) || !isfinite(g) || (!tiny && !isfinite(diff));
+    const bool brk = bad || tiny;
     const bool conv = k.check_tol && diff < k.tol;
     const bool last = !brk && (conv || kiter >= k.max_iter);
     if (brk) {  // reference :413 — stop before this iteration's update
       if (wg == 0 && tid == 0) {
+        if (it == 0) entered_all();
         st->status = bad ? 4 : 2;
         st->iter = kiter;
         st->done = 1;
@@ -276,6 +295,7 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
         }
       }
       if (wg == 0 && tid == 0) {
+        if (it == 0) entered_all();
         st->gprev = g;
         st->rz_cur = g;
         st->alpha = alpha;
@@ -410,7 +430,8 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
       __syncthreads();
       stamp(4);
       if (wv == 0) {
-        if (lane == 0) __hip_atomic_fetch_add(rp.ctr + (wg & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (lane == 0 && !(it == 0 && wg == rp.fault_wg))  // (fault hook: one workgroup never arrives)
+          __hip_atomic_fetch_add(rp.ctr + (wg & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int x = lane & 7;
         const unsigned want = unsigned(it + 1) * unsigned((rp.nwg - x + 7) / 8);
         const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
@@ -439,10 +460,12 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
     }
 
     // ---- every tile's partial sums (wave n < 7: quantity n over ≤ 256
-    //      tiles), ring 2 of r (wave 7) ----
+    //      tiles — setup_resident refuses larger grids, kResMaxTiles), ring 2
+    //      of r (wave 7) ----
     if (wv < 7) {
       const double* P = rp.partials + size_t(buf) * size_t(rp.nwg) * 8 + wv;
       double v[4];
+      static_assert(kResMaxTiles == 4 * 64, "gather width");
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int t = j * 64 + lane;

@@ -28,6 +28,20 @@ int device_count() {
 
 void set_device(int dev) { PE_HIP_CHECK(hipSetDevice(dev)); }
 
+int current_device() {
+  int d = -1;
+  PE_HIP_CHECK(hipGetDevice(&d));
+  return d;
+}
+
+// "dddd:bb:dd.f" of a device: which physical GPU a rank drives (bench.py
+// reports it per rank, so "N ranks on N distinct GPUs" is checkable).
+std::string device_pci_bus_id(int dev) {
+  char buf[64] = {0};
+  PE_HIP_CHECK(hipDeviceGetPCIBusId(buf, int(sizeof buf), dev));
+  return std::string(buf);
+}
+
 std::string device_name(int dev) {
   hipDeviceProp_t p;
   PE_HIP_CHECK(hipGetDeviceProperties(&p, dev));

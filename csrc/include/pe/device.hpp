@@ -30,6 +30,8 @@ struct PeerSum;
 int device_count();
 void set_device(int dev);
 std::string device_name(int dev);
+int current_device();
+std::string device_pci_bus_id(int dev);
 
 // Stream-ordered transport over device buffers.
 class DeviceComm {
@@ -124,11 +126,17 @@ class DeviceSolver {
   // Switch the convergence test on / off (drops cached graphs): the bench
   // times fixed-work steps, then solves to convergence on the same solver.
   void set_check_tol(bool on);
+  // Initial guess of the next reset() / solve() (bench: the BASELINE
+  // random-init solve on the same solver as the zero-init one).
+  void set_init(Init init, uint64_t seed, double amp);
   // Tuning probe: re-lay out the work items for `ti` rows per item, re-reading
   // the PE_* layout knobs (same allocation, so configurations compare at one
   // memory placement).  Drops cached graphs.
   void relayout(int ti, int order = -1);  // probe: re-lay out the items (ti rows; order 0 / 3, -1 keeps)
   double time_iterations(int64_t iters, bool use_graph);  // device seconds (events)
+  // Wait for the stream; with PE_WATCHDOG_S set (or a stall injected) the
+  // wait is bounded: no progress for that long aborts the communicator and
+  // throws (the bench's timed region and solve are both covered).
   void synchronize();
 
   // Phases (used by the virtual-rank group driver and tests).
@@ -158,6 +166,7 @@ class DeviceSolver {
   // LDS-resident single sweep (resident.hip): small single-rank blocks run
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
   bool resident() const { return resident_; }
+  bool resident_fallback() const { return resident_fallback_; }
   bool overlap() const { return overlap_; }
   // Halo rows pushed by the sweep itself over xGMI (row slabs + in-sweep P2P
   // sums): no exchange call in the iteration, which is then graph-capturable.
@@ -165,6 +174,9 @@ class DeviceSolver {
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   int placement_choice() const { return placement_best_; }       // index into placement_ms()
+  // multi-rank: the slowest rank's chosen ms/sweep (the job runs at its pace;
+  // this rank's own choice when alone, 0 without a search)
+  double placement_job_ms() const { return placement_job_ms_; }
   double placement_seconds() const { return placement_s_; }      // wall time of the search
   double construct_seconds() const { return ctor_s_; }           // wall time of the constructor
   double exchange_us() const { return exchange_us_; }            // measured halo exchange (multi-rank)
@@ -203,7 +215,8 @@ class DeviceSolver {
   void set_fused_fields(double* x0, double* x1, double* w);
   void setup_items();  // item lists: static LPT layout or dynamic per-XCD shards (+ halo/interior overlap)
   void create_halo_stream();
-  void choose_placement();
+  void choose_placement();   // local search, then (multi-rank) the coordinated retry round
+  bool placement_search(bool retry);  // local; true when the kept candidate is in the best class
   void carve_placement();  // PE_PLACEMENT=carve experiment (relative offsets within one allocation)
   void measure_exchange();  // sets exchange_us_ (collective)
   void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
@@ -279,6 +292,7 @@ class DeviceSolver {
   double watchdog_s_ = 0;   // PE_WATCHDOG_S: abort if a chunk makes no progress this long (0 = off)
   bool fault_stall_ = false;  // PE_FAULT_INJECT=stall: pretend the device never finishes (watchdog test)
   hipEvent_t ev_[2] = {nullptr, nullptr};
+  hipEvent_t ev_sync_ = nullptr;  // synchronize() under the watchdog
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
   std::vector<hipEvent_t> evpool_;
   std::vector<PhaseRec> recs_;
@@ -288,6 +302,7 @@ class DeviceSolver {
   double ctor_s_ = 0, copy_setup_s_ = 0, placement_s_ = 0;
   bool ctor_counted_ = false;
   int placement_best_ = 0;
+  double placement_job_ms_ = 0;
   bool tune_ti_ = false;          // rows per item chosen by timing candidate sweeps
   std::vector<float> ti_ms_;      // their per-sweep times
   std::vector<int> ti_rows_;      // the candidates timed
@@ -295,6 +310,8 @@ class DeviceSolver {
   int lay_items_ = 0;                  // static layout: most items on one wave
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;
+  bool resident_fallback_ = false;  // a resident launch aborted (status 5): switched to the streaming sweep
+  int stream_chunk_ = 16;           // chunk length of the streaming sweep (after a resident fallback)
   std::unique_ptr<dev::ResParams> rp_;
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials

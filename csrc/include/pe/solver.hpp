@@ -38,6 +38,11 @@ namespace pe {
 //             (the reference's time_solver spans assembly, malloc, H2D, the
 //             loop and free, poisson_mpi_cuda2.cu:1010-1016)
 //   iterate — wall time of the iteration loop only
+//   wait    — device solver, in-sweep cross-rank sum (P2P transport): the
+//             time the sweeps' final blocks waited for the peers' flags
+//             (s_memrealtime around the spin; it includes the halo push's
+//             delivery, which those flags signal, and any rank imbalance —
+//             what the reference's MPI_Allreduce time holds)
 // Device solver: the per-phase device times come from hipEvent pairs around
 // the phases of sampled iterations (no host sync in the loop; every
 // PE_TIMER_SAMPLE-th chunk, default 8, its first two iterations; every
@@ -47,6 +52,7 @@ struct Timers {
   double gpu = 0, copy = 0, halo = 0, reduce = 0, prec = 0, dot = 0, setup = 0, solver = 0;
   double iterate = 0;  // wall time of the iteration loop only
   double construct = 0, sampled = 0;
+  double wait = 0;  // in-sweep cross-rank wait (see above)
   bool dot_fused = false;
 };
 
@@ -96,6 +102,7 @@ struct SolveResult {
   int Px = 1, Py = 1;
   std::string backend;
   std::string algo;      // device: "fused" (single-sweep) or "classic"
+  bool resident_fallback = false;  // device: a resident launch aborted, the solve finished on the streaming sweep
 };
 
 // ---- CPU backends (reference stage0..3 equivalents) -----------------------

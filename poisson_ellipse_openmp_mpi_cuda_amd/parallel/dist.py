@@ -135,6 +135,16 @@ def rccl_comm(ctx: DistContext, tag: str = "pe/rccl_uid"):
     return comm
 
 
+def drop_comm(comm) -> None:
+    """Forget a cached communicator after a solve that ended non-finite or
+    aborted: its P2P sequence counter / slot flags may no longer match the
+    peers', so the next solve of the job builds a fresh one (collectively —
+    every rank sees the same non-finite status, which is computed from the
+    same reduced sums, and an aborted rank ends its process)."""
+    for k in [k for k, v in _COMMS.items() if v is comm]:
+        del _COMMS[k]
+
+
 def _gloo_group():
     global _GLOO
     if _GLOO is None:

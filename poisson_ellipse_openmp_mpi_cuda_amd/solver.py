@@ -58,6 +58,7 @@ class SolveReport:
     comm: str = ""  # device transport of a multi-rank HIP run (e.g. "rccl", "p2p-allreduce+rccl")
     xr: bool = False  # the sweep sums its scalars over ranks itself (P2P transport, no allreduce launch)
     halo_push: bool = False  # the sweep pushes its edge rows to the neighbours over xGMI (no exchange call)
+    resident_fallback: bool = False  # a resident launch aborted (barrier timeout); the solve finished streaming
 
     @property
     def iters_per_s(self) -> float:
@@ -102,7 +103,8 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         last_diff=float(res.last_diff), timers=dict(res.timers), l2_err=float(res.l2_err),
         max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank,
         algo=str(getattr(res, "algo", "")), nonfinite=bool(getattr(res, "nonfinite", False)),
-        history=list(res.history) if len(res.history) else None)
+        history=list(res.history) if len(res.history) else None,
+        resident_fallback=bool(getattr(res, "resident_fallback", False)))
 
 
 def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str | None = None,
@@ -179,7 +181,14 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
         comm = _dist.rccl_comm(ctx)
         blk = _decomp.block(prob.M, prob.N, world, rank, decomp)
     solver = nat.DeviceSolver(P, blk, comm, opt)
-    res = solver.solve()
+    try:
+        res = solver.solve()
+    except Exception:
+        if comm is not None:
+            _dist.drop_comm(comm)
+        raise
+    if comm is not None and (res.nonfinite or not np.isfinite(res.last_diff)):
+        _dist.drop_comm(comm)  # its P2P sequence may be out of step with the peers'
     w = None
     if return_w:
         wl = np.asarray(solver.w())

@@ -5,7 +5,8 @@ Reference formats: stage2 ``M=.., N=.. | Iter=.. | Time=%.6f s``
 ``Total Time`` / ``Init`` / ``Solver`` / ``Finalization`` lines
 (stage4-mpi+cuda/poisson_mpi_cuda2.cu:968-979, :1026-1034).  The legacy
 stage-4 labels are kept verbatim in parity mode ("MPI halo exchange" there
-includes the allreduces; the D⁻¹ work is fused into the sweep, so its line
+includes the allreduces — here: exchange + allreduce launches + the in-sweep
+cross-rank wait, timer ``wait``; the D⁻¹ work is fused into the sweep, so its line
 says so instead of printing a zero); the JSON report uses honest category
 names.
 """
@@ -40,7 +41,7 @@ def legacy_lines(rep, tol: float = 1e-6) -> str:
     if st == "stage4":
         out.append(f"   GPU compute time (Ap + D^{{-1}}r, max over ranks) ~ {t.get('gpu', 0):g} s")
         out.append(f"   Host<->Device copy time (max over ranks)        ~ {t.get('copy', 0):g} s")
-        out.append(f"   MPI halo exchange time (max over ranks)         ~ {t.get('halo', 0) + t.get('reduce', 0):g} s")
+        out.append(f"   MPI halo exchange time (max over ranks)         ~ {t.get('halo', 0) + t.get('reduce', 0) + t.get('wait', 0):g} s")
         fused = "n/a (fused into the GPU sweep)"
         out.append(f"   Preconditioner CPU part time (max over ranks)   ~ {fused}")
         dot = fused if t.get("dot_fused", False) else f"{t.get('dot', 0):g} s"

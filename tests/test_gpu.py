@@ -432,12 +432,108 @@ def test_bench_halo_push_graphs(gpu, nproc):
     assert d["l2_err"] == pytest.approx(one.l2_err, rel=1e-6)
 
 
+def test_bench_self_launch_and_random_init(gpu):
+    """`bench.py --gpus 2` with no launcher starts its 2 ranks itself (here
+    sharing the one GPU through the host-staged test transport): one JSON
+    line, n_gpus 2, every rank listed with its device, the job-wide placement
+    and the random-init solve reported."""
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "20",
+                          "--warmup", "2", "--grid", "512", "512", "--decomp", "rows"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [l for l in out.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    c = d["config"]
+    assert d["n_gpus"] == 2 and c["comm_ranks"] == 2 and d["valid"] and d["converged"]
+    assert [r["rank"] for r in c["ranks"]] == [0, 1] and all(r["pci_bus_id"] for r in c["ranks"])
+    ri = d["random_init"]
+    assert ri["converged"] and ri["iters"] > 0 and ri["l2_err"] < 1e-2
+    assert "wait" in d["t_breakdown_s"]
+
+
+def test_bench_stalled_rank_fails_fast(gpu):
+    """bench.py under torchrun with rank 1 stalled (PE_FAULT_INJECT=stall@rank:1):
+    its bounded wait (PE_WATCHDOG_S) fires, the rank exits non-zero and the
+    job ends — within 90 s, never a hang."""
+    import signal
+
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_FAULT_INJECT="stall@rank:1", PE_WATCHDOG_S="2")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps",
+           "20", "--warmup", "2", "--grid", "512", "512"]
+    p = subprocess.Popen(cmd, cwd=ROOT, env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True,
+                         start_new_session=True)
+    try:
+        out, err = p.communicate(timeout=90)
+    except subprocess.TimeoutExpired:
+        os.killpg(p.pid, signal.SIGKILL)
+        p.communicate()
+        pytest.fail("a stalled rank hung bench.py instead of failing it")
+    assert p.returncode != 0
+    assert "watchdog" in err, err[-3000:]
+
+
+def test_slow_rank_shows_in_tmpi(gpu):
+    """T_MPI of the default multi-rank path (in-sweep P2P sums + halo push):
+    with rank 1's sweeps idling 300 µs before their cross-rank sum
+    (PE_FAULT_INJECT=slow@rank:1,us:300) the job's `wait` timer — max over
+    ranks, rank 0 waits for rank 1 every iteration — is ≈ iterations × 300 µs
+    (reference T_MPI: poisson_mpi_cuda2.cu:870-873, :891-895, :924-928, max over
+    ranks :962-966)."""
+    from conftest import free_port
+
+    def run(fault):
+        env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+        if fault:
+            env["PE_FAULT_INJECT"] = fault
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+               "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+               "poisson_ellipse_openmp_mpi_cuda_amd", "--json", "--quiet", "--decomp", "rows", "400", "600"]
+        out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-3000:]
+        d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert d["xr"] and d["iters"] == 546
+        return d["timers"]["wait"]
+
+    base = run(None)
+    slow = run("slow@rank:1,us:300")
+    want = 546 * 300e-6
+    assert 0.7 * want <= slow - base <= 2.0 * want, (base, slow)
+
+
 @pytest.mark.parametrize("algo", ["fused", "classic"])
 def test_fault_injection_nan_stops_cleanly(gpu, algo, monkeypatch):
     monkeypatch.setenv("PE_FAULT_INJECT", "nan@iter:20")
     rep = solve(EllipseProblem(400, 600), backend="hip", algo=algo)
     assert rep.nonfinite and not rep.converged
     assert 20 <= rep.iters <= 23
+
+
+@pytest.mark.parametrize("K", [20, 21])
+def test_forced_breakdown_terminal_path(gpu, K, monkeypatch):
+    """|den| < 1e-15 (PE_FAULT_INJECT=zero@iter:K zeroes the (p, A p) sums of
+    sweep K) stops the solve at iteration K+1 before its update (reference
+    :413) — K = 20: the breakdown is met by a deferring sweep (nothing
+    pending), K = 21: by an applying sweep (it adds the pending α_K p_K).
+    Every wave takes the terminal path (wave-counted hand-off, no workgroup
+    barrier); w equals a run capped at K iterations."""
+    prob = EllipseProblem(200, 300)
+    monkeypatch.setenv("PE_RESIDENT", "0")
+    monkeypatch.setenv("PE_FAULT_INJECT", f"zero@iter:{K}")
+    brk = solve(prob, backend="hip", return_w=True, algo="fused")
+    assert brk.breakdown and not brk.converged and brk.iters == K + 1
+    monkeypatch.delenv("PE_FAULT_INJECT")
+    capped = EllipseProblem(200, 300)
+    capped.max_iter = K
+    ref = solve(capped, backend="hip", return_w=True, algo="fused")
+    assert ref.iters == K
+    np.testing.assert_allclose(brk.w, ref.w, rtol=0, atol=1e-15 * np.abs(ref.w).max())
 
 
 def test_watchdog_fires_on_stall(gpu, monkeypatch):
@@ -518,6 +614,38 @@ def test_resident_matches_streaming(gpu, M, N, monkeypatch):
         assert res.iters == GOLDEN_ITERS[(M, N, "weighted")]
     np.testing.assert_allclose(res.w, ref.w, rtol=0, atol=1e-10)
     assert res.l2_err == pytest.approx(ref.l2_err, rel=1e-7)
+
+
+def test_resident_barrier_timeout_falls_back(gpu, monkeypatch):
+    """A resident launch whose grid barrier times out (PE_FAULT_INJECT=resbarrier:
+    one workgroup never arrives; 0.1 s limit) aborts with nothing written
+    back; the solver clears the abort, switches to the streaming sweep and
+    still converges in the golden count (reference iteration must complete:
+    poisson_mpi_decomp.cpp:400-457)."""
+    monkeypatch.setenv("PE_FAULT_INJECT", "resbarrier")
+    monkeypatch.setenv("PE_RES_TIMEOUT_S", "0.1")
+    rep = solve(EllipseProblem(800, 1200), backend="hip")
+    assert rep.resident_fallback and rep.algo == "fused (resident fallback)"
+    assert rep.converged and rep.iters == 989
+    assert rep.l2_err == pytest.approx(1.92e-4, rel=5e-3)
+
+
+@pytest.mark.parametrize("M,N,chunk,max_iter", [(800, 1200, 988, 0), (300, 700, 512, 513)])
+def test_resident_terminal_at_launch_start(gpu, M, N, chunk, max_iter, monkeypatch):
+    """The solve ends on the FIRST iteration of a resident launch (convergence at
+    989 with 988-iteration launches; the cap 513 with 512): workgroup 0 writes
+    the terminal state only after every workgroup has read the entry state,
+    so every tile adds its α·p and the result equals the streaming sweep's."""
+    prob = EllipseProblem(M, N)
+    if max_iter:
+        prob.max_iter = max_iter
+    monkeypatch.setenv("PE_RESIDENT", "0")
+    ref = solve(prob, backend="hip", return_w=True, chunk=chunk)
+    monkeypatch.delenv("PE_RESIDENT")
+    res = solve(prob, backend="hip", return_w=True, chunk=chunk)
+    assert res.algo == "resident" and ref.algo == "fused"
+    assert res.iters == ref.iters == (max_iter or 989)
+    np.testing.assert_allclose(res.w, ref.w, rtol=0, atol=1e-10)
 
 
 @pytest.mark.parametrize("parts", [[60], [7, 13, 40], [1, 1, 58]])

@@ -123,3 +123,21 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     # 2047 rows: slabs while every rank keeps >= 512 rows (2 and 4 GPUs) → the
     # halo is pushed by the sweep and the iterations run as captured graphs
     assert c["halo"].startswith("in-sweep xGMI push") == (c["decomposition"]["Py"] == 1)
+
+
+@pytest.mark.parametrize("nproc", [2, 8])
+def test_bench_self_launch_real_gpus(gpu, nproc):
+    """`python bench.py --gpus N` with no launcher (how the driver may call it):
+    N ranks on N distinct GPUs, RCCL saw N ranks, n_gpus == N."""
+    _need(nproc)
+    env = dict(os.environ)
+    for k in ("PE_COMM", "WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    out = _run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(nproc), "--steps", "40", "--warmup",
+                "5", "--grid", "2048", "2048", "--no-random-solve"], env, timeout=300)
+    lines = [l for l in out.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    c = d["config"]
+    assert d["n_gpus"] == nproc and c["comm_ranks"] == nproc and c["distinct_gpus"] == nproc
+    assert d["valid"] and d["converged"] and d["iters_converged"] == 1730
