@@ -60,6 +60,14 @@ py::dict state_dict(const dev::DevState& s) {
                                           s.fs[0][6]),
                            py::make_tuple(s.fs[1][0], s.fs[1][1], s.fs[1][2], s.fs[1][3], s.fs[1][4], s.fs[1][5],
                                           s.fs[1][6]));
+  py::list f2;
+  for (int b = 0; b < 2; ++b) {
+    py::list v;
+    for (int n = 0; n < dev::kNS2; ++n) v.append(s.fs2[b][n]);
+    f2.append(py::tuple(v));
+  }
+  d["fs2"] = py::tuple(f2);
+  d["wait_s"] = double(s.xr_wait) * 1e-8;
   return d;
 }
 
@@ -423,6 +431,7 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
+      .def_property_readonly("two_step", &DeviceSolver::two_step, "two iterations per sweep (fused2.hip)")
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("overlap", &DeviceSolver::overlap)

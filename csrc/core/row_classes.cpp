@@ -56,24 +56,24 @@ int64_t last_true(int64_t lo, int64_t hi, P pred) {
 
 }  // namespace
 
-std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi) {
-  const int64_t L = -1, H = cols_hi;  // row-table index range
-  auto sA = [&](int64_t j) { return rowT[(j + 1) * 4 + 0]; };
-  auto eA = [&](int64_t j) { return rowT[(j + 1) * 4 + 1]; };
-  auto hB = [&](int64_t j) { return rowT[(j + 1) * 4 + 2]; };
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi, int64_t lo) {
+  const int64_t L = lo, H = cols_hi;  // row-table index range
+  auto sA = [&](int64_t j) { return rowT[(j - lo) * 4 + 0]; };
+  auto eA = [&](int64_t j) { return rowT[(j - lo) * 4 + 1]; };
+  auto hB = [&](int64_t j) { return rowT[(j - lo) * 4 + 2]; };
   // Peak of the unimodal halfB(j).
   int64_t peak = L;
   for (int64_t j = L; j <= H; ++j)
     if (hB(j) > hB(peak)) peak = j;
 
   auto a_in = [&](int64_t q) {
-    const double half = colT[(q + 1) * 4 + 0];
+    const double half = colT[(q - lo) * 4 + 0];
     if (half < 0) return Iv{};
     return Iv{first_true(L, H, [&](int64_t j) { return sA(j) >= -half; }),
               last_true(L, H, [&](int64_t j) { return eA(j) <= half; })};
   };
   auto a_notout = [&](int64_t q) {
-    const double half = colT[(q + 1) * 4 + 0];
+    const double half = colT[(q - lo) * 4 + 0];
     if (half < 0) return Iv{};
     return Iv{first_true(L, H, [&](int64_t j) { return eA(j) > -half; }),
               last_true(L, H, [&](int64_t j) { return sA(j) < half; })};
@@ -85,16 +85,16 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t row
     return Iv{first_true(L, peak, ok), last_true(peak, H, ok)};
   };
   auto b_in = [&](int64_t q) {
-    const double sB = colT[(q + 1) * 4 + 1], eB = colT[(q + 1) * 4 + 2];
+    const double sB = colT[(q - lo) * 4 + 1], eB = colT[(q - lo) * 4 + 2];
     return b_level(std::max(-sB, eB), false);
   };
   auto b_notout = [&](int64_t q) {
-    const double sB = colT[(q + 1) * 4 + 1], eB = colT[(q + 1) * 4 + 2];
+    const double sB = colT[(q - lo) * 4 + 1], eB = colT[(q - lo) * 4 + 2];
     return b_level(std::max(-eB, sB), true);
   };
 
-  std::vector<int> out(size_t(rows_hi + 2) * 4, 0);
-  for (int64_t q = -1; q <= rows_hi - 1; ++q) {
+  std::vector<int> out(size_t(rows_hi - lo + 1) * 4, 0);
+  for (int64_t q = lo; q <= rows_hi - 1; ++q) {
     const Iv bi = b_in(q);
     const Iv in = meet(meet(a_in(q), a_in(q + 1)), meet(bi, shift(bi, -1)));
     const Iv bn = b_notout(q);
@@ -104,7 +104,7 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t row
         olo = std::min(olo, v.lo);
         ohi = std::max(ohi, v.hi);
       }
-    int* o = out.data() + (q + 1) * 4;
+    int* o = out.data() + (q - lo) * 4;
     o[0] = in.empty() ? 1 : int(in.lo);
     o[1] = in.empty() ? 0 : int(in.hi);
     o[2] = int(olo);
@@ -113,24 +113,24 @@ std::vector<int> row_classes(const double* colT, const double* rowT, int64_t row
   return out;
 }
 
-std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi) {
+std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi, int64_t lo) {
   const double h1 = P.h1(), h2 = P.h2();
-  std::vector<double> t((rows_hi + 2) * 4 + (cols_hi + 2) * 4, 0.0);
+  std::vector<double> t((rows_hi - lo + 1) * 4 + (cols_hi - lo + 1) * 4, 0.0);
   double* col = t.data();
-  double* row = t.data() + (rows_hi + 2) * 4;
-  for (int64_t li = -1; li <= rows_hi; ++li) {
+  double* row = t.data() + (rows_hi - lo + 1) * 4;
+  for (int64_t li = lo; li <= rows_hi; ++li) {
     const int64_t gi = blk.i0 - 1 + li;
     const double x = P.A1 + gi * h1;  // x_i exactly as the reference forms it
-    double* c = col + (li + 1) * 4;
+    double* c = col + (li - lo) * 4;
     c[0] = chord_half_vertical(x - 0.5 * h1, P.cx, P.cy, P.sx);
     c[1] = x - 0.5 * h1;
     c[2] = x + 0.5 * h1;
     c[3] = x;
   }
-  for (int64_t lj = -1; lj <= cols_hi; ++lj) {
+  for (int64_t lj = lo; lj <= cols_hi; ++lj) {
     const int64_t gj = blk.j0 - 1 + lj;
     const double y = P.A2 + gj * h2;
-    double* r = row + (lj + 1) * 4;
+    double* r = row + (lj - lo) * 4;
     r[0] = y - 0.5 * h2;
     r[1] = y + 0.5 * h2;
     r[2] = chord_half_horizontal(y - 0.5 * h2, P.cx, P.cy, P.sy);

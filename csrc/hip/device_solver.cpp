@@ -71,9 +71,20 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     comm_ = self_.get();
   }
   const bool can_fuse = opt_.variant == 0 && fused_possible(prob_, blk_);
-  if (opt_.algo == 2 && !can_fuse)
+  if ((opt_.algo == 2 || opt_.algo == 3) && !can_fuse)
     throw std::invalid_argument("single-sweep algorithm needs variant 0 and >= 2 rows/columns per split block");
-  fused_ = opt_.algo == 2 || (opt_.algo == 0 && can_fuse);
+  fused_ = opt_.algo == 2 || opt_.algo == 3 || (opt_.algo == 0 && can_fuse);
+  // Two iterations per sweep (fused2.hip): single-rank blocks of ≥ 8 × 8
+  // nodes (algo 3, or auto: PE_TWO=0/1 overrides).  Its 4-deep halo and
+  // 20-sum reduction are not wired to the multi-rank transports yet.
+  {
+    const bool two_ok = fused_ && comm_->size() == 1 && blk_.nx >= 8 && blk_.ny >= 8;
+    if (opt_.algo == 3 && !two_ok)
+      throw std::invalid_argument("two-step sweep: single-rank blocks of at least 8 x 8 nodes only");
+    bool auto_two = false;
+    if (const char* e = std::getenv("PE_TWO")) auto_two = std::atoi(e) != 0;
+    two_ = two_ok && (opt_.algo == 3 || (opt_.algo == 0 && auto_two));
+  }
 
   mark("start");
   PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
@@ -90,11 +101,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (fused_) {
     // Planes: columns -1 .. 124·nstrips+2 (strip loads never leave the row),
     // rows -1 .. nx+4 (two prefetch rows past the halo).  x[b] interleaves the
-    // r and p planes by row.
-    strips = (ny + dev::kFSW - 1) / dev::kFSW;
-    plane_ = ((dev::kFSW * strips + 4 + 7) / 8) * 8;
+    // r and p planes by row.  Two-step sweep: halo depth 4 — columns -3 ..
+    // 120·nstrips+4, rows -3 .. nx+6.
+    fsw_ = two_ ? dev::kFSW2 : dev::kFSW;
+    hdep_ = two_ ? 4 : 2;
+    strips = (ny + fsw_ - 1) / fsw_;
+    plane_ = ((fsw_ * strips + 2 * hdep_ + 7) / 8) * 8;
     if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
-    const int64_t rows = nx + 6;
+    const int64_t rows = nx + 2 * hdep_ + 2;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
     wsize_ = ((rows * plane_ + 64 + 31) / 32) * 32;
     k.pitch = 2 * plane_;
@@ -111,8 +125,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     mark("field allocs");
     set_fused_fields(fields_, xalt_, walt_);
     hsize_ = std::max<int64_t>(1, nx) * 4;
-    rows_hi = nx + 3;
-    cols_hi = dev::kFSW * strips + 3;
+    rows_hi = two_ ? nx + 6 : nx + 3;
+    cols_hi = two_ ? dev::kFSW2 * strips + 7 : dev::kFSW * strips + 3;
+    tab_lo_ = two_ ? -4 : -1;
   } else {
     strips = (ny + dev::kSW - 1) / dev::kSW;
     const int64_t A = blk_.alloc;
@@ -126,9 +141,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     hsize_ = std::max<int64_t>(1, nx);
   }
   mark("fields");
-  const int64_t ntab = (rows_hi + 2) * 4 + (cols_hi + 2) * 4;
+  const int64_t nrow_tab = rows_hi - tab_lo_ + 1, ncol_tab = cols_hi - tab_lo_ + 1;
+  const int64_t ntab = nrow_tab * 4 + ncol_tab * 4;
   PE_HIP_CHECK(hipMalloc(&tables_, sizeof(double) * ntab));
-  PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * (rows_hi + 2) * 4));
+  PE_HIP_CHECK(hipMalloc(&rowcls_, sizeof(int) * nrow_tab * 4));
   PE_HIP_CHECK(hipMalloc(&halo_, sizeof(double) * hsize_ * 4));
   PE_HIP_CHECK(hipMalloc(&st_, sizeof(DevState)));
   PE_HIP_CHECK(hipHostMalloc(&hst_, sizeof(DevState) * 2, hipHostMallocDefault));
@@ -140,6 +156,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   PE_HIP_CHECK(hipEventCreate(&t1_));
 
   k.fused = fused_ ? 1 : 0;
+  k.steps = two_ ? 2 : 1;
   k.nx = nx;
   k.ny = ny;
   k.M = prob_.M;
@@ -164,9 +181,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.weighted = prob_.norm == Norm::Weighted ? 1 : 0;
   k.max_iter = prob_.iter_cap();
   for (int d = 0; d < 4; ++d) k.has[d] = blk_.has(d) ? 1 : 0;
-  k.colT = tables_;
-  k.rowcls = rowcls_;
-  k.rowT = tables_ + (rows_hi + 2) * 4;
+  // tables start at local index tab_lo_; the kernels index them by (local + 1)
+  k.colT = tables_ - (tab_lo_ + 1) * 4;
+  k.rowcls = rowcls_ - (tab_lo_ + 1) * 4;
+  k.rowT = tables_ + nrow_tab * 4 - (tab_lo_ + 1) * 4;
   k.send_dn = halo_;
   k.send_up = halo_ + hsize_;
   k.recv_dn = halo_ + 2 * hsize_;
@@ -233,8 +251,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   //    155-159 vs 188 µs, 2400×3200 80 vs 109).
   if (fused_ && ti_env == 0) ti = huge ? 18 : big ? 24 : 10;
   k.order = (fused_ && huge) ? 3 : 0;
+  if (two_) {  // static LPT layout only; taller items (8 pipeline-fill rows each)
+    if (ti_env == 0) ti = big ? 40 : 24;
+    ti = std::max(4, std::min(ti, dev::kTImax2));
+    k.order = 0;
+  }
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
   if (!fused_ && k.order > 1) k.order = 0;
+  if (two_) k.order = 0;
   k.ti = (fused_ && ti_env < 0) ? 1 << 20 : ti;  // bands mode: long items → general kernel
   int per_cu = fused_ ? dev::resident_blocks_S(k, 2) : dev::resident_blocks_classic(opt_.variant);
   if (per_cu <= 0) per_cu = 4;
@@ -262,6 +286,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // 8-rank 8192² block 10 rows — profiles/r2_mid_tune.txt).
   static constexpr int kTiCands[4] = {8, 10, 14, 18};
   tune_ti_ = fused_ && ti_env == 0 && k.order == 0 && npts >= double(1 << 20) && !big;
+  if (two_) tune_ti_ = false;  // (rows per item of the two-step sweep: fixed until measured)
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
   const int ti_min = tune_ti_ ? kTiCands[0] : ti;
   set_items(ti);
@@ -403,13 +428,18 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
-  const double t_iter = pts * (fused_ ? 48.0 : 64.0) / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
+  const double t_iter = pts * (two_ ? 24.0 : fused_ ? 48.0 : 64.0) / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
   int c = int(0.5e-3 / t_iter);
   c = std::max(8, std::min(128, c));
   c += c & 1;
+  if (two_) c = (c + 3) / 4 * 4;  // whole sweeps, an even number of them (graph parity)
   stream_chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
+  if (two_) {
+    chunk_ = (chunk_ + 3) / 4 * 4;
+    stream_chunk_ = chunk_;
+  }
   mark("tuning+rest");
   // PE_WARM_COPY=1: one small pageable copy at construction.  The runtime
   // sets up its pageable-copy path lazily at the first such copy of the
@@ -547,9 +577,11 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
   fields_ = x0;
   xalt_ = x1;
   walt_ = w;
-  k.x[0] = x0 + k.pitch + 1;  // local (0, 0): row -1, column -1 at element 0
-  k.x[1] = x1 + k.pitch + 1;
-  k.w = w + plane_ + 1;
+  // local (0, 0): row -(hdep-1), column -(hdep-1) at element 0
+  const int64_t h = hdep_ - 1;
+  k.x[0] = x0 + h * k.pitch + h;
+  k.x[1] = x1 + h * k.pitch + h;
+  k.w = w + h * plane_ + h;
   k.r = k.x[0];
   k.p[0] = k.x[0] + plane_;
   k.p[1] = k.x[1] + plane_;
@@ -655,13 +687,13 @@ void DeviceSolver::upload(void* dst, const void* src, size_t bytes) {
 }
 
 void DeviceSolver::build_tables(int64_t rows_hi, int64_t cols_hi) {
-  const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi);
+  const std::vector<double> t = chord_tables(prob_, blk_, rows_hi, cols_hi, tab_lo_);
   const auto t0 = clk::now();
   upload(tables_, t.data(), sizeof(double) * t.size());
   copy_setup_s_ += secs(t0, clk::now());
   const double* col = t.data();
-  const double* row = t.data() + (rows_hi + 2) * 4;
-  rowcls_host_ = row_classes(col, row, rows_hi, cols_hi);
+  const double* row = t.data() + (rows_hi - tab_lo_ + 1) * 4;
+  rowcls_host_ = row_classes(col, row, rows_hi, cols_hi, tab_lo_);
   const std::vector<int>& rc = rowcls_host_;
   const auto t1 = clk::now();
   upload(rowcls_, rc.data(), sizeof(int) * rc.size());
@@ -770,7 +802,7 @@ hipEvent_t DeviceSolver::pooled_event() {
 
 void DeviceSolver::mark_begin(int ph, hipStream_t s) {
   if (!sampling_) return;
-  PhaseRec r{ph, sample_iter_, 1, pooled_event(), nullptr};
+  PhaseRec r{ph, sample_iter_, two_ ? 2 : 1, pooled_event(), nullptr};  // (a two-step sweep covers 2 iterations)
   PE_HIP_CHECK(hipEventRecord(r.a, s));
   recs_.push_back(r);
 }
@@ -874,7 +906,7 @@ void DeviceSolver::enqueue_iteration(int par) {
       mark_end(stream_);
     }
   }
-  if (sampling_) ++sample_iter_;
+  if (sampling_) sample_iter_ += two_ ? 2 : 1;
 }
 
 // Chunk graphs are cached per length (a run of n iterations uses the chunk
@@ -882,11 +914,12 @@ void DeviceSolver::enqueue_iteration(int par) {
 hipGraphExec_t DeviceSolver::graph_for(int iters) {
   for (const auto& g : graphs_)
     if (g.first == iters) return g.second;
-  if (iters & 1) throw std::logic_error("graph chunks must have an even length");
+  const int per = two_ ? 2 : 1;
+  if (iters % (2 * per)) throw std::logic_error("graph chunks must hold an even number of sweeps");
   hipGraph_t g = nullptr;
   hipGraphExec_t ge = nullptr;
   PE_HIP_CHECK(hipStreamBeginCapture(stream_, hipStreamCaptureModeThreadLocal));
-  for (int it = 0; it < iters; ++it) enqueue_iteration(it & 1);
+  for (int it = 0; it < iters / per; ++it) enqueue_iteration(it & 1);
   PE_HIP_CHECK(hipStreamEndCapture(stream_, &g));
   PE_HIP_CHECK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
   PE_HIP_CHECK(hipGraphDestroy(g));
@@ -926,12 +959,14 @@ void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
     PE_HIP_CHECK(hipGetLastError());
     return;
   }
-  if (sample_iters == 0 && opt_.use_graph && graphs_usable() && par_ == 0 && iters >= 2) {
-    const int n = iters - (iters & 1);
+  // (two-step sweep: one launch = 2 iterations; chunks are multiples of 4)
+  const int per = two_ ? 2 : 1;
+  if (sample_iters == 0 && opt_.use_graph && graphs_usable() && par_ == 0 && iters >= 2 * per) {
+    const int n = iters - iters % (2 * per);
     PE_HIP_CHECK(hipGraphLaunch(graph_for(n), stream_));
     it = n;
   }
-  for (; it < iters; ++it) {
+  for (; it < iters; it += per) {
     sampling_ = it < sample_iters;
     enqueue_iteration(par_);
     par_ ^= 1;
@@ -944,8 +979,9 @@ void DeviceSolver::prepare_graphs(int64_t iters) {
   if (!graphs_usable()) return;
   // the chunk lengths run_iterations(iters) launches from parity 0
   const int64_t full = iters / chunk_, rest = iters % chunk_;
+  const int64_t q = two_ ? 4 : 2;
   if (full > 0) graph_for(chunk_);
-  if (rest >= 2) graph_for(int(rest - (rest & 1)));
+  if (rest >= q) graph_for(int(rest - rest % q));
   // the capture enqueued nothing: the stream state is unchanged
 }
 
@@ -1030,7 +1066,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
-  res.algo = resident_ ? "resident" : fused_ ? "fused" : "classic";
+  res.algo = resident_ ? "resident" : two_ ? "two-step" : fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   // T_solver spans construction (allocation, tables, placement search) like

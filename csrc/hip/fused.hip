@@ -1289,6 +1289,10 @@ static auto with_kS(const KParams& k, F&& f) {
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
+  if (k.steps == 2) {  // two iterations per sweep (fused2.hip)
+    launch_S2(k, par, s);
+    return;
+  }
   // each variant runs on its own resident grid (from the occupancy API; both
   // are 2 workgroups per CU since the band-coefficient LDS ring, 74 KB per
   // workgroup — the deferring sweep's 212 VGPRs alone would allow 2 as well)
@@ -1338,6 +1342,7 @@ void launch_wflush(const KParams& k, hipStream_t s) {
 }
 
 int resident_blocks_S(const KParams& k, int wm) {
+  if (k.steps == 2) return resident_blocks_S2();
   auto occ = [](auto kern) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kern, TJ, 0) != hipSuccess) n = 0;

@@ -1,0 +1,632 @@
+// Two-step single sweep: TWO Jacobi-PCG iterations per pass over memory.
+//
+// fused.hip's single sweep needs one pass per iteration because the scalars
+// of iteration k+1 depend on dot products of iteration k's vectors.  Here a
+// sweep advances iterations K+1 and K+2 at once: every scalar both of them
+// need is a quadratic form in dot products of basis vectors that the
+// PREVIOUS sweep could compute around its own outputs r_K, p_K (an s-step /
+// communication-avoiding CG with s = 2, in the exact-expansion form of the
+// single-reduction recurrence, without a stored basis):
+//
+//   z = D⁻¹r_K,  s = A p_K,  q = A z,  u = D⁻¹q,  v = D⁻¹s,  Au, Av
+//   p₁ = z + β₁p,          A p₁ = q + β₁s
+//   α₁ = (r,z)/(p₁,Ap₁),   r₁ = r − α₁Ap₁,   z₁ = z − α₁(u + β₁v)
+//   (r₁,z₁) = (r,z) − 2α₁(z,Ap₁) + α₁²(Ap₁, D⁻¹Ap₁)   → β₂
+//   p₂ = z₁ + β₂p₁ = (1+β₂)z + β₁β₂p − α₁u − α₁β₁v   → (p₂,Ap₂), ‖p₂‖² from
+//   the A-Gram and the plain Gram of {z, p, u, v}          → α₂
+//
+// so the sweep reads r_K, p_K, w and writes r_{K+2}, p_{K+2}, w:
+// 48 B per node per TWO iterations (24 B / iteration, against 40 for the
+// single sweep with its deferred w update), and ONE 20-sum reduction per two
+// iterations (half the cross-rank latency of the single sweep).  The stop
+// test of both iterations is known before the sweep (|α₁|‖p₁‖, |α₂|‖p₂‖), so
+// the iteration count and every terminal case keep the reference's exact
+// semantics (stage2-mpi/poisson_mpi_decomp.cpp:400-457: breakdown before the
+// update, stop after it); the sums are formed in a different order, which is
+// the only numerical difference (the prototype and the device reproduce the
+// golden counts: tests/test_gpu.py).
+//
+// Machine mapping (gfx950): the march of fused.hip with a 4-deep pipeline.
+// Each wave64 strip loads 128 columns and outputs the middle 120 (lanes
+// 2..61: the radius-4 dependence costs 2 lanes per side, all j-neighbours
+// come from DPP lane shifts); rows march with five stages in flight
+//   A  row t    p₁ = zc·D⁻¹r + β₁p                      (loads of row t)
+//   B  row t−1  s₁ = Ap₁, r₁, z₁, p₂
+//   C  row t−2  s₂ = Ap₂, r₂, z₂, v = D⁻¹s₂ → r₂, p₂, w += α₁p₁ + α₂p₂ stored
+//   D  row t−3  q = Az₂, u = D⁻¹q
+//   E  row t−4  Au, Av
+// and each stage adds its row's share of the 20 sums.  Rotating row windows
+// (period 2 or 3) live in registers; the loop is unrolled by 6 so every slot
+// index is a compile-time constant.  Boundary-band rows (items with the band
+// flag) evaluate their coefficients at each stage from the chord tables
+// (division-free cset_rc; a few % of the row steps).
+//
+// Layout: fused.hip's (x[b] interleaves the r and p planes by row) with a
+// 4-deep halo: local rows −3..nx+4 and columns −3..ny+4 hold data; buffer
+// element 0 of a row is column −3.
+#include <cstdlib>
+
+#include "kcommon.hpp"
+#include "peer_sum.hpp"
+
+#pragma clang fp contract(fast)
+
+namespace pe {
+namespace dev {
+
+namespace {
+
+constexpr int FSW2 = kFSW2;
+#ifndef PE_S2_XD
+#define PE_S2_XD 3
+#endif
+#ifndef PE_S2_WD
+#define PE_S2_WD 3
+#endif
+constexpr int kS2XD = PE_S2_XD, kS2WD = PE_S2_WD;
+constexpr int NS = kNS2;
+
+__device__ __forceinline__ double2 dd(double a, double b) { return make_double2(a, b); }
+__device__ __forceinline__ int2 cload_i2(const int2* p) {
+  const long long v = cload(reinterpret_cast<const long long*>(p));
+  return make_int2(int(v), int(v >> 32));
+}
+
+// Scalars of the sweep covering iterations K+1, K+2 (K = st->iter) from the
+// previous sweep's 20 unweighted sums R (a pure function of the state: every
+// wave evaluates it and gets the same bits).  Sum layout (kNS2):
+//   0 (r,z)  1 (z,q)  2 (z,s)  3 (p,s)  4 (q,u)  5 (u,s)  6 (s,v)  7 (u,Au)
+//   8 (u,Av) 9 (v,Av) 10 (z,z) 11 (z,p) 12 (z,u) 13 (z,v) 14 (p,p) 15 (p,u)
+//   16 (p,v) 17 (u,u) 18 (u,v) 19 (v,v)
+struct Scal2 {
+  bool first;
+  long long K;
+  double zc, g1, b1, den1, a1, d1, g2, b2, den2, a2, d2;
+};
+
+__device__ __forceinline__ double qform(const double (&c)[4], const double (&m)[4][4]) {
+  double s = 0.0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    s += c[i] * c[i] * m[i][i];
+#pragma unroll
+    for (int j = i + 1; j < 4; ++j) s += 2.0 * c[i] * c[j] * m[i][j];
+  }
+  return s;
+}
+
+__device__ __forceinline__ Scal2 sweep2_scalars(const KParams& k, const DevState* st, int par) {
+  Scal2 c;
+  c.first = st->started == 0;
+  c.K = st->iter;
+  c.zc = c.g1 = c.b1 = c.a1 = c.d1 = c.g2 = c.b2 = c.a2 = c.d2 = 0.0;
+  c.den1 = c.den2 = 1.0;
+  if (c.first) return c;
+  const double hh = k.h1 * k.h2;
+  const double* R = st->fs2[par ^ 1];
+  c.zc = 1.0;
+  c.g1 = R[0] * hh;
+  c.b1 = c.K == 0 ? 0.0 : c.g1 / st->gprev;
+  c.den1 = (R[1] + 2.0 * c.b1 * R[2] + c.b1 * c.b1 * R[3]) * hh;
+  c.a1 = c.g1 / c.den1;
+  const double pn1 = fmax(R[10] + 2.0 * c.b1 * R[11] + c.b1 * c.b1 * R[14], 0.0);
+  c.d1 = k.weighted ? fabs(c.a1) * sqrt(pn1 * hh) : fabs(c.a1) * sqrt(pn1);
+  c.g2 = (R[0] - 2.0 * c.a1 * (R[1] + c.b1 * R[2]) + c.a1 * c.a1 * (R[4] + 2.0 * c.b1 * R[5] + c.b1 * c.b1 * R[6])) * hh;
+  c.b2 = c.g2 / c.g1;
+  const double cf[4] = {1.0 + c.b2, c.b1 * c.b2, -c.a1, -c.a1 * c.b1};
+  const double G[4][4] = {{R[1], R[2], R[4], R[5]}, {R[2], R[3], R[5], R[6]}, {R[4], R[5], R[7], R[8]},
+                          {R[5], R[6], R[8], R[9]}};
+  const double P[4][4] = {{R[10], R[11], R[12], R[13]}, {R[11], R[14], R[15], R[16]}, {R[12], R[15], R[17], R[18]},
+                          {R[13], R[16], R[18], R[19]}};
+  c.den2 = qform(cf, G) * hh;
+  c.a2 = c.g2 / c.den2;
+  const double pn2 = fmax(qform(cf, P), 0.0);
+  c.d2 = k.weighted ? fabs(c.a2) * sqrt(pn2 * hh) : fabs(c.a2) * sqrt(pn2);
+  return c;
+}
+
+// How the sweep ends the solve, if it does (a pure function of the scalars):
+//   brk1  iteration K+1 breaks down (|den| < 1e-15 or non-finite scalars):
+//         stop before its update (reference :413), w unchanged;
+//   last1 iteration K+1 converges / hits the cap: w += α₁p₁ only;
+//   brk2  iteration K+2 breaks down: w += α₁p₁ only (K+1 completed);
+//   last2 iteration K+2 converges / hits the cap: the full sweep, then stop.
+struct Term2 {
+  bool brk1, bad1, last1, conv1, brk2, bad2, last2, conv2;
+};
+__device__ __forceinline__ Term2 sweep2_term(const KParams& k, const Scal2& c) {
+  Term2 t{false, false, false, false, false, false, false, false};
+  if (c.first) return t;
+  const bool tiny1 = fabs(c.den1) < 1e-15;
+  t.bad1 = !isfinite(c.g1) || !isfinite(c.den1) || (!tiny1 && !isfinite(c.d1));
+  t.brk1 = t.bad1 || tiny1;
+  if (t.brk1) return t;
+  t.conv1 = k.check_tol && c.d1 < k.tol;
+  t.last1 = t.conv1 || c.K + 1 >= k.max_iter;
+  if (t.last1) return t;
+  const bool tiny2 = fabs(c.den2) < 1e-15;
+  t.bad2 = !isfinite(c.g2) || !isfinite(c.den2) || (!tiny2 && !isfinite(c.d2));
+  t.brk2 = t.bad2 || tiny2;
+  if (t.brk2) return t;
+  t.conv2 = k.check_tol && c.d2 < k.tol;
+  t.last2 = t.conv2 || c.K + 2 >= k.max_iter;
+  return t;
+}
+
+__device__ __forceinline__ void hist_put(const KParams& k, long long kiter, double d) {
+  if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = d;
+}
+
+// Terminal state of a sweep that stops before its own work (brk1 / last1 /
+// brk2); one thread, after every wave of the grid has read the state.
+__device__ __forceinline__ void sweep2_terminal(const KParams& k, DevState* st, const Scal2& c, const Term2& t) {
+  if (t.brk1) {
+    st->status = t.bad1 ? 4 : 2;
+    st->iter = c.K + 1;
+  } else {
+    hist_put(k, c.K + 1, c.d1);
+    st->last_diff = c.d1;
+    st->alpha = c.a1;
+    st->beta = c.b1;
+    st->rz_cur = c.g1;
+    st->gprev = c.g1;
+    if (t.last1) {
+      st->iter = c.K + 1;
+      st->status = t.conv1 ? 1 : 3;
+    } else {  // brk2
+      st->iter = c.K + 2;
+      st->status = t.bad2 ? 4 : 2;
+    }
+  }
+  st->done = 1;
+  st->wpend = 0;
+}
+
+// State update after a full sweep (one thread; sums t[] global).
+__device__ __forceinline__ void sweep2_finalize(const KParams& k, DevState* st, int par, const Scal2& c,
+                                                const Term2& tm, const double (&t)[NS]) {
+#pragma unroll
+  for (int n = 0; n < NS; ++n) st->fs2[par][n] = t[n];
+  // fault hooks (PE_FAULT_INJECT): the sums of the sweep completing iteration K
+  if (k.fault_iter > 0 && (c.K + 1 == k.fault_iter || c.K + 2 == k.fault_iter) && !c.first)
+    st->fs2[par][1] = __builtin_nan("");
+  if (k.fault_zero > 0 && (c.K + 1 == k.fault_zero || c.K + 2 == k.fault_zero) && !c.first)
+    st->fs2[par][1] = st->fs2[par][2] = st->fs2[par][3] = 0.0;
+  st->wpend = 0;
+  st->wpar = par;
+  if (c.first) {
+    st->started = 1;
+    return;
+  }
+  hist_put(k, c.K + 1, c.d1);
+  hist_put(k, c.K + 2, c.d2);
+  st->last_diff = c.d2;
+  st->alpha = c.a2;
+  st->beta = c.b2;
+  st->rz_cur = c.g2;
+  st->gprev = c.g2;
+  st->iter = c.K + 2;
+  if (tm.last2) {
+    st->status = tm.conv2 ? 1 : 3;
+    st->done = 1;
+  }
+}
+
+// w += α₁ p₁ pointwise over the owned nodes (terminal paths last1 / brk2):
+// p₁ = zc·D⁻¹r + β₁p from the input buffer, 1/D from the march's own
+// coefficient path (cset_rc) so p₁ has the sweep's bits.
+__device__ void w_add_p1(const KParams& k, const double* xin, const Scal2& c) {
+  const int64_t n = k.nx * k.ny;
+  for (int64_t idx = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * blockDim.x) {
+    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
+    const double r = xin[li * k.pitch + lj], pold = xin[li * k.pitch + k.poff + lj];
+    const int* rc = k.rowcls + (li + 1) * 4;
+    const double* ctr = k.colT + (li + 1) * 4;
+    const double* tv = k.rowT + (lj + 1) * 4;
+    const double d = cset_rc(k, RowCls{rc[0], rc[1], rc[2], rc[3]}, CT{ctr[0], ctr[4], ctr[1], ctr[2]}, lj,
+                             TV{tv[0], tv[1], tv[2], tv[6]}).d;
+    const double p1 = c.zc * (r * d) + c.b1 * pold;
+    double& w = k.w[li * k.wpitch + lj];
+    w = w + c.a1 * p1;
+  }
+}
+
+// Per-wave LDS: the tables a boundary-band row evaluates its coefficients
+// from — the strip's row-table entries (per column) and the item's
+// column-table entries and row classes (per row, rows t0 .. t0+63) — and a
+// ring of the face coefficients of the last 6 rows (band items only).  A row
+// is evaluated ONCE, when it enters the pipeline (stage A): its vertical-face
+// a0 and horizontal-face b0 per column go to ring slot (row − t0) mod 6; the
+// stages that apply the operator to a band row read a0 of the row and of the
+// row below it (= its a1), b0 of the column and of the next one (= its b1,
+// written by the neighbouring lane) and form 1/D from them (dinv_faces: the
+// bits of the evaluation).  Plain rows keep the select path and no ring
+// reads.  In LDS rather than lanes: the five-stage march would spill.
+struct WaveTV2 {
+  double sA[128], eA[128], hB[130];
+  int4 rc[64];
+  double half[65], sB[64], eB[64];
+  double a0r[6][128];
+  double b0r[6][130];
+};
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st2nt(double* p, double2 v) {
+  __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+}
+__device__ __forceinline__ double2 ldnt(const double* p) {
+  const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+  return make_double2(t.x, t.y);
+}
+
+struct RowCtx {
+  int2 rcv;      // interior interval of row segbase + lane (lane l ↔ row segbase + l)
+  unsigned long long genmask;
+  int segbase;
+};
+
+// Stage rows below the item's first row (pipeline fill) are garbage rows
+// whose results are never used: the lane index is wrapped, not trusted.
+__device__ __forceinline__ void row_in(const RowCtx& rx, int q, int c0, bool& in0, bool& in1, bool& gen) {
+  const int l = (q - rx.segbase) & 63;
+  const int lo = __builtin_amdgcn_readlane(rx.rcv.x, l), hi = __builtin_amdgcn_readlane(rx.rcv.y, l);
+  in0 = c0 >= lo && c0 <= hi;
+  in1 = c0 + 1 >= lo && c0 + 1 <= hi;
+  gen = (rx.genmask >> l) & 1ull;
+}
+
+__device__ __forceinline__ double lap(const KParams& k, double f, double pm, double p0, double pn, double pl,
+                                      double pr) {
+  return f * (((p0 - pm) - (pn - p0)) * k.ih1sq + ((p0 - pl) - (pr - p0)) * k.ih2sq);
+}
+
+// Stage A of a band item: row q's faces into ring slot `sl`; returns 1/D.
+__device__ __forceinline__ double2 enter_band(const KParams& k, const RowCtx& rx, WaveTV2& tv, int q, int c0, int jl,
+                                              int sl) {
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  double2 d, a0, b0;
+  if (gen) {
+    const int l = (q - rx.segbase) & 63;
+    const int4 r4 = tv.rc[l];
+    const RowCls rc{r4.x, r4.y, r4.z, r4.w};
+    const CT ct{tv.half[l], tv.half[l + 1], tv.sB[l], tv.eB[l]};
+    const CS x0 = cset_rc(k, rc, ct, c0, TV{tv.sA[jl], tv.eA[jl], tv.hB[jl], tv.hB[jl + 1]});
+    const CS x1 = cset_rc(k, rc, ct, c0 + 1, TV{tv.sA[jl + 1], tv.eA[jl + 1], tv.hB[jl + 1], tv.hB[jl + 2]});
+    d = dd(x0.d, x1.d);
+    a0 = dd(x0.a0, x1.a0);
+    b0 = dd(x0.b0, x1.b0);
+  } else {
+    const double f0 = in0 ? 1.0 : k.inv_eps, f1 = in1 ? 1.0 : k.inv_eps;
+    d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+    a0 = dd(f0, f1);
+    b0 = a0;
+  }
+  *reinterpret_cast<double2*>(&tv.a0r[sl][jl]) = a0;
+  *reinterpret_cast<double2*>(&tv.b0r[sl][jl]) = b0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return d;
+}
+
+// The 5-point operator at row q (slot sl, the row below it in slot sln) for
+// the lane's two columns; d = 1/D of the row.
+template <bool BAND>
+__device__ __forceinline__ double2 apply2(const KParams& k, const RowCtx& rx, const WaveTV2& tv, int q, int c0, int jl,
+                                          int sl, int sln, const double2& um, const double2& u0, const double2& un,
+                                          double2& d) {
+  const double ul = dpp_shr1(u0.y), ur = dpp_shl1(u0.x);
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  if (BAND && gen) {
+    const double2 a0 = *reinterpret_cast<const double2*>(&tv.a0r[sl][jl]);
+    const double2 a1 = *reinterpret_cast<const double2*>(&tv.a0r[sln][jl]);
+    const double2 b0 = *reinterpret_cast<const double2*>(&tv.b0r[sl][jl]);
+    const double b2 = tv.b0r[sl][jl + 2];
+    const CS x0{a0.x, a1.x, b0.x, b0.y, dinv_faces(k, a0.x, a1.x, b0.x, b0.y)};
+    const CS x1{a0.y, a1.y, b0.y, b2, dinv_faces(k, a0.y, a1.y, b0.y, b2)};
+    d = dd(x0.d, x1.d);
+    return dd(stencil<false>(k, x0, um.x, u0.x, un.x, ul, u0.y), stencil<false>(k, x1, um.y, u0.y, un.y, u0.x, ur));
+  }
+  d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+  return dd(lap(k, in0 ? 1.0 : k.inv_eps, um.x, u0.x, un.x, ul, u0.y),
+            lap(k, in1 ? 1.0 : k.inv_eps, um.y, u0.y, un.y, u0.x, ur));
+}
+
+__device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx, int q, int c0) {
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  return dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+}
+
+// The item march (one strip × rows ib..ie), accumulating this wave's sums.
+// Sums are taken over the item's rows (uniform row tests) without per-term
+// column masks: every sum has a factor among z, p, u, v, which are exactly 0
+// at the global-boundary and padding columns (z, u, v masked there; p stays 0),
+// and the lanes that do not own their columns (0, 1, 62, 63: the recomputed
+// halo of the strip) are dropped once, at the end of the sweep.  (Blocks
+// split across y — halo columns with real data — are not run by this kernel.)
+template <bool BAND>
+__device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par, int s, int ib, int ie,
+                                      WaveTV2& tvw, double (&acc)[NS]) {
+  const int lane = threadIdx.x & 63;
+  const int ny = int(k.ny);
+  const int64_t pitch = k.pitch, poff = k.poff, wp = k.wpitch;
+  const double* __restrict__ Xm = k.x[par ^ 1] - 3;  // row pointers at column -3
+  double* __restrict__ Ym = k.x[par] - 3;
+  double* __restrict__ Wm = k.w - 3;
+  const int J = -3 + s * FSW2;
+  const int c0 = J + 2 * lane;
+  const int jl = 2 * lane;
+  const unsigned off = unsigned(c0 + 3);
+  const int64_t g0 = k.gj0 + c0;
+  const bool lv0 = c0 <= ny + 4 && g0 >= 1 && g0 <= k.N - 1;
+  const bool lv1 = c0 + 1 <= ny + 4 && g0 + 1 >= 1 && g0 + 1 <= k.N - 1;
+  const bool inner = lane >= 2 && lane <= 61;
+  const bool o0 = inner && c0 >= 1 && c0 <= ny;
+  const bool o1 = inner && c0 + 1 >= 1 && c0 + 1 <= ny;
+  const double a1 = sc.a1, b1 = sc.b1, a2 = sc.a2, b2 = sc.b2, zc = sc.zc;
+
+  // Row classes / column tables of rows t0 .. t0+63 (one per lane; items
+  // have ≤ kTImax2 rows, so rows ib-4 .. ie+5 fit).
+  const int t0 = ib - 4;
+  RowCtx rx;
+  rx.segbase = t0;
+  {
+    const int nr = ie + 6 - t0;
+    const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (t0 + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+    rx.rcv = make_int2(rc4.x, rc4.y);
+    rx.genmask = 0;
+    if (BAND) {
+      rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
+      if (rx.genmask != 0) {
+        const double* ctr = k.colT + (min(t0 + lane, ie + 5) + 1) * 4;
+        tvw.rc[lane] = rc4;
+        tvw.half[lane] = ctr[0];
+        tvw.sB[lane] = ctr[1];
+        tvw.eB[lane] = ctr[2];
+        if (lane == 63) tvw.half[64] = ctr[4];
+        const double* tb = k.rowT + (c0 + 1) * 4;
+        const double4 a = *reinterpret_cast<const double4*>(tb);
+        const double4 b = *reinterpret_cast<const double4*>(tb + 4);
+        tvw.sA[jl] = a.x;
+        tvw.eA[jl] = a.y;
+        tvw.hB[jl] = a.z;
+        tvw.sA[jl + 1] = b.x;
+        tvw.eA[jl + 1] = b.y;
+        tvw.hB[jl + 1] = b.z;
+        if (lane == 63) {
+          tvw.hB[128] = tb[10];
+          tvw.hB[129] = tb[14];
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+      }
+    }
+  }
+  auto interior = [&](int q) {  // global interior row
+    const int64_t gr = k.gi0 + q;
+    return gr >= 1 && gr <= k.M - 1;
+  };
+  auto ldx = [&](int t, unsigned o) -> double2 { return ld2(Xm + int64_t(t) * pitch + o); };
+
+  // prefetch ring (3 rows): x rows t, t+1, t+2; w rows t-2, t-1, t
+  const int tmax = ie + 4;
+  // rows of loads in flight: x (r, p) XD, w WD (each 2 or 3: divides the unroll)
+  constexpr int XD = kS2XD, WD = kS2WD;
+  double2 RQ[XD], PQ[XD], WQ[WD];
+#pragma unroll
+  for (int q = 0; q < XD; ++q) {
+    const int t = min(t0 + q, tmax);
+    RQ[q] = ldx(t, off);
+    PQ[q] = ldx(t, poff + off);
+  }
+#pragma unroll
+  for (int q = 0; q < WD; ++q) WQ[q] = ldnt(Wm + int64_t(min(max(t0 - 2 + q, ib), ie)) * wp + off);
+  double2 P1[3], RI[2], R1[2], P2[3], Z2[3], S2[2], V[3], U[3];
+#pragma unroll
+  for (int q = 0; q < 3; ++q) P1[q] = P2[q] = Z2[q] = V[q] = U[q] = dd(0.0, 0.0);
+#pragma unroll
+  for (int q = 0; q < 2; ++q) RI[q] = R1[q] = S2[q] = dd(0.0, 0.0);
+  double (&sv)[NS] = acc;  // the wave's running sums
+
+  const int nsteps = ie + 4 - t0 + 1;
+  for (int g = 0; 6 * g < nsteps; ++g) {
+#pragma unroll
+    for (int jj = 0; jj < 6; ++jj) {
+      const int n = 6 * g + jj;
+      if (n >= nsteps) break;
+      const int t = t0 + n;
+      // slots (compile-time): m3[d] = (n - d) mod 3, m2[d] = (n - d) mod 2
+      const int s0 = jj % 3, s1 = (jj + 2) % 3, s2 = (jj + 1) % 3;  // rows t, t-1, t-2 (mod 3): t-3 ≡ t
+      const int e0 = jj & 1, e1 = (jj + 1) & 1;                     // rows t, t-1 (mod 2): t-2 ≡ t
+      const int r0 = jj, r1s = (jj + 5) % 6, r2s = (jj + 4) % 6;    // band ring slots (mod 6) of rows t .. t-4
+      const int r3s = (jj + 3) % 6, r4s = (jj + 2) % 6;
+      // ---- A: row t ----
+      const int xs = jj % XD, ws = jj % WD;
+      const double2 rin = RQ[xs], pin = PQ[xs], wrow = WQ[ws];
+      {
+        const int tn = min(t + XD, tmax);
+        RQ[xs] = ldx(tn, off);
+        PQ[xs] = ldx(tn, poff + off);
+        WQ[ws] = ldnt(Wm + int64_t(min(max(t - 2 + WD, ib), ie)) * wp + off);
+      }
+      {
+        const double2 d = BAND ? enter_band(k, rx, tvw, t, c0, jl, r0) : dinv_plain(k, rx, t, c0);
+        const bool ri = interior(t);
+        const double z0 = (ri && lv0) ? rin.x * d.x : 0.0, z1 = (ri && lv1) ? rin.y * d.y : 0.0;
+        P1[s0] = dd(zc * z0 + b1 * pin.x, zc * z1 + b1 * pin.y);
+        RI[e0] = rin;
+      }
+      // ---- B: row t-1 ----
+      {
+        double2 d;
+        const double2 s1v = apply2<BAND>(k, rx, tvw, t - 1, c0, jl, r1s, r0, P1[s2], P1[s1], P1[s0], d);
+        const double2 ri = RI[e1];
+        const double2 r1 = dd(ri.x - a1 * s1v.x, ri.y - a1 * s1v.y);
+        const bool rr = interior(t - 1);
+        const double z0 = (rr && lv0) ? r1.x * d.x : 0.0, z1 = (rr && lv1) ? r1.y * d.y : 0.0;
+        const double2 p1 = P1[s1];
+        R1[e1] = r1;
+        P2[s1] = dd(zc * z0 + b2 * p1.x, zc * z1 + b2 * p1.y);
+      }
+      // ---- C: row t-2 (outputs) ----
+      {
+        const int q = t - 2;
+        double2 d;
+        const double2 s2v = apply2<BAND>(k, rx, tvw, q, c0, jl, r2s, r1s, P2[s0], P2[s2], P2[s1], d);
+        const double2 r1 = R1[e0];
+        const double2 r2 = dd(r1.x - a2 * s2v.x, r1.y - a2 * s2v.y);
+        const bool rr = interior(q);
+        const double2 z2 = dd((rr && lv0) ? r2.x * d.x : 0.0, (rr && lv1) ? r2.y * d.y : 0.0);
+        Z2[s2] = z2;
+        S2[e0] = s2v;
+        const double2 p2 = P2[s2];
+        if (q >= ib && q <= ie) {
+          const double2 p1 = P1[s2];
+          const double2 wv = dd(wrow.x + a1 * p1.x + a2 * p2.x, wrow.y + a1 * p1.y + a2 * p2.y);
+          double* yr = Ym + int64_t(q) * pitch + off;
+          double* wd = Wm + int64_t(q) * wp + off;
+          if (o0 && o1) {
+            st2nt(yr, r2);
+            st2nt(yr + poff, p2);
+            st2nt(wd, wv);
+          } else if (o0) {
+            yr[0] = r2.x;
+            yr[poff] = p2.x;
+            wd[0] = wv.x;
+          }
+          sv[0] += r2.x * z2.x + r2.y * z2.y;            // (r,z)
+          sv[2] += z2.x * s2v.x + z2.y * s2v.y;          // (z,s)
+          sv[3] += p2.x * s2v.x + p2.y * s2v.y;          // (p,s)
+          sv[10] += z2.x * z2.x + z2.y * z2.y;           // (z,z)
+          sv[11] += z2.x * p2.x + z2.y * p2.y;           // (z,p)
+          sv[14] += p2.x * p2.x + p2.y * p2.y;           // (p,p)
+        }
+      }
+      // ---- D: row t-3 ----
+      {
+        const int q = t - 3;
+        double2 d;
+        const double2 qv = apply2<BAND>(k, rx, tvw, q, c0, jl, r3s, r2s, Z2[s1], Z2[s0], Z2[s2], d);
+        const bool rr = interior(q);
+        const double2 sr = S2[e1];
+        const double2 u = dd((rr && lv0) ? qv.x * d.x : 0.0, (rr && lv1) ? qv.y * d.y : 0.0);
+        const double2 v = dd((rr && lv0) ? sr.x * d.x : 0.0, (rr && lv1) ? sr.y * d.y : 0.0);
+        U[s0] = u;
+        V[s0] = v;
+        if (q >= ib && q <= ie) {
+          const double2 z = Z2[s0], p = P2[s0];
+          sv[1] += z.x * qv.x + z.y * qv.y;              // (z,q)
+          sv[4] += qv.x * u.x + qv.y * u.y;              // (q,u)
+          sv[5] += u.x * sr.x + u.y * sr.y;              // (u,s)
+          sv[6] += sr.x * v.x + sr.y * v.y;              // (s,v)
+          sv[12] += z.x * u.x + z.y * u.y;               // (z,u)
+          sv[13] += z.x * v.x + z.y * v.y;               // (z,v)
+          sv[15] += p.x * u.x + p.y * u.y;               // (p,u)
+          sv[16] += p.x * v.x + p.y * v.y;               // (p,v)
+          sv[17] += u.x * u.x + u.y * u.y;               // (u,u)
+          sv[18] += u.x * v.x + u.y * v.y;               // (u,v)
+          sv[19] += v.x * v.x + v.y * v.y;               // (v,v)
+        }
+      }
+      // ---- E: row t-4 ----
+      {
+        const int q = t - 4;
+        if (q >= ib && q <= ie) {
+          double2 d;
+          const double2 au = apply2<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, U[s2], U[s1], U[s0], d);
+          const double2 av = apply2<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, V[s2], V[s1], V[s0], d);
+          const double2 u = U[s1], v = V[s1];
+          sv[7] += u.x * au.x + u.y * au.y;              // (u,Au)
+          sv[8] += u.x * av.x + u.y * av.y;              // (u,Av)
+          sv[9] += v.x * av.x + v.y * av.y;              // (v,Av)
+        }
+      }
+    }
+  }
+}
+
+__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS2(KParams k, int par) {
+  DevState* st = k.st;
+  const int done = st->done;
+  const Scal2 sc = sweep2_scalars(k, st, par);
+  const Term2 tm = sweep2_term(k, sc);
+  __shared__ double sm[4 * NS];
+  __shared__ int sflag;
+  __shared__ WaveTV2 tvs[kWPB];
+  const int lane = int(threadIdx.x & 63);
+  const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  if (done) return;
+  if (tm.brk1 || tm.last1 || tm.brk2) {
+    if (!tm.brk1) w_add_p1(k, k.x[par ^ 1], sc);
+    if (arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
+      sweep2_terminal(k, st, sc, tm);
+      __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
+  double acc[NS];
+#pragma unroll
+  for (int n = 0; n < NS; ++n) acc[n] = 0.0;
+  {  // band ring: defined contents (the never-written column 128 of b0 and the
+     // slots garbage pipeline-fill rows read stay finite)
+    WaveTV2& tv = tvs[wid];
+    for (int i = lane; i < 6 * 128; i += 64) (&tv.a0r[0][0])[i] = 0.0;
+    for (int i = lane; i < 6 * 130; i += 64) (&tv.b0r[0][0])[i] = 0.0;
+  }
+  const int W = k.lwaves;
+  for (int pos = int(blockIdx.x) * kWPB + wid; pos < k.nslots; pos += W) {
+    const int2 e = cload_i2(k.ilist + pos);
+    const int rows = e.y >> 20;
+    if (rows == 0) continue;  // empty position of the static layout
+    const int s = e.y & 0xFFFFF, ib = e.x & kRowMask;
+    const int ie = min(ib + rows - 1, int(k.nx));
+    if (e.x & kBandBit) march<true>(k, sc, par, s, ib, ie, tvs[wid], acc);
+    else march<false>(k, sc, par, s, ib, ie, tvs[wid], acc);
+  }
+  if (lane < 2 || lane > 61)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
+#pragma unroll
+    for (int n = 0; n < NS; ++n) acc[n] = 0.0;
+  block_reduce<NS, false>(acc, sm);
+  if (publish_last<NS>(k.partial + NS * size_t(blockIdx.x), acc, &st->ticket[0], gridDim.x, &sflag)) {
+    double t[NS];
+    reduce_partials<NS>(k.partial, gridDim.x, t, sm);
+    __shared__ double xv[NS + 1];
+    __shared__ unsigned long long sseq;
+    __shared__ int sok;
+    if (k.xr.peers) {  // cross-rank sum of the 20 sums inside the sweep (P2P transport)
+      if (threadIdx.x == 0)
+#pragma unroll
+        for (int n = 0; n < NS; ++n) xv[n] = t[n];
+      peer_sum_block(k.xr, xv, NS, &sseq, &sok);
+      if (threadIdx.x == 0)
+#pragma unroll
+        for (int n = 0; n < NS; ++n) t[n] = xv[n];
+    }
+    if (threadIdx.x == 0) {
+      sweep2_finalize(k, st, par, sc, tm, t);
+      __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+}  // namespace
+
+void launch_S2(const KParams& k, int par, hipStream_t s) {
+  hipLaunchKernelGGL(kS2, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+}
+
+int resident_blocks_S2() {
+  int n = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kS2, TJ, 0) != hipSuccess) {
+    (void)hipGetLastError();
+    n = 0;
+  }
+  return n;
+}
+
+}  // namespace dev
+}  // namespace pe

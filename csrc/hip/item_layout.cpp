@@ -119,9 +119,10 @@ void DeviceSolver::setup_items() {
   const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
   // Does local row q have a boundary-band node in strip s's 128 loaded
   // columns?  (The kernel's has_gen on the same row-class table.)
+  const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step)
   auto row_gen = [&](int64_t q, int s) {
-    const int64_t J = -1 + int64_t(s) * dev::kFSW;
-    const int64_t t = q + 1;  // table index of local row q
+    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
+    const int64_t t = q - tab_lo_;  // table index of local row q
     if (t < 0 || t >= rows_tab) return false;
     const int* r = &rowcls_host_[size_t(t) * 4];
     const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
@@ -129,11 +130,11 @@ void DeviceSolver::setup_items() {
   };
   auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
     double c = 0.0;
-    for (int64_t q = ib - 2; q <= ie + 2; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
+    for (int64_t q = ib - H; q <= ie + H; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
     return c;
   };
   auto rows_band = [&](int64_t ib, int64_t ie, int s) {
-    for (int64_t q = ib - 2; q <= ie + 2; ++q)
+    for (int64_t q = ib - H; q <= ie + H; ++q)
       if (row_gen(q, s)) return true;
     return false;
   };
@@ -142,7 +143,7 @@ void DeviceSolver::setup_items() {
     return rows_cost(ib, ie, s);
   };
   // {first row | band flag, strip | rows << 20}; the band flag selects the
-  // kernel's coefficient path (rows ib-2 .. ie+2 include a boundary-band row)
+  // kernel's coefficient path (rows ib-H .. ie+H include a boundary-band row)
   auto entry = [&](int64_t ib, int64_t rows, int s) {
     const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
     return int2{int(ib) | flag, s | int(rows << 20)};
@@ -151,8 +152,8 @@ void DeviceSolver::setup_items() {
   // feed the exchange) and under the halo push (their xGMI stores then
   // overlap the rest of the sweep instead of ending it)
   auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
-    const int64_t J = -1 + int64_t(s) * dev::kFSW;
-    const int64_t jlo = std::max<int64_t>(1, J + 2), jhi = std::min<int64_t>(blk_.ny, J + dev::kFSW + 1);
+    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
+    const int64_t jlo = std::max<int64_t>(1, J + H), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + H - 1);
     return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
            ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
             (blk_.has(UP) && jhi >= blk_.ny - 1));
@@ -185,7 +186,7 @@ void DeviceSolver::setup_items() {
     // more items than waves the layout balances them, and every cut re-reads
     // 4 more halo rows (2048²: 96 vs 91 µs per iteration with cuts)
     const int W0 = std::max(1, std::min(waves_avail, k.nitems));
-    const double share = k.nitems >= waves_avail ? 1e300 : std::max(total / W0, (double(k.ti + 4) + overhead) * 1.15);
+    const double share = k.nitems >= waves_avail ? 1e300 : std::max(total / W0, (double(k.ti + 2 * H) + overhead) * 1.15);
     std::vector<Piece> pcs;
     for (int ch = 0; ch < nchunks; ++ch)
       for (int s = 0; s < k.nstrips; ++s) {
@@ -207,7 +208,7 @@ void DeviceSolver::setup_items() {
         }
       }
     // PE_SEGMENTS=1 (experiment): the segment layout below
-    if (const char* sg = std::getenv("PE_SEGMENTS"); sg && std::atoi(sg) == 1) {
+    if (const char* sg = std::getenv("PE_SEGMENTS"); sg && std::atoi(sg) == 1 && !two_) {
       // Segment layout: one tall item per wave.  Each strip's rows are cut
       // into segments of equal estimated cost, and the strips' segment
       // counts are dealt (largest remaining segment cost first) so that the
@@ -338,7 +339,7 @@ void DeviceSolver::setup_items() {
     for (int s = 0; s < k.nstrips; ++s) cc += cost[size_t(ch) * k.nstrips + s] = item_cost(ch, s);
     ccost[size_t(ch) + 1] = ccost[size_t(ch)] + cc;
   }
-  const double light = double(k.ti + 4);
+  const double light = double(k.ti + 2 * H);
   std::vector<int> cut(size_t(nsh) + 1, 0);
   for (int x = 1; x < nsh; ++x) {
     const double target = ccost.back() * x / nsh;
@@ -415,7 +416,8 @@ void DeviceSolver::setup_resident() {
   resident_ = false;
   const char* e = std::getenv("PE_RESIDENT");
   if (e && std::atoi(e) == 0) return;
-  if (!fused_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0) return;
+  if (!fused_ || two_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0)
+    return;
   const int nx = int(blk_.nx);
   int cus = 256;
   {
@@ -441,7 +443,7 @@ void DeviceSolver::setup_resident() {
       const int J0 = 1 + dev::kFSW * sx;
       for (int q = rs[size_t(t)] - 2; q < rs[size_t(t) + 1] + 2; ++q) {
         if (q + 1 < 0 || q + 1 >= rows_tab) continue;
-        const int* r = &rowcls_host_[size_t(q + 1) * 4];
+        const int* r = &rowcls_host_[size_t(q - tab_lo_) * 4];
         for (int c = J0 - 2; c < J0 + 126; ++c)
           if (c >= r[2] && c <= r[3] && !(c >= r[0] && c <= r[1])) ++nb;
       }

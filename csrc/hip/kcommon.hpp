@@ -313,6 +313,13 @@ struct CT {
   double half0, half1, sB, eB;
 };
 
+// 1/D from the four face coefficients (fast arithmetic; the one expression
+// every single-sweep path uses, so a diagonal recomputed from stored faces
+// has the bits of the one evaluated with them).
+__device__ __forceinline__ double dinv_faces(const KParams& k, double a0, double a1, double b0, double b1) {
+  return rcp_nr(fma(a1 + a0, k.ih1sq, (b1 + b0) * k.ih2sq));
+}
+
 // cset with the row class already in SGPRs (fast arithmetic).
 __device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, const CT& ct, int64_t lj, const TV& t) {
   CS x;
@@ -328,7 +335,7 @@ __device__ __forceinline__ CS cset_rc(const KParams& k, const RowCls& c, const C
     x.a1 = fcoef_fast(chord_len(ct.half1, t.sA, t.eA), k.h2, ih2, k.inv_eps);
     x.b0 = fcoef_fast(chord_len(t.hB, ct.sB, ct.eB), k.h1, ih1, k.inv_eps);
     x.b1 = fcoef_fast(chord_len(t.hB1, ct.sB, ct.eB), k.h1, ih1, k.inv_eps);
-    x.d = rcp_nr((x.a1 + x.a0) * k.ih1sq + (x.b1 + x.b0) * k.ih2sq);
+    x.d = dinv_faces(k, x.a0, x.a1, x.b0, x.b1);
   }
   return x;
 }

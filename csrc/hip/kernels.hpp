@@ -55,13 +55,16 @@ struct DevState {
   // so its wait is inside this one).
   unsigned long long xr_wait;
   unsigned long long xr_n;
+  // Two-step sweep (fused2.hip): the 20 unweighted sums of sweep k in
+  // fs2[k & 1] (layout: fused2.hip, sweep2_scalars).
+  double fs2[2][24];
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
 // peers[r] = rank r's buffer (2 × P slots of kP2PSlot doubles: n ≤ kP2PSlot-1
 // values + a sequence flag) mapped into this process, seq = this rank's
 // reduction counter (device), timeout in s_memrealtime ticks (100 MHz).
-constexpr int kP2PSlot = 16;
+constexpr int kP2PSlot = 24;  // ≥ 20 sums of the two-step sweep + the flag
 struct PeerSum {
   double* const* peers;
   unsigned long long* seq;
@@ -168,6 +171,9 @@ struct KParams {
   // PE_FAULT_INJECT=slow@rank:R,us:X — this rank's final reduction block
   // idles X µs (in ticks) before the cross-rank sum (T_MPI test hook)
   long long slow_ticks;
+  // iterations per sweep: 1 single sweep (fused.hip kS), 2 two-step sweep
+  // (fused2.hip kS2: 4-deep halo, 120-column strips, 20 sums)
+  int steps;
 };
 constexpr int kFoldGroup = 64;
 
@@ -181,6 +187,9 @@ constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live
 constexpr int kBandBit = 1 << 30;
 constexpr int kRowMask = kBandBit - 1;
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
+constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
+constexpr int kNS2 = 20;         // two-step sweep: sums per sweep
+constexpr int kTImax2 = 48;      // two-step sweep: max rows per item (rows ib-4 .. ie+5 live one per lane)
 
 // LDS-resident single sweep (resident.hip): small single-rank blocks run many
 // iterations in ONE launch.  The block is cut into tiles of one 124-column
@@ -267,6 +276,10 @@ void launch_delay(double us, hipStream_t s);  // test transport: stream-ordered 
 // Resident 256-thread blocks per CU of the marching kernels (occupancy API;
 // 0 when unavailable).  Sizes the persistent grids.
 int resident_blocks_S(const KParams& k, int wm);  // wm 0: deferring sweep, 2: applying sweep
+// Two-step sweep (fused2.hip): one launch = iterations K+1 and K+2 (static
+// item list only; launch_S dispatches here when k.steps == 2).
+void launch_S2(const KParams& k, int par, hipStream_t s);
+int resident_blocks_S2();
 // (k.ti / k.order select the kernel variant: set them first)
 int resident_blocks_classic(int variant);
 

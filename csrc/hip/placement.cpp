@@ -269,7 +269,8 @@ bool DeviceSolver::placement_search(bool retry) {
     // PE_PLACEMENT_FAST_TBS (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
     // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
     // 0.56-0.60 ms placements when better ones were a try or two further.)
-    const double tbs = 40.0 * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
+    const double bps = two_ ? 48.0 : 40.0;  // streamed bytes per node and sweep
+    const double tbs = bps * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
     if (tbs >= fast_tbs) {
       fast = true;
       break;
@@ -295,7 +296,7 @@ bool DeviceSolver::placement_search(bool retry) {
   // a retry appends its candidates (its first is the first round's pick, re-timed)
   placement_best_ = int(placement_ms_.size() + best);
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
-  return fast || 40.0 * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
+  return fast || (two_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
 }
 
 // Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE

@@ -163,6 +163,8 @@ class DeviceSolver {
   std::vector<HaloPhase> halo_phases(int buf) const;
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
+  // two iterations per sweep (fused2.hip)
+  bool two_step() const { return two_; }
   // LDS-resident single sweep (resident.hip): small single-rank blocks run
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
   bool resident() const { return resident_; }
@@ -258,6 +260,10 @@ class DeviceSolver {
   SolveOptions opt_;
   hipStream_t stream_ = nullptr;
   bool fused_ = false;
+  bool two_ = false;      // two-step sweep (fused2.hip): 2 iterations per launch
+  int fsw_ = 124;         // output columns per strip (kFSW / kFSW2)
+  int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4)
+  int64_t tab_lo_ = -1;   // first local index of the chord tables / row classes
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w
   double* xalt_ = nullptr;    // single-sweep: x1 (separate allocation)
   double* walt_ = nullptr;    // single-sweep: w
@@ -333,13 +339,17 @@ class DeviceSolver {
 // that every face coefficient of node (q, lj) is exactly 1 for lj ∈ [in_lo,
 // in_hi] and exactly 1/eps for lj ∉ [out_lo, out_hi], lj ∈ [-1, cols_hi].
 // Conservative: anything else is evaluated exactly.  (rows_hi+2) × 4 ints.
-std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi);
+// Tables and classes start at local index `lo` (-1; the two-step sweep's
+// 4-deep halo: -4): entry of local q at (q - lo).
+std::vector<int> row_classes(const double* colT, const double* rowT, int64_t rows_hi, int64_t cols_hi,
+                             int64_t lo = -1);
 // Chord tables of a block: (rows_hi+2)×4 column entries {halfA, sB, eB, x}
 // for li ∈ [-1, rows_hi], then (cols_hi+2)×4 row entries {sA, eA, halfB, y}
 // for lj ∈ [-1, cols_hi]; indexed by local index + 1.  The classic kernels
 // use rows_hi = nx+2, cols_hi = ny+2; the single-sweep kernel reaches two
 // halo nodes further and past ny into strip padding.
-std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi);
+std::vector<double> chord_tables(const Problem& P, const Block& blk, int64_t rows_hi, int64_t cols_hi,
+                                 int64_t lo = -1);
 // Host mirror of the kernels' coefficient path for local (li, lj) ∈
 // [0, nx+1] × [0, ny+1]: a(li, lj), b(li, lj) and the class (0 interior,
 // 1 exterior, 2 boundary band).  Row-major (nx+2) × (ny+2).

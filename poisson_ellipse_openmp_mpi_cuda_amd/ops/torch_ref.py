@@ -215,6 +215,95 @@ def single_sweep(prob: EllipseProblem, iters: int, device="cpu") -> SingleSweepS
     return SingleSweepState(iters, sums, alphas, betas, r, p, w)
 
 
+@dataclass
+class TwoStepState:
+    sweeps: int
+    sums: list    # per sweep j = 0 (S_0) .. J: the 20 unweighted sums (csrc/hip/fused2.hip layout)
+    alpha: list   # (α₁, α₂) per sweep j ≥ 1
+    beta: list    # (β₁, β₂)
+    diff: list    # (‖Δw‖ of iteration 2j-1, of 2j)
+    r: torch.Tensor
+    p: torch.Tensor
+    w: torch.Tensor
+
+
+def two_step_sums(r, p, a, b, h1, h2, Dinv):
+    """The 20 sums of the basis around (r, p) (fused2.hip, sweep2_scalars)."""
+    inner = lambda u, v: float((u[1:-1, 1:-1] * v[1:-1, 1:-1]).sum())  # noqa: E731  (unweighted)
+    A = lambda u: apply_A(u, a, b, h1, h2)  # noqa: E731
+    z = Dinv * r
+    s = A(p)
+    q = A(z)
+    u = Dinv * q
+    v = Dinv * s
+    Au, Av = A(u), A(v)
+    return [inner(r, z), inner(z, q), inner(z, s), inner(p, s), inner(q, u), inner(u, s), inner(s, v),
+            inner(u, Au), inner(u, Av), inner(v, Av), inner(z, z), inner(z, p), inner(z, u), inner(z, v),
+            inner(p, p), inner(p, u), inner(p, v), inner(u, u), inner(u, v), inner(v, v)]
+
+
+def two_step_scalars(R, gprev: float, K: int, hh: float, weighted: bool = True):
+    """(g1, β1, α1, ‖Δw‖1, g2, β2, α2, ‖Δw‖2) of the sweep covering iterations
+    K+1, K+2 from the previous sweep's sums R — the device's sweep2_scalars."""
+    g1 = R[0] * hh
+    b1 = 0.0 if K == 0 else g1 / gprev
+    den1 = (R[1] + 2.0 * b1 * R[2] + b1 * b1 * R[3]) * hh
+    a1 = g1 / den1
+    pn1 = max(R[10] + 2.0 * b1 * R[11] + b1 * b1 * R[14], 0.0)
+    d1 = abs(a1) * math.sqrt(pn1 * hh if weighted else pn1)
+    g2 = (R[0] - 2.0 * a1 * (R[1] + b1 * R[2]) + a1 * a1 * (R[4] + 2.0 * b1 * R[5] + b1 * b1 * R[6])) * hh
+    b2 = g2 / g1
+    c = [1.0 + b2, b1 * b2, -a1, -a1 * b1]
+    G = [[R[1], R[2], R[4], R[5]], [R[2], R[3], R[5], R[6]], [R[4], R[5], R[7], R[8]], [R[5], R[6], R[8], R[9]]]
+    P = [[R[10], R[11], R[12], R[13]], [R[11], R[14], R[15], R[16]], [R[12], R[15], R[17], R[18]],
+         [R[13], R[16], R[18], R[19]]]
+    qf = lambda m: sum(c[i] * c[j] * m[i][j] for i in range(4) for j in range(4))  # noqa: E731
+    den2 = qf(G) * hh
+    a2 = g2 / den2
+    pn2 = max(qf(P), 0.0)
+    d2 = abs(a2) * math.sqrt(pn2 * hh if weighted else pn2)
+    return g1, b1, a1, d1, g2, b2, a2, d2, den1, den2
+
+
+def two_step(prob: EllipseProblem, sweeps: int, device="cpu") -> TwoStepState:
+    """The two-iterations-per-sweep recurrence of csrc/hip/fused2.hip on the
+    reference operator (divisions): S_0 (the sums around r₀ = B, p₀ = 0),
+    then `sweeps` sweeps, each advancing iterations K+1 and K+2 with scalars
+    from the previous sweep's 20 sums.  Algebraically the reference PCG
+    (stage2-mpi/poisson_mpi_decomp.cpp:400-457), two iterations at a time."""
+    a, b, B = assemble(prob, device)
+    h1, h2 = prob.h1, prob.h2
+    hh = h1 * h2
+    D = diag(a, b, h1, h2)
+    Dinv = torch.zeros_like(D)
+    m = D != 0
+    Dinv[m] = 1.0 / D[m]
+    A = lambda u: apply_A(u, a, b, h1, h2)  # noqa: E731
+    r = B.clone()
+    p = torch.zeros_like(B)
+    w = torch.zeros_like(B)
+    sums = [two_step_sums(r, p, a, b, h1, h2, Dinv)]
+    alphas, betas, diffs = [], [], []
+    gprev = 0.0
+    for j in range(1, sweeps + 1):
+        K = 2 * (j - 1)
+        g1, b1, a1, d1, g2, b2, a2, d2, _, _ = two_step_scalars(sums[-1], gprev, K, hh, prob.norm == "weighted")
+        z = Dinv * r
+        p1 = z + b1 * p
+        r1 = r - a1 * A(p1)
+        z1 = Dinv * r1
+        p2 = z1 + b2 * p1
+        r = r1 - a2 * A(p2)
+        w = w + a1 * p1 + a2 * p2
+        p = p2
+        gprev = g2
+        sums.append(two_step_sums(r, p, a, b, h1, h2, Dinv))
+        alphas.append((a1, a2))
+        betas.append((b1, b2))
+        diffs.append((d1, d2))
+    return TwoStepState(sweeps, sums, alphas, betas, diffs, r, p, w)
+
+
 def error_vs_analytic(prob: EllipseProblem, w: torch.Tensor):
     """(L2 error in D, h-weighted; max error in D) against u = F(1-cx x²-cy y²)/(2cx+2cy)."""
     x, y = _grid(prob, w.device)
