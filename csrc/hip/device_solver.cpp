@@ -78,10 +78,33 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // nodes (algo 3, or auto: PE_TWO=0/1 overrides).  Its 4-deep halo and
   // 20-sum reduction are not wired to the multi-rank transports yet.
   {
-    const bool two_ok = fused_ && comm_->size() == 1 && blk_.nx >= 8 && blk_.ny >= 8;
+    // single-rank blocks of ≥ 8 × 8 nodes, or row slabs (Py = 1) of ≥ 8 rows
+    // per rank over a multi-rank transport (every input global: every rank
+    // decides the same)
+    const bool single = comm_->size() == 1 && blk_.Px * blk_.Py == 1 && blk_.nx >= 8 && blk_.ny >= 8;
+    const bool slabs = comm_->size() > 1 && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= 8 && prob_.N - 1 >= 8;
+    const bool two_ok = fused_ && (single || slabs);
     if (opt_.algo == 3 && !two_ok)
-      throw std::invalid_argument("two-step sweep: single-rank blocks of at least 8 x 8 nodes only");
-    bool auto_two = false;
+      throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
+    // auto: every single-rank block the LDS-resident kernel cannot hold
+    // (1x MI355X, fresh processes, T_solver two-step vs single sweep:
+    // 1600×2400 0.110 vs 0.127 s, 2048² 0.113 vs 0.133, 4096² 0.378 vs 0.584,
+    // 8192² 2.60 vs 3.24, 16384² 13.7 vs 21.7; the resident kernel keeps
+    // ≤ 800×1200: 0.044 vs 0.059 s — profiles/r3_grids_two.txt).  The
+    // estimate mirrors setup_resident's geometry test.
+    bool resident_likely = false;
+    {
+      const char* r = std::getenv("PE_RESIDENT");
+      int ncu = 256, dv = 0;
+      if (hipGetDevice(&dv) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dv);
+      const int64_t ns = (blk_.ny + dev::kFSW - 1) / dev::kFSW;
+      if (!(r && std::atoi(r) == 0) && opt_.variant == 0 && ns <= ncu) {
+        const int64_t ntr = std::max<int64_t>(1, std::min<int64_t>(ncu / ns, blk_.nx / 8));
+        resident_likely = blk_.nx >= 2 * ntr && (blk_.nx + ntr - 1) / ntr <= dev::kResMaxRows &&
+                          ntr * ns <= dev::kResMaxTiles;
+      }
+    }
+    bool auto_two = slabs || !resident_likely;
     if (const char* e = std::getenv("PE_TWO")) auto_two = std::atoi(e) != 0;
     two_ = two_ok && (opt_.algo == 3 || (opt_.algo == 0 && auto_two));
   }
@@ -157,6 +180,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 
   k.fused = fused_ ? 1 : 0;
   k.steps = two_ ? 2 : 1;
+  k.hdep = hdep_;
   k.nx = nx;
   k.ny = ny;
   k.M = prob_.M;
@@ -413,7 +437,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // The halo push goes live with the in-sweep sum (its flags are the push's
   // delivery signal); the local sweeps above ran without either.
   if (push_) {
-    const int64_t side = 2 * k.pitch;
+    const int64_t side = int64_t(hdep_) * k.pitch;
     double* lo = static_cast<double*>(hpeers_[size_t(blk_.nbr[LEFT] >= 0 ? blk_.nbr[LEFT] : blk_.rank)]);
     double* hi = static_cast<double*>(hpeers_[size_t(blk_.nbr[RIGHT] >= 0 ? blk_.nbr[RIGHT] : blk_.rank)]);
     for (int b = 0; b < 2; ++b) {
@@ -467,10 +491,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 void DeviceSolver::setup_halo_push() {
   push_ = false;
   if (!fused_ || comm_->size() < 2 || !comm_->peer_sum() || blk_.Py != 1) return;
-  if ((prob_.M - 1) / blk_.Px < 4) return;  // edge rows 1, 2 and nx-1, nx distinct
+  if ((prob_.M - 1) / blk_.Px < 2 * hdep_) return;  // edge rows 1..h and nx-h+1..nx distinct
   if (const char* e = std::getenv("PE_XR"); e && std::atoi(e) == 0) return;
   if (const char* e = std::getenv("PE_HALO"); e && std::string(e) == "exchange") return;
-  const size_t bytes = sizeof(double) * 8 * size_t(kp_->pitch);  // [parity][side][2 rows]
+  const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);  // [parity][side][hdep rows]
   void* buf = nullptr;
   if (hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
     buf = nullptr;
@@ -496,7 +520,7 @@ void DeviceSolver::setup_halo_push() {
   // sweep can push.
   {
     KParams t = *kp_;
-    const int64_t side = 2 * t.pitch;
+    const int64_t side = int64_t(hdep_) * t.pitch;
     for (int b = 0; b < 2; ++b) {
       t.hpush_lo[b] = blk_.has(LEFT) ? static_cast<double*>(hpeers_[size_t(blk_.nbr[LEFT])]) + (2 * b + 1) * side
                                      : nullptr;
@@ -722,14 +746,17 @@ std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
   if (blk_.has(DOWN)) ph[0].ex.push_back(Exchange{DOWN, blk_.nbr[DOWN], k.send_dn, const_cast<double*>(k.recv_dn), c});
   if (blk_.has(UP)) ph[0].ex.push_back(Exchange{UP, blk_.nbr[UP], k.send_up, const_cast<double*>(k.recv_up), c});
   ph[0].unpack = blk_.has(DOWN) || blk_.has(UP);
-  // Phase 1: two full interleaved (r, p) rows per side, halo columns included
-  // (so the corners arrive from the diagonal rank through the x neighbour).
+  // Phase 1: hdep full interleaved (r, p) rows per side, halo columns
+  // included (so the corners arrive from the diagonal rank through the x
+  // neighbour): rows 1..h → the LEFT neighbour's rows nx'+1..nx'+h, rows
+  // nx-h+1..nx → the RIGHT neighbour's rows 1-h..0.
   double* x = k.x[buf];
-  const int64_t n = 2 * k.pitch;
-  if (blk_.has(LEFT)) ph[1].ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], x + 1 * k.pitch - 1, x - 1 * k.pitch - 1, n});
+  const int64_t h = hdep_, n = h * k.pitch;
+  if (blk_.has(LEFT))
+    ph[1].ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], x + 1 * k.pitch - (h - 1), x + (1 - h) * k.pitch - (h - 1), n});
   if (blk_.has(RIGHT))
-    ph[1].ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], x + (blk_.nx - 1) * k.pitch - 1,
-                                x + (blk_.nx + 1) * k.pitch - 1, n});
+    ph[1].ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], x + (blk_.nx - h + 1) * k.pitch - (h - 1),
+                                x + (blk_.nx + 1) * k.pitch - (h - 1), n});
   return ph;
 }
 
@@ -784,7 +811,9 @@ void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 // Cross-rank sum of sweep `par`'s 7 sums: nothing to enqueue when the sweep
 // sums them over ranks itself (k.xr, P2P transport).
 void DeviceSolver::enqueue_fs_reduce(int par) {
-  if (!kp_->xr.peers) comm_->allreduce_sum(st_->fs[par], 7, stream_);
+  if (kp_->xr.peers) return;
+  if (two_) comm_->allreduce_sum(st_->fs2[par], dev::kNS2, stream_);
+  else comm_->allreduce_sum(st_->fs[par], 7, stream_);
 }
 
 // Sampled phase timing: event pairs from a pool; a record's events are read

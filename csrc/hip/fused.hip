@@ -1177,12 +1177,13 @@ __global__ void kUnpack(KParams k, int b) {
 // last reduction waited for; the loads are system-scope (the buffer is
 // written over xGMI, never through this GPU's caches).
 __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
-  const int64_t n = 2 * k.pitch;
-  double* x = k.x[b] - 1;  // row 0, column -1
+  const int h = k.hdep;
+  const int64_t n = int64_t(h) * k.pitch;
+  double* x = k.x[b] - (h - 1);  // row 0, column -(h-1)
   for (int side = 0; side < 2; ++side) {
     if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
     const double* src = k.hrecv + (int64_t(b) * 2 + side) * n;
-    double* dst = x + (side == 0 ? int64_t(-1) : k.nx + 1) * k.pitch;
+    double* dst = x + (side == 0 ? int64_t(1 - h) : k.nx + 1) * k.pitch;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
       dst[i] = __hip_atomic_load(src + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1193,12 +1194,13 @@ __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
 // the next sweep's halo reads find them there.  System-scope stores, as the
 // pushes': the sweep's loads bypass this GPU's caches.
 __global__ __launch_bounds__(256) void kHaloSeed(KParams k, int b) {
-  const int64_t n = 2 * k.pitch;
-  const double* x = k.x[b] - 1;  // row 0, column -1
+  const int h = k.hdep;
+  const int64_t n = int64_t(h) * k.pitch;
+  const double* x = k.x[b] - (h - 1);  // row 0, column -(h-1)
   for (int side = 0; side < 2; ++side) {
     if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
     double* dst = const_cast<double*>(k.hrecv) + (int64_t(b) * 2 + side) * n;  // this rank's own buffer
-    const double* src = x + (side == 0 ? int64_t(-1) : k.nx + 1) * k.pitch;
+    const double* src = x + (side == 0 ? int64_t(1 - h) : k.nx + 1) * k.pitch;
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x)
       __hip_atomic_store(dst + i, src[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
   }
@@ -1213,7 +1215,7 @@ __device__ __forceinline__ double push_code(int rank, int side, int b, int64_t i
   return double((rank * 2 + side) * 2 + b) * 1e7 + double(i);
 }
 __global__ __launch_bounds__(256) void kPushTestWrite(KParams k, int me) {
-  const int64_t n = 2 * k.pitch;
+  const int64_t n = int64_t(k.hdep) * k.pitch;
   for (int b = 0; b < 2; ++b)
     for (int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x; i < n; i += int64_t(gridDim.x) * blockDim.x) {
       if (k.hpush_lo[b]) __hip_atomic_store(k.hpush_lo[b] + i, push_code(me, 1, b, i), __ATOMIC_RELAXED,
@@ -1224,7 +1226,7 @@ __global__ __launch_bounds__(256) void kPushTestWrite(KParams k, int me) {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
 }
 __global__ __launch_bounds__(256) void kPushTestCheck(KParams k, int left, int right, int* bad) {
-  const int64_t n = 2 * k.pitch;
+  const int64_t n = int64_t(k.hdep) * k.pitch;
   int nbad = 0;
   for (int b = 0; b < 2; ++b)
     for (int side = 0; side < 2; ++side) {
@@ -1365,14 +1367,14 @@ void launch_push_test_check(const KParams& k, int left, int right, int* bad, hip
 
 void launch_halo_import(const KParams& k, int b, hipStream_t s) {
   if (!k.push || (!k.has[LEFT] && !k.has[RIGHT])) return;
-  const int64_t n = 2 * k.pitch;
+  const int64_t n = int64_t(k.hdep) * k.pitch;
   const unsigned g = unsigned(std::min<int64_t>(64, (n + 255) / 256));
   hipLaunchKernelGGL(kHaloImport, dim3(g), dim3(256), 0, s, k, b);
 }
 
 void launch_halo_seed(const KParams& k, int b, hipStream_t s) {
   if (!k.push || (!k.has[LEFT] && !k.has[RIGHT])) return;
-  const int64_t n = 2 * k.pitch;
+  const int64_t n = int64_t(k.hdep) * k.pitch;
   const unsigned g = unsigned(std::min<int64_t>(64, (n + 255) / 256));
   hipLaunchKernelGGL(kHaloSeed, dim3(g), dim3(256), 0, s, k, b);
 }

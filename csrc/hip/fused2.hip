@@ -341,13 +341,19 @@ __device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx
 }
 
 // The item march (one strip × rows ib..ie), accumulating this wave's sums.
+// PUSH (row slabs over the P2P transport, KParams::push): output rows 1..4 /
+// nx-3..nx are also stored into the x-neighbours' fine-grained receive
+// buffers over xGMI (system-scope write-through stores, drained and released
+// at the end of the item: delivered before this rank's cross-rank-sum flags),
+// and the halo rows -3..0 / nx+1..nx+4 are read from this rank's receive
+// buffer (system-scope loads) — fused.hip's halo push at depth 4.
 // Sums are taken over the item's rows (uniform row tests) without per-term
 // column masks: every sum has a factor among z, p, u, v, which are exactly 0
 // at the global-boundary and padding columns (z, u, v masked there; p stays 0),
 // and the lanes that do not own their columns (0, 1, 62, 63: the recomputed
 // halo of the strip) are dropped once, at the end of the sweep.  (Blocks
 // split across y — halo columns with real data — are not run by this kernel.)
-template <bool BAND>
+template <bool BAND, bool PUSH>
 __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par, int s, int ib, int ie,
                                       WaveTV2& tvw, double (&acc)[NS]) {
   const int lane = threadIdx.x & 63;
@@ -410,7 +416,37 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
     const int64_t gr = k.gi0 + q;
     return gr >= 1 && gr <= k.M - 1;
   };
-  auto ldx = [&](int t, unsigned o) -> double2 { return ld2(Xm + int64_t(t) * pitch + o); };
+  const int nx = int(k.nx);
+  // receive buffer of the parity this sweep reads: [side][4 rows], rows from column -3
+  const double* hrd = PUSH ? k.hrecv + int64_t(par ^ 1) * 8 * pitch : nullptr;
+  auto ldx = [&](int t, unsigned o) -> double2 {
+    if constexpr (PUSH) {
+      if ((t < 1 && k.has[LEFT]) || (t > nx && k.has[RIGHT])) {
+        const double* h = hrd + int64_t(t < 1 ? t + 3 : t - nx + 3) * pitch + o;
+        return dd(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                  __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      }
+    }
+    return ld2(Xm + int64_t(t) * pitch + o);
+  };
+  bool pushed = false;
+  auto push_row = [&](int q, const double2& r2, const double2& p2) {
+    auto put = [&](double* base, int slot) {
+      double* d = base + int64_t(slot) * pitch + off;
+      if (o0) {
+        __hip_atomic_store(d, r2.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(d + poff, p2.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      if (o1) {
+        __hip_atomic_store(d + 1, r2.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(d + 1 + poff, p2.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      pushed = true;
+    };
+    // rows 1..4 → the LEFT neighbour's rows nx'+1..nx'+4; nx-3..nx → the RIGHT one's -3..0
+    if (q <= 4 && k.hpush_lo[par] != nullptr) put(k.hpush_lo[par], q - 1);
+    if (q >= nx - 3 && k.hpush_hi[par] != nullptr) put(k.hpush_hi[par], q - (nx - 3));
+  };
 
   // prefetch ring (3 rows): x rows t, t+1, t+2; w rows t-2, t-1, t
   const int tmax = ie + 4;
@@ -498,6 +534,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
             yr[poff] = p2.x;
             wd[0] = wv.x;
           }
+          if constexpr (PUSH) push_row(q, r2, p2);
           sv[0] += r2.x * z2.x + r2.y * z2.y;            // (r,z)
           sv[2] += z2.x * s2v.x + z2.y * s2v.y;          // (z,s)
           sv[3] += p2.x * s2v.x + p2.y * s2v.y;          // (p,s)
@@ -547,8 +584,16 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
       }
     }
   }
+  if constexpr (PUSH) {
+    if (pushed) {  // delivered before this wave arrives anywhere
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  }
 }
 
+template <bool PUSH>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS2(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
@@ -584,8 +629,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     if (rows == 0) continue;  // empty position of the static layout
     const int s = e.y & 0xFFFFF, ib = e.x & kRowMask;
     const int ie = min(ib + rows - 1, int(k.nx));
-    if (e.x & kBandBit) march<true>(k, sc, par, s, ib, ie, tvs[wid], acc);
-    else march<false>(k, sc, par, s, ib, ie, tvs[wid], acc);
+    if (e.x & kBandBit) march<true, PUSH>(k, sc, par, s, ib, ie, tvs[wid], acc);
+    else march<false, PUSH>(k, sc, par, s, ib, ie, tvs[wid], acc);
   }
   if (lane < 2 || lane > 61)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
 #pragma unroll
@@ -598,9 +643,14 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     __shared__ unsigned long long sseq;
     __shared__ int sok;
     if (k.xr.peers) {  // cross-rank sum of the 20 sums inside the sweep (P2P transport)
-      if (threadIdx.x == 0)
+      if (threadIdx.x == 0) {
 #pragma unroll
         for (int n = 0; n < NS; ++n) xv[n] = t[n];
+        if (k.slow_ticks > 0) {  // PE_FAULT_INJECT=slow@rank (test hook): idle before the cross-rank sum
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < k.slow_ticks) __builtin_amdgcn_s_sleep(2);
+        }
+      }
       peer_sum_block(k.xr, xv, NS, &sseq, &sok);
       if (threadIdx.x == 0)
 #pragma unroll
@@ -616,12 +666,13 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
 }  // namespace
 
 void launch_S2(const KParams& k, int par, hipStream_t s) {
-  hipLaunchKernelGGL(kS2, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+  if (k.push) hipLaunchKernelGGL(kS2<true>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+  else hipLaunchKernelGGL(kS2<false>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
 }
 
 int resident_blocks_S2() {
   int n = 0;
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kS2, TJ, 0) != hipSuccess) {
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, kS2<false>, TJ, 0) != hipSuccess) {
     (void)hipGetLastError();
     n = 0;
   }

@@ -77,7 +77,7 @@ void DeviceSolver::setup_items() {
   // PE_OVERLAP=1 / 0 forces it on / off.
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = false;
-  if (fused_ && comm_->size() > 1 && nb && !push_) {
+  if (fused_ && !two_ && comm_->size() > 1 && nb && !push_) {  // (the two-step sweep runs without the overlap)
     if (e) {
       overlap_ = std::atoi(e) != 0;
     } else {

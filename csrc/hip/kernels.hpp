@@ -174,6 +174,7 @@ struct KParams {
   // iterations per sweep: 1 single sweep (fused.hip kS), 2 two-step sweep
   // (fused2.hip kS2: 4-deep halo, 120-column strips, 20 sums)
   int steps;
+  int hdep;  // halo depth of the single-sweep layouts: 2 (kS), 4 (kS2); rows per side of a push message
 };
 constexpr int kFoldGroup = 64;
 
