@@ -310,9 +310,15 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // 8-rank 8192² block 10 rows — profiles/r2_mid_tune.txt).
   static constexpr int kTiCands[4] = {8, 10, 14, 18};
   tune_ti_ = fused_ && ti_env == 0 && k.order == 0 && npts >= double(1 << 20) && !big;
-  if (two_) tune_ti_ = false;  // (rows per item of the two-step sweep: fixed until measured)
+  // Two-step sweep: tuned among {16, 24, 32, 40, 48} below 2²⁵ nodes (the
+  // best height moves with the block: 1600×2400 16 rows 39.9 µs/iter vs 47.7
+  // at 40, 2048² 24 rows, 4096² 32 rows 102.3 vs 108.7; 8192² and 16384²
+  // within ±2 % over 24-48 rows: fixed 40 — one placement per grid,
+  // tools/ti_probe.py, profiles/r3_ti_probe.txt).
+  static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
+  if (two_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
-  const int ti_min = tune_ti_ ? kTiCands[0] : ti;
+  const int ti_min = tune_ti_ ? (two_ ? kTiCands2[0] : kTiCands[0]) : ti;
   set_items(ti);
   // block partials: interior grid, then (overlap) the boundary grid after it
   const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(wave_cap, wave_cap0) / dev::kWPB + 1), 4096);
@@ -359,13 +365,15 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // wave means a quarter of the waves runs a 4th item while the rest idle
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
     std::vector<int> cands(kTiCands, kTiCands + 4);
+    if (two_) cands.assign(kTiCands2, kTiCands2 + 5);
     // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
     // at 18, one placement, profiles/r2_ti_big.txt)
-    if (npts >= 12e6) cands.insert(cands.end(), {24, 30});
+    if (npts >= 12e6 && !two_) cands.insert(cands.end(), {24, 30});
     {
       const int64_t W = std::max(dev::kWPB, wave_cap_);
+      const int tlo = two_ ? kTiCands2[0] : kTiCands[0], thi = two_ ? dev::kTImax2 : 40;
       for (int q = 2; q <= 5; ++q)
-        for (int t = kTiCands[0]; t <= 40; ++t)
+        for (int t = tlo; t <= thi; ++t)
           if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
             cands.push_back(t);
             break;

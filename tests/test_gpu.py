@@ -164,10 +164,10 @@ def test_item_sum_fold_matches_reduction_kernel(gpu, M, N, monkeypatch):
     monkeypatch.setenv("PE_RESIDENT", "0")
     monkeypatch.setenv("PE_FOLD", "1")
     prob = EllipseProblem(M, N)
-    a = solve(prob, backend="hip", return_w=True)
-    b = solve(prob, backend="hip", return_w=True)
+    a = solve(prob, backend="hip", return_w=True, algo="fused")
+    b = solve(prob, backend="hip", return_w=True, algo="fused")
     monkeypatch.setenv("PE_FOLD", "0")
-    c = solve(prob, backend="hip", return_w=True)
+    c = solve(prob, backend="hip", return_w=True, algo="fused")
     assert a.iters == b.iters and abs(a.iters - c.iters) <= 1
     assert a.iters == {(800, 1200): 989, (2048, 2048): 1730}[(M, N)]
     assert np.array_equal(a.w, b.w)
@@ -213,9 +213,9 @@ def test_random_init_matches_cpu(gpu):
 def test_bitwise_deterministic_and_graph_equivalent(gpu, monkeypatch):
     monkeypatch.setenv("PE_RESIDENT", "0")  # the streaming sweep (500×700 would run resident)
     prob = EllipseProblem(500, 700)
-    a = solve(prob, backend="hip", return_w=True)  # eager launches (default)
-    b = solve(prob, backend="hip", return_w=True)
-    c = solve(prob, backend="hip", return_w=True, graph=True)  # chunks replayed from hipGraphs
+    a = solve(prob, backend="hip", return_w=True, algo="fused")  # eager launches (default)
+    b = solve(prob, backend="hip", return_w=True, algo="fused")
+    c = solve(prob, backend="hip", return_w=True, graph=True, algo="fused")  # chunks replayed from hipGraphs
     assert a.iters == b.iters == c.iters
     assert np.array_equal(a.w, b.w) and np.array_equal(a.w, c.w)
 
@@ -609,7 +609,7 @@ def test_resident_matches_streaming(gpu, M, N, monkeypatch):
     (different summation order only), golden counts on the published grids."""
     prob = EllipseProblem(M, N)
     monkeypatch.setenv("PE_RESIDENT", "0")
-    ref = solve(prob, backend="hip", return_w=True)
+    ref = solve(prob, backend="hip", return_w=True, algo="fused")
     monkeypatch.delenv("PE_RESIDENT")
     res = solve(prob, backend="hip", return_w=True)
     assert res.algo == "resident" and ref.algo == "fused"
@@ -644,7 +644,7 @@ def test_resident_terminal_at_launch_start(gpu, M, N, chunk, max_iter, monkeypat
     if max_iter:
         prob.max_iter = max_iter
     monkeypatch.setenv("PE_RESIDENT", "0")
-    ref = solve(prob, backend="hip", return_w=True, chunk=chunk)
+    ref = solve(prob, backend="hip", return_w=True, chunk=chunk, algo="fused")
     monkeypatch.delenv("PE_RESIDENT")
     res = solve(prob, backend="hip", return_w=True, chunk=chunk)
     assert res.algo == "resident" and ref.algo == "fused"
@@ -687,6 +687,7 @@ def test_resident_state_matches_streaming_kernel(gpu, nat, monkeypatch):
         monkeypatch.setenv("PE_RESIDENT", flag)
         opt = nat.SolveOptions()
         opt.check_tol = False
+        opt.algo = 2 if flag == "0" else 0
         s = nat.DeviceSolver(prob.to_native(), blk, None, opt)
         assert s.resident == (flag == "1")
         s.reset()
