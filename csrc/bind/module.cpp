@@ -432,6 +432,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("two_step", &DeviceSolver::two_step, "two iterations per sweep (fused2.hip)")
+      .def_property_readonly("segment_layout", &DeviceSolver::segment_layout)
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("overlap", &DeviceSolver::overlap)

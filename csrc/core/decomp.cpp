@@ -53,12 +53,15 @@ ProcessGrid process_grid_from_spec(const std::string& spec, int P, int M, int N)
   if (spec == "aspect") return choose_process_grid(P, M, N, DecompMode::Aspect);
   if (spec == "rows") return choose_process_grid(P, M, N, DecompMode::Rows);
   if (spec == "cols") return choose_process_grid(P, M, N, DecompMode::Cols);
-  // "device": the single-sweep GPU solver's preference — P×1 row slabs while
-  // every rank keeps >= 512 rows (one contiguous two-row exchange per side,
-  // no strided strips, and the wider rows sweep faster: 8 ranks on 8192²
-  // measured 116 vs 129 µs per rank block for 4×2), else the aspect rule.
+  // "device": the GPU solver's preference — P×1 row slabs while every rank
+  // keeps >= 32 rows, else the aspect rule.  Slabs run the two-step sweep (two
+  // iterations per pass, 4-row halo pushed by the sweep itself over xGMI, one
+  // contiguous message per side, no strided strips); 2D blocks run the single
+  // sweep.  Per rank block, zero-latency transport (profiles/r3_block_probe.txt):
+  // 4096² on 8 ranks 28.3 µs/iter as 8×1 vs 39.8 as 4×2, on 4 ranks 41.2 vs
+  // 59.7 (4×1 / 2×2); 2048² on 8: 23.4 vs 31.9; 16384² on 8: 168 vs 279.
   if (spec == "device") {
-    if ((int64_t(M) - 1) / P >= 512) return choose_process_grid(P, M, N, DecompMode::Rows);
+    if ((int64_t(M) - 1) / P >= 32) return choose_process_grid(P, M, N, DecompMode::Rows);
     return choose_process_grid(P, M, N, DecompMode::Aspect);
   }
   const auto x = spec.find('x');

@@ -365,7 +365,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // wave means a quarter of the waves runs a 4th item while the rest idle
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
     std::vector<int> cands(kTiCands, kTiCands + 4);
-    if (two_) cands.assign(kTiCands2, kTiCands2 + 5);
+    if (two_) cands.assign(kTiCands2, kTiCands2 + 5);  // (+ 0: the segment layout, added below)
     // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
     // at 18, one placement, profiles/r2_ti_big.txt)
     if (npts >= 12e6 && !two_) cands.insert(cands.end(), {24, 30});
@@ -380,11 +380,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
           }
       std::sort(cands.begin(), cands.end());
       cands.erase(std::unique(cands.begin(), cands.end()), cands.end());
+      // (two-step sweep, PE_TI_SEGMENTS=1: also one tall segment per wave — its
+      // 8 pipeline-fill rows re-read once per segment; it lost to the LPT items
+      // on the 2/4/8-rank 8192² slabs, 128 vs 110 µs per sweep at 8 ranks:
+      // profiles/r3_block_probe.txt)
+      if (two_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
     }
     float best_ms = 0.f;
     int best = ti;
     for (int cand : cands) {
-      set_items(cand);
+      seg_layout_ = cand == 0;
+      set_items(cand == 0 ? ti : cand);
       setup_items();
       enqueue_init();
       dev::launch_S(*kp_, 1, stream_);
@@ -402,7 +408,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
         best = cand;
       }
     }
-    set_items(best);
+    seg_layout_ = best == 0;
+    set_items(best == 0 ? ti : best);
     setup_items();
   }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {

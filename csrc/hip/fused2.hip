@@ -374,44 +374,48 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
   const bool o1 = inner && c0 + 1 >= 1 && c0 + 1 <= ny;
   const double a1 = sc.a1, b1 = sc.b1, a2 = sc.a2, b2 = sc.b2, zc = sc.zc;
 
-  // Row classes / column tables of rows t0 .. t0+63 (one per lane; items
-  // have ≤ kTImax2 rows, so rows ib-4 .. ie+5 fit).
   const int t0 = ib - 4;
+  // Row classes / column tables of rows segbase .. segbase+63 (one per lane),
+  // reloaded every ~54 rows on tall items (stage rows t-4 .. t and the
+  // column-table row t+1 stay inside the window).
   RowCtx rx;
-  rx.segbase = t0;
-  {
-    const int nr = ie + 6 - t0;
-    const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (t0 + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+  auto load_seg = [&](int base) {
+    rx.segbase = base;
+    const int nr = ie + 6 - base;
+    const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
     rx.rcv = make_int2(rc4.x, rc4.y);
     rx.genmask = 0;
     if (BAND) {
       rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
       if (rx.genmask != 0) {
-        const double* ctr = k.colT + (min(t0 + lane, ie + 5) + 1) * 4;
+        const double* ctr = k.colT + (min(base + lane, ie + 5) + 1) * 4;
         tvw.rc[lane] = rc4;
         tvw.half[lane] = ctr[0];
         tvw.sB[lane] = ctr[1];
         tvw.eB[lane] = ctr[2];
         if (lane == 63) tvw.half[64] = ctr[4];
-        const double* tb = k.rowT + (c0 + 1) * 4;
-        const double4 a = *reinterpret_cast<const double4*>(tb);
-        const double4 b = *reinterpret_cast<const double4*>(tb + 4);
-        tvw.sA[jl] = a.x;
-        tvw.eA[jl] = a.y;
-        tvw.hB[jl] = a.z;
-        tvw.sA[jl + 1] = b.x;
-        tvw.eA[jl + 1] = b.y;
-        tvw.hB[jl + 1] = b.z;
-        if (lane == 63) {
-          tvw.hB[128] = tb[10];
-          tvw.hB[129] = tb[14];
-        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       }
     }
+  };
+  if (BAND) {  // the strip's row-table entries (per column), once per band item
+    const double* tb = k.rowT + (c0 + 1) * 4;
+    const double4 a = *reinterpret_cast<const double4*>(tb);
+    const double4 b = *reinterpret_cast<const double4*>(tb + 4);
+    tvw.sA[jl] = a.x;
+    tvw.eA[jl] = a.y;
+    tvw.hB[jl] = a.z;
+    tvw.sA[jl + 1] = b.x;
+    tvw.eA[jl + 1] = b.y;
+    tvw.hB[jl + 1] = b.z;
+    if (lane == 63) {
+      tvw.hB[128] = tb[10];
+      tvw.hB[129] = tb[14];
+    }
   }
+  load_seg(t0);
   auto interior = [&](int q) {  // global interior row
     const int64_t gr = k.gi0 + q;
     return gr >= 1 && gr <= k.M - 1;
@@ -470,6 +474,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
 
   const int nsteps = ie + 4 - t0 + 1;
   for (int g = 0; 6 * g < nsteps; ++g) {
+    if (t0 + 6 * g + 6 - rx.segbase > 63) load_seg(t0 + 6 * g - 4);  // tall items: next row window
 #pragma unroll
     for (int jj = 0; jj < 6; ++jj) {
       const int n = 6 * g + jj;

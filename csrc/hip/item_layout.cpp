@@ -207,8 +207,10 @@ void DeviceSolver::setup_items() {
           pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
         }
       }
-    // PE_SEGMENTS=1 (experiment): the segment layout below
-    if (const char* sg = std::getenv("PE_SEGMENTS"); sg && std::atoi(sg) == 1 && !two_) {
+    // Segment layout (PE_SEGMENTS=1, or chosen by the two-step sweep's
+    // rows-per-item tuner, seg_layout_): one tall item per wave
+    const char* sg = std::getenv("PE_SEGMENTS");
+    if (seg_layout_ || (sg && std::atoi(sg) == 1)) {
       // Segment layout: one tall item per wave.  Each strip's rows are cut
       // into segments of equal estimated cost, and the strips' segment
       // counts are dealt (largest remaining segment cost first) so that the

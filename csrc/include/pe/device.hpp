@@ -165,6 +165,7 @@ class DeviceSolver {
   bool fused() const { return fused_; }
   // two iterations per sweep (fused2.hip)
   bool two_step() const { return two_; }
+  bool segment_layout() const { return seg_layout_; }  // static layout of one tall segment per wave
   // LDS-resident single sweep (resident.hip): small single-rank blocks run
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
   bool resident() const { return resident_; }
@@ -264,6 +265,7 @@ class DeviceSolver {
   int fsw_ = 124;         // output columns per strip (kFSW / kFSW2)
   int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4)
   int64_t tab_lo_ = -1;   // first local index of the chord tables / row classes
+  bool seg_layout_ = false;  // static layout of tall equal-cost segments, one per wave (setup_items)
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w
   double* xalt_ = nullptr;    // single-sweep: x1 (separate allocation)
   double* walt_ = nullptr;    // single-sweep: w

@@ -76,7 +76,7 @@ def test_neighbour_symmetry(P):
 
 @pytest.mark.parametrize("spec,P,expect", [("rows", 8, (8, 1)), ("cols", 4, (1, 4)), ("4x2", 8, (4, 2)),
                                            ("1x1", 1, (1, 1)), ("reference", 8, (2, 4)), ("aspect", 8, (4, 2)),
-                                           ("device", 8, (8, 1)), ("device", 32, (8, 4))])
+                                           ("device", 8, (8, 1)), ("device", 32, (32, 1)), ("device", 512, (32, 16))])
 def test_grid_specs(spec, P, expect):
     assert D.process_grid(P, 8192, 8192, spec) == expect
 
@@ -100,10 +100,12 @@ def test_thread_ranks_explicit_grid_matches_serial(spec):
 
 
 def test_device_spec_falls_back_to_aspect_for_thin_slabs():
-    # 8192² on 8 ranks keeps 1023 rows per slab → rows; 16 ranks on 4096² would
-    # leave 255 rows → the aspect rule
+    # row slabs (the two-step sweep's halo push) while every rank keeps >= 32
+    # rows: 8192² on 8 ranks → 8×1, 4096² on 16 → 16×1; 128 ranks on 2048²
+    # would leave 15 rows → the aspect rule
     assert D.process_grid(8, 8192, 8192, "device") == (8, 1)
-    assert D.process_grid(16, 4096, 4096, "device") == D.process_grid(16, 4096, 4096, "aspect")
+    assert D.process_grid(16, 4096, 4096, "device") == (16, 1)
+    assert D.process_grid(128, 2048, 2048, "device") == D.process_grid(128, 2048, 2048, "aspect")
     assert D.default_spec("hip") == "device" and D.default_spec("ranks") == "aspect"
 
 

@@ -66,3 +66,37 @@ def test_operator_symmetric_positive():
     rhs = torch_ref.dot(u, Av, prob.h1, prob.h2)
     assert lhs == pytest.approx(rhs, rel=1e-10)
     assert torch_ref.dot(Au, u, prob.h1, prob.h2) > 0
+
+
+@pytest.mark.parametrize("M,N", [(40, 40), (60, 90), (31, 17)])
+def test_two_step_recurrence_is_pcg(M, N):
+    """The two-iterations-per-sweep recurrence of csrc/hip/fused2.hip
+    (torch_ref.two_step: scalars of iterations K+1, K+2 from 20 dot products
+    of the basis around r_K, p_K) against the reference PCG and the single-sweep
+    recurrence: same α, β, w to rounding, and the same stop iteration."""
+    prob = EllipseProblem(M, N)
+    J = 12
+    two = torch_ref.two_step(prob, J)
+    one = torch_ref.single_sweep(prob, 2 * J)
+    for j in range(J):
+        for s in range(2):
+            assert two.alpha[j][s] == pytest.approx(one.alpha[2 * j + s], rel=1e-10)
+            assert two.beta[j][s] == pytest.approx(one.beta[2 * j + s], rel=1e-9, abs=1e-14)
+    scale = float(one.w.abs().max())
+    assert float((two.w - one.w).abs().max()) <= 1e-12 * scale
+    # iteration count of the reference loop: the first k with ‖Δw‖ < δ
+    ref = torch_ref.pcg(prob)
+    diffs = [d for pair in two.diff for d in pair]
+    k = next((i + 1 for i, d in enumerate(diffs) if d < prob.tol), None)
+    if k is not None:
+        assert k == ref.iters
+
+
+def test_two_step_stop_test_matches_reference_history():
+    """‖Δw‖ of every iteration from the 20-sum quadratic forms equals the
+    reference loop's directly computed norm (rel 1e-7) up to convergence."""
+    prob = EllipseProblem(40, 40)
+    ref = torch_ref.pcg(prob, keep_history=True)
+    two = torch_ref.two_step(prob, (ref.iters + 1) // 2)
+    diffs = [d for pair in two.diff for d in pair][: ref.iters]
+    np.testing.assert_allclose(diffs, ref.history, rtol=1e-7)
