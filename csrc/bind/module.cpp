@@ -67,6 +67,10 @@ py::dict state_dict(const dev::DevState& s) {
     f2.append(py::tuple(v));
   }
   d["fs2"] = py::tuple(f2);
+  d["fixpend"] = s.fixpend;
+  py::list c3;
+  for (int n = 0; n < 12; ++n) c3.append(s.sc3[n]);
+  d["sc3"] = py::tuple(c3);
   d["wait_s"] = double(s.xr_wait) * 1e-8;
   return d;
 }
@@ -431,7 +435,8 @@ PYBIND11_MODULE(_native, m) {
            })
       .def_property_readonly("chunk", &DeviceSolver::chunk)
       .def_property_readonly("fused", &DeviceSolver::fused)
-      .def_property_readonly("two_step", &DeviceSolver::two_step, "two iterations per sweep (fused2.hip)")
+      .def_property_readonly("two_step", &DeviceSolver::two_step, "several iterations per sweep (fused2.hip / fused3.hip)")
+      .def_property_readonly("sweep_steps", &DeviceSolver::sweep_steps, "iterations per sweep launch (1, 2, 3)")
       .def_property_readonly("segment_layout", &DeviceSolver::segment_layout)
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)

@@ -62,7 +62,7 @@ void DeviceSolver::save_checkpoint(const std::string& path) {
   h.rank = blk_.rank;
   h.Px = blk_.Px;
   h.Py = blk_.Py;
-  h.fused = two_ ? 2 : fused_ ? 1 : 0;  // 2: two-step layout (4-deep halo)
+  h.fused = sstep_ ? steps_ : fused_ ? 1 : 0;  // 2 / 3: two- / three-step layout (4- / 6-deep halo)
   h.variant = opt_.variant;
   h.par = par_;
   h.i0 = blk_.i0;
@@ -99,7 +99,7 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
   ck_io(f, &h, sizeof(h), false, path);
   size_t field_bytes = fused_ ? sizeof(double) * (2 * xsize_ + wsize_) : sizeof(double) * 4 * blk_.alloc;
   const bool ok = std::memcmp(h.magic, "PECKPT1", 8) == 0 && h.version == 1 && h.M == prob_.M && h.N == prob_.N &&
-                  h.rank == blk_.rank && h.Px == blk_.Px && h.Py == blk_.Py && h.fused == (two_ ? 2 : fused_ ? 1 : 0) &&
+                  h.rank == blk_.rank && h.Px == blk_.Px && h.Py == blk_.Py && h.fused == (sstep_ ? steps_ : fused_ ? 1 : 0) &&
                   h.variant == opt_.variant && h.i0 == blk_.i0 && h.j0 == blk_.j0 && h.nx == blk_.nx &&
                   h.ny == blk_.ny && h.state_bytes == int64_t(sizeof(DevState)) &&
                   h.field_bytes == int64_t(field_bytes) && h.halo_bytes == int64_t(sizeof(double) * hsize_ * 4);

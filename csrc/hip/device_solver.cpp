@@ -71,21 +71,26 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     comm_ = self_.get();
   }
   const bool can_fuse = opt_.variant == 0 && fused_possible(prob_, blk_);
-  if ((opt_.algo == 2 || opt_.algo == 3) && !can_fuse)
+  if (opt_.algo >= 2 && !can_fuse)
     throw std::invalid_argument("single-sweep algorithm needs variant 0 and >= 2 rows/columns per split block");
-  fused_ = opt_.algo == 2 || opt_.algo == 3 || (opt_.algo == 0 && can_fuse);
-  // Two iterations per sweep (fused2.hip): single-rank blocks of ≥ 8 × 8
-  // nodes (algo 3, or auto: PE_TWO=0/1 overrides).  Its 4-deep halo and
-  // 20-sum reduction are not wired to the multi-rank transports yet.
+  fused_ = opt_.algo >= 2 || (opt_.algo == 0 && can_fuse);
+  // Several iterations per sweep (fused2.hip: 2, fused3.hip: 3): single-rank
+  // blocks of ≥ 8 × 8 nodes, or row slabs (Py = 1) over a multi-rank
+  // transport of ≥ 4s rows per rank (the 2s-deep halo comes from one
+  // neighbour and the pushed edge rows are distinct).  Every input is global: every rank
+  // decides the same.  algo 3 / 4 force two / three steps; auto takes three
+  // where it can (PE_STEPS=1/2/3 overrides; PE_TWO=0 keeps one).
   {
-    // single-rank blocks of ≥ 8 × 8 nodes, or row slabs (Py = 1) of ≥ 8 rows
-    // per rank over a multi-rank transport (every input global: every rank
-    // decides the same)
-    const bool single = comm_->size() == 1 && blk_.Px * blk_.Py == 1 && blk_.nx >= 8 && blk_.ny >= 8;
-    const bool slabs = comm_->size() > 1 && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= 8 && prob_.N - 1 >= 8;
-    const bool two_ok = fused_ && (single || slabs);
+    auto single = [&](int64_t m) { return comm_->size() == 1 && blk_.Px * blk_.Py == 1 && blk_.nx >= m && blk_.ny >= m; };
+    auto slabs = [&](int64_t m) {
+      return comm_->size() > 1 && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= m && prob_.N - 1 >= m;
+    };
+    const bool two_ok = fused_ && (single(8) || slabs(8));
+    const bool three_ok = fused_ && (single(8) || slabs(12));
     if (opt_.algo == 3 && !two_ok)
       throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
+    if (opt_.algo == 4 && !three_ok)
+      throw std::invalid_argument("three-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 12 rows");
     // auto: every single-rank block the LDS-resident kernel cannot hold
     // (1x MI355X, fresh processes, T_solver two-step vs single sweep:
     // 1600×2400 0.110 vs 0.127 s, 2048² 0.113 vs 0.133, 4096² 0.378 vs 0.584,
@@ -104,9 +109,15 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
                           ntr * ns <= dev::kResMaxTiles;
       }
     }
-    bool auto_two = slabs || !resident_likely;
-    if (const char* e = std::getenv("PE_TWO")) auto_two = std::atoi(e) != 0;
-    two_ = two_ok && (opt_.algo == 3 || (opt_.algo == 0 && auto_two));
+    bool auto_ms = slabs(8) || !resident_likely;
+    if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
+    int want = 3;
+    if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
+    steps_ = 1;
+    if (opt_.algo == 3) steps_ = 2;
+    else if (opt_.algo == 4) steps_ = 3;
+    else if (opt_.algo == 0 && auto_ms) steps_ = (want >= 3 && three_ok) ? 3 : (want >= 2 && two_ok) ? 2 : 1;
+    sstep_ = steps_ > 1;
   }
 
   mark("start");
@@ -126,8 +137,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // rows -1 .. nx+4 (two prefetch rows past the halo).  x[b] interleaves the
     // r and p planes by row.  Two-step sweep: halo depth 4 — columns -3 ..
     // 120·nstrips+4, rows -3 .. nx+6.
-    fsw_ = two_ ? dev::kFSW2 : dev::kFSW;
-    hdep_ = two_ ? 4 : 2;
+    fsw_ = steps_ == 3 ? dev::kFSW3 : steps_ == 2 ? dev::kFSW2 : dev::kFSW;
+    hdep_ = 2 * steps_;
     strips = (ny + fsw_ - 1) / fsw_;
     plane_ = ((fsw_ * strips + 2 * hdep_ + 7) / 8) * 8;
     if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
@@ -148,9 +159,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     mark("field allocs");
     set_fused_fields(fields_, xalt_, walt_);
     hsize_ = std::max<int64_t>(1, nx) * 4;
-    rows_hi = two_ ? nx + 6 : nx + 3;
-    cols_hi = two_ ? dev::kFSW2 * strips + 7 : dev::kFSW * strips + 3;
-    tab_lo_ = two_ ? -4 : -1;
+    // (multi-step: rows -hdep .. nx+hdep+2, columns -hdep .. fsw·strips+hdep+3)
+    rows_hi = sstep_ ? nx + hdep_ + 2 : nx + 3;
+    cols_hi = sstep_ ? fsw_ * strips + hdep_ + 3 : dev::kFSW * strips + 3;
+    tab_lo_ = sstep_ ? -hdep_ : -1;
   } else {
     strips = (ny + dev::kSW - 1) / dev::kSW;
     const int64_t A = blk_.alloc;
@@ -179,7 +191,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   PE_HIP_CHECK(hipEventCreate(&t1_));
 
   k.fused = fused_ ? 1 : 0;
-  k.steps = two_ ? 2 : 1;
+  k.steps = steps_;
   k.hdep = hdep_;
   k.nx = nx;
   k.ny = ny;
@@ -275,14 +287,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   //    155-159 vs 188 µs, 2400×3200 80 vs 109).
   if (fused_ && ti_env == 0) ti = huge ? 18 : big ? 24 : 10;
   k.order = (fused_ && huge) ? 3 : 0;
-  if (two_) {  // static LPT layout only; taller items (8 pipeline-fill rows each)
-    if (ti_env == 0) ti = big ? 40 : 24;
-    ti = std::max(4, std::min(ti, dev::kTImax2));
+  if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
+    if (ti_env == 0) ti = steps_ == 3 ? (big ? 48 : 32) : (big ? 40 : 24);
+    ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
   if (!fused_ && k.order > 1) k.order = 0;
-  if (two_) k.order = 0;
+  if (sstep_) k.order = 0;
   k.ti = (fused_ && ti_env < 0) ? 1 << 20 : ti;  // bands mode: long items → general kernel
   int per_cu = fused_ ? dev::resident_blocks_S(k, 2) : dev::resident_blocks_classic(opt_.variant);
   if (per_cu <= 0) per_cu = 4;
@@ -316,9 +328,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // within ±2 % over 24-48 rows: fixed 40 — one placement per grid,
   // tools/ti_probe.py, profiles/r3_ti_probe.txt).
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
-  if (two_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
+  static constexpr int kTiCands3[5] = {24, 32, 40, 48, 64};
+  const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
+  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
-  const int ti_min = tune_ti_ ? (two_ ? kTiCands2[0] : kTiCands[0]) : ti;
+  const int ti_min = tune_ti_ ? (sstep_ ? tic[0] : kTiCands[0]) : ti;
   set_items(ti);
   // block partials: interior grid, then (overlap) the boundary grid after it
   const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(wave_cap, wave_cap0) / dev::kWPB + 1), 4096);
@@ -365,13 +379,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // wave means a quarter of the waves runs a 4th item while the rest idle
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
     std::vector<int> cands(kTiCands, kTiCands + 4);
-    if (two_) cands.assign(kTiCands2, kTiCands2 + 5);  // (+ 0: the segment layout, added below)
+    if (sstep_) cands.assign(tic, tic + 5);  // (+ 0: the segment layout, added below)
     // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
     // at 18, one placement, profiles/r2_ti_big.txt)
-    if (npts >= 12e6 && !two_) cands.insert(cands.end(), {24, 30});
+    if (npts >= 12e6 && !sstep_) cands.insert(cands.end(), {24, 30});
     {
       const int64_t W = std::max(dev::kWPB, wave_cap_);
-      const int tlo = two_ ? kTiCands2[0] : kTiCands[0], thi = two_ ? dev::kTImax2 : 40;
+      const int tlo = sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? dev::kTImax3 : sstep_ ? dev::kTImax2 : 40;
       for (int q = 2; q <= 5; ++q)
         for (int t = tlo; t <= thi; ++t)
           if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
@@ -384,7 +398,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       // 8 pipeline-fill rows re-read once per segment; it lost to the LPT items
       // on the 2/4/8-rank 8192² slabs, 128 vs 110 µs per sweep at 8 ranks:
       // profiles/r3_block_probe.txt)
-      if (two_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
+      if (sstep_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
     }
     float best_ms = 0.f;
     int best = ti;
@@ -467,16 +481,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
-  const double t_iter = pts * (two_ ? 24.0 : fused_ ? 48.0 : 64.0) / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
+  const double t_iter = pts * (sstep_ ? 48.0 / steps_ : fused_ ? 48.0 : 64.0) / 4.5e12 + 6e-6 + (comm_->size() > 1 ? 40e-6 : 0.0);
   int c = int(0.5e-3 / t_iter);
   c = std::max(8, std::min(128, c));
   c += c & 1;
-  if (two_) c = (c + 3) / 4 * 4;  // whole sweeps, an even number of them (graph parity)
+  if (sstep_) c = (c + 2 * steps_ - 1) / (2 * steps_) * (2 * steps_);  // whole sweeps, an even number of them (graph parity)
   stream_chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
   if (resident_) c = 512;  // one launch per chunk (≈ 5 ms of iterations at 800×1200)
   chunk_ = opt_.chunk > 0 ? (opt_.chunk + (opt_.chunk & 1)) : c;
-  if (two_) {
-    chunk_ = (chunk_ + 3) / 4 * 4;
+  if (sstep_) {
+    chunk_ = (chunk_ + 2 * steps_ - 1) / (2 * steps_) * (2 * steps_);
     stream_chunk_ = chunk_;
   }
   mark("tuning+rest");
@@ -827,7 +841,7 @@ void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 // sums them over ranks itself (k.xr, P2P transport).
 void DeviceSolver::enqueue_fs_reduce(int par) {
   if (kp_->xr.peers) return;
-  if (two_) comm_->allreduce_sum(st_->fs2[par], dev::kNS2, stream_);
+  if (sstep_) comm_->allreduce_sum(st_->fs2[par], steps_ == 3 ? dev::kNS3 : dev::kNS2, stream_);
   else comm_->allreduce_sum(st_->fs[par], 7, stream_);
 }
 
@@ -846,7 +860,7 @@ hipEvent_t DeviceSolver::pooled_event() {
 
 void DeviceSolver::mark_begin(int ph, hipStream_t s) {
   if (!sampling_) return;
-  PhaseRec r{ph, sample_iter_, two_ ? 2 : 1, pooled_event(), nullptr};  // (a two-step sweep covers 2 iterations)
+  PhaseRec r{ph, sample_iter_, steps_, pooled_event(), nullptr};  // (a multi-step sweep covers steps_ iterations)
   PE_HIP_CHECK(hipEventRecord(r.a, s));
   recs_.push_back(r);
 }
@@ -869,7 +883,7 @@ void DeviceSolver::harvest(size_t n) {
   recs_.erase(recs_.begin(), recs_.begin() + std::ptrdiff_t(n));
 }
 
-void DeviceSolver::enqueue_iteration(int par) {
+void DeviceSolver::enqueue_iteration(int par, int mlimit) {
   const int ncomm = comm_->size();
   if (fused_ && overlap_) {
     KParams ko = *kp_;
@@ -912,7 +926,13 @@ void DeviceSolver::enqueue_iteration(int par) {
     }
   } else if (fused_) {
     mark_begin(kPhSweep, stream_);
-    dev::launch_S(*kp_, par, stream_, false);
+    if (mlimit > 0) {  // a partial three-step sweep: the run's last mlimit < 3 iterations
+      KParams kk = *kp_;
+      kk.mlimit = mlimit;
+      dev::launch_S(kk, par, stream_, false);
+    } else {
+      dev::launch_S(*kp_, par, stream_, false);
+    }
     mark_end(stream_);
     if (kp_->order == 3 && !kp_->fold) {
       mark_begin(kPhDot, stream_);
@@ -950,7 +970,7 @@ void DeviceSolver::enqueue_iteration(int par) {
       mark_end(stream_);
     }
   }
-  if (sampling_) sample_iter_ += two_ ? 2 : 1;
+  if (sampling_) sample_iter_ += mlimit > 0 ? mlimit : steps_;
 }
 
 // Chunk graphs are cached per length (a run of n iterations uses the chunk
@@ -958,7 +978,7 @@ void DeviceSolver::enqueue_iteration(int par) {
 hipGraphExec_t DeviceSolver::graph_for(int iters) {
   for (const auto& g : graphs_)
     if (g.first == iters) return g.second;
-  const int per = two_ ? 2 : 1;
+  const int per = steps_;
   if (iters % (2 * per)) throw std::logic_error("graph chunks must hold an even number of sweeps");
   hipGraph_t g = nullptr;
   hipGraphExec_t ge = nullptr;
@@ -1003,8 +1023,10 @@ void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
     PE_HIP_CHECK(hipGetLastError());
     return;
   }
-  // (two-step sweep: one launch = 2 iterations; chunks are multiples of 4)
-  const int per = two_ ? 2 : 1;
+  // (multi-step sweep: one launch = steps_ iterations; chunks are multiples
+  // of 2·steps_; a three-step run of n iterations ends with a partial sweep
+  // when 3 ∤ n)
+  const int per = steps_;
   if (sample_iters == 0 && opt_.use_graph && graphs_usable() && par_ == 0 && iters >= 2 * per) {
     const int n = iters - iters % (2 * per);
     PE_HIP_CHECK(hipGraphLaunch(graph_for(n), stream_));
@@ -1012,7 +1034,7 @@ void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   }
   for (; it < iters; it += per) {
     sampling_ = it < sample_iters;
-    enqueue_iteration(par_);
+    enqueue_iteration(par_, steps_ == 3 && iters - it < per ? iters - it : 0);
     par_ ^= 1;
   }
   sampling_ = false;
@@ -1023,7 +1045,7 @@ void DeviceSolver::prepare_graphs(int64_t iters) {
   if (!graphs_usable()) return;
   // the chunk lengths run_iterations(iters) launches from parity 0
   const int64_t full = iters / chunk_, rest = iters % chunk_;
-  const int64_t q = two_ ? 4 : 2;
+  const int64_t q = 2 * steps_;
   if (full > 0) graph_for(chunk_);
   if (rest >= q) graph_for(int(rest - rest % q));
   // the capture enqueued nothing: the stream state is unchanged
@@ -1049,7 +1071,14 @@ void DeviceSolver::wait_event(hipEvent_t ev) {
 }
 
 void DeviceSolver::enqueue_wflush() {
-  if (fused_) dev::launch_wflush(*kp_, stream_);
+  if (!fused_) return;
+  if (steps_ == 3) {  // a three-step sweep that converged early: its w fix-up (no-op otherwise)
+    KParams kk = *kp_;
+    kk.mlimit = -1;
+    dev::launch_S(kk, par_, stream_);
+    return;
+  }
+  dev::launch_wflush(*kp_, stream_);
 }
 
 void DeviceSolver::read_state(DevState* out) {
@@ -1110,7 +1139,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
-  res.algo = resident_ ? "resident" : two_ ? "two-step" : fused_ ? "fused" : "classic";
+  res.algo = resident_ ? "resident" : steps_ == 3 ? "three-step" : steps_ == 2 ? "two-step" : fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   // T_solver spans construction (allocation, tables, placement search) like

@@ -46,8 +46,8 @@
 // element 0 of a row is column −3.
 #include <cstdlib>
 
-#include "kcommon.hpp"
 #include "peer_sum.hpp"
+#include "sstep.hpp"
 
 #pragma clang fp contract(fast)
 
@@ -65,12 +65,6 @@ constexpr int FSW2 = kFSW2;
 #endif
 constexpr int kS2XD = PE_S2_XD, kS2WD = PE_S2_WD;
 constexpr int NS = kNS2;
-
-__device__ __forceinline__ double2 dd(double a, double b) { return make_double2(a, b); }
-__device__ __forceinline__ int2 cload_i2(const int2* p) {
-  const long long v = cload(reinterpret_cast<const long long*>(p));
-  return make_int2(int(v), int(v >> 32));
-}
 
 // Scalars of the sweep covering iterations K+1, K+2 (K = st->iter) from the
 // previous sweep's 20 unweighted sums R (a pure function of the state: every
@@ -153,10 +147,6 @@ __device__ __forceinline__ Term2 sweep2_term(const KParams& k, const Scal2& c) {
   return t;
 }
 
-__device__ __forceinline__ void hist_put(const KParams& k, long long kiter, double d) {
-  if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = d;
-}
-
 // Terminal state of a sweep that stops before its own work (brk1 / last1 /
 // brk2); one thread, after every wave of the grid has read the state.
 __device__ __forceinline__ void sweep2_terminal(const KParams& k, DevState* st, const Scal2& c, const Term2& t) {
@@ -231,115 +221,6 @@ __device__ void w_add_p1(const KParams& k, const double* xin, const Scal2& c) {
   }
 }
 
-// Per-wave LDS: the tables a boundary-band row evaluates its coefficients
-// from — the strip's row-table entries (per column) and the item's
-// column-table entries and row classes (per row, rows t0 .. t0+63) — and a
-// ring of the face coefficients of the last 6 rows (band items only).  A row
-// is evaluated ONCE, when it enters the pipeline (stage A): its vertical-face
-// a0 and horizontal-face b0 per column go to ring slot (row − t0) mod 6; the
-// stages that apply the operator to a band row read a0 of the row and of the
-// row below it (= its a1), b0 of the column and of the next one (= its b1,
-// written by the neighbouring lane) and form 1/D from them (dinv_faces: the
-// bits of the evaluation).  Plain rows keep the select path and no ring
-// reads.  In LDS rather than lanes: the five-stage march would spill.
-struct WaveTV2 {
-  double sA[128], eA[128], hB[130];
-  int4 rc[64];
-  double half[65], sB[64], eB[64];
-  double a0r[6][128];
-  double b0r[6][130];
-};
-
-typedef double v2d __attribute__((ext_vector_type(2)));
-__device__ __forceinline__ void st2nt(double* p, double2 v) {
-  __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
-}
-__device__ __forceinline__ double2 ldnt(const double* p) {
-  const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
-  return make_double2(t.x, t.y);
-}
-
-struct RowCtx {
-  int2 rcv;      // interior interval of row segbase + lane (lane l ↔ row segbase + l)
-  unsigned long long genmask;
-  int segbase;
-};
-
-// Stage rows below the item's first row (pipeline fill) are garbage rows
-// whose results are never used: the lane index is wrapped, not trusted.
-__device__ __forceinline__ void row_in(const RowCtx& rx, int q, int c0, bool& in0, bool& in1, bool& gen) {
-  const int l = (q - rx.segbase) & 63;
-  const int lo = __builtin_amdgcn_readlane(rx.rcv.x, l), hi = __builtin_amdgcn_readlane(rx.rcv.y, l);
-  in0 = c0 >= lo && c0 <= hi;
-  in1 = c0 + 1 >= lo && c0 + 1 <= hi;
-  gen = (rx.genmask >> l) & 1ull;
-}
-
-__device__ __forceinline__ double lap(const KParams& k, double f, double pm, double p0, double pn, double pl,
-                                      double pr) {
-  return f * (((p0 - pm) - (pn - p0)) * k.ih1sq + ((p0 - pl) - (pr - p0)) * k.ih2sq);
-}
-
-// Stage A of a band item: row q's faces into ring slot `sl`; returns 1/D.
-__device__ __forceinline__ double2 enter_band(const KParams& k, const RowCtx& rx, WaveTV2& tv, int q, int c0, int jl,
-                                              int sl) {
-  bool in0, in1, gen;
-  row_in(rx, q, c0, in0, in1, gen);
-  double2 d, a0, b0;
-  if (gen) {
-    const int l = (q - rx.segbase) & 63;
-    const int4 r4 = tv.rc[l];
-    const RowCls rc{r4.x, r4.y, r4.z, r4.w};
-    const CT ct{tv.half[l], tv.half[l + 1], tv.sB[l], tv.eB[l]};
-    const CS x0 = cset_rc(k, rc, ct, c0, TV{tv.sA[jl], tv.eA[jl], tv.hB[jl], tv.hB[jl + 1]});
-    const CS x1 = cset_rc(k, rc, ct, c0 + 1, TV{tv.sA[jl + 1], tv.eA[jl + 1], tv.hB[jl + 1], tv.hB[jl + 2]});
-    d = dd(x0.d, x1.d);
-    a0 = dd(x0.a0, x1.a0);
-    b0 = dd(x0.b0, x1.b0);
-  } else {
-    const double f0 = in0 ? 1.0 : k.inv_eps, f1 = in1 ? 1.0 : k.inv_eps;
-    d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
-    a0 = dd(f0, f1);
-    b0 = a0;
-  }
-  *reinterpret_cast<double2*>(&tv.a0r[sl][jl]) = a0;
-  *reinterpret_cast<double2*>(&tv.b0r[sl][jl]) = b0;
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  return d;
-}
-
-// The 5-point operator at row q (slot sl, the row below it in slot sln) for
-// the lane's two columns; d = 1/D of the row.
-template <bool BAND>
-__device__ __forceinline__ double2 apply2(const KParams& k, const RowCtx& rx, const WaveTV2& tv, int q, int c0, int jl,
-                                          int sl, int sln, const double2& um, const double2& u0, const double2& un,
-                                          double2& d) {
-  const double ul = dpp_shr1(u0.y), ur = dpp_shl1(u0.x);
-  bool in0, in1, gen;
-  row_in(rx, q, c0, in0, in1, gen);
-  if (BAND && gen) {
-    const double2 a0 = *reinterpret_cast<const double2*>(&tv.a0r[sl][jl]);
-    const double2 a1 = *reinterpret_cast<const double2*>(&tv.a0r[sln][jl]);
-    const double2 b0 = *reinterpret_cast<const double2*>(&tv.b0r[sl][jl]);
-    const double b2 = tv.b0r[sl][jl + 2];
-    const CS x0{a0.x, a1.x, b0.x, b0.y, dinv_faces(k, a0.x, a1.x, b0.x, b0.y)};
-    const CS x1{a0.y, a1.y, b0.y, b2, dinv_faces(k, a0.y, a1.y, b0.y, b2)};
-    d = dd(x0.d, x1.d);
-    return dd(stencil<false>(k, x0, um.x, u0.x, un.x, ul, u0.y), stencil<false>(k, x1, um.y, u0.y, un.y, u0.x, ur));
-  }
-  d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
-  return dd(lap(k, in0 ? 1.0 : k.inv_eps, um.x, u0.x, un.x, ul, u0.y),
-            lap(k, in1 ? 1.0 : k.inv_eps, um.y, u0.y, un.y, u0.x, ur));
-}
-
-__device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx, int q, int c0) {
-  bool in0, in1, gen;
-  row_in(rx, q, c0, in0, in1, gen);
-  return dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
-}
-
 // The item march (one strip × rows ib..ie), accumulating this wave's sums.
 // PUSH (row slabs over the P2P transport, KParams::push): output rows 1..4 /
 // nx-3..nx are also stored into the x-neighbours' fine-grained receive
@@ -355,7 +236,7 @@ __device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx
 // split across y — halo columns with real data — are not run by this kernel.)
 template <bool BAND, bool PUSH>
 __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par, int s, int ib, int ie,
-                                      WaveTV2& tvw, double (&acc)[NS]) {
+                                      WaveTV<6>& tvw, double (&acc)[NS]) {
   const int lane = threadIdx.x & 63;
   const int ny = int(k.ny);
   const int64_t pitch = k.pitch, poff = k.poff, wp = k.wpitch;
@@ -379,42 +260,8 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
   // reloaded every ~54 rows on tall items (stage rows t-4 .. t and the
   // column-table row t+1 stay inside the window).
   RowCtx rx;
-  auto load_seg = [&](int base) {
-    rx.segbase = base;
-    const int nr = ie + 6 - base;
-    const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
-    rx.rcv = make_int2(rc4.x, rc4.y);
-    rx.genmask = 0;
-    if (BAND) {
-      rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
-      if (rx.genmask != 0) {
-        const double* ctr = k.colT + (min(base + lane, ie + 5) + 1) * 4;
-        tvw.rc[lane] = rc4;
-        tvw.half[lane] = ctr[0];
-        tvw.sB[lane] = ctr[1];
-        tvw.eB[lane] = ctr[2];
-        if (lane == 63) tvw.half[64] = ctr[4];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      }
-    }
-  };
-  if (BAND) {  // the strip's row-table entries (per column), once per band item
-    const double* tb = k.rowT + (c0 + 1) * 4;
-    const double4 a = *reinterpret_cast<const double4*>(tb);
-    const double4 b = *reinterpret_cast<const double4*>(tb + 4);
-    tvw.sA[jl] = a.x;
-    tvw.eA[jl] = a.y;
-    tvw.hB[jl] = a.z;
-    tvw.sA[jl + 1] = b.x;
-    tvw.eA[jl + 1] = b.y;
-    tvw.hB[jl + 1] = b.z;
-    if (lane == 63) {
-      tvw.hB[128] = tb[10];
-      tvw.hB[129] = tb[14];
-    }
-  }
+  auto load_seg = [&](int base) { load_rows<BAND>(k, rx, tvw, base, ie + 5, J); };
+  if (BAND) load_strip_tables(k, tvw, c0);  // the strip's row-table entries, once per band item
   load_seg(t0);
   auto interior = [&](int q) {  // global interior row
     const int64_t gr = k.gi0 + q;
@@ -504,7 +351,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
       // ---- B: row t-1 ----
       {
         double2 d;
-        const double2 s1v = apply2<BAND>(k, rx, tvw, t - 1, c0, jl, r1s, r0, P1[s2], P1[s1], P1[s0], d);
+        const double2 s1v = apply_row<BAND>(k, rx, tvw, t - 1, c0, jl, r1s, r0, P1[s2], P1[s1], P1[s0], d);
         const double2 ri = RI[e1];
         const double2 r1 = dd(ri.x - a1 * s1v.x, ri.y - a1 * s1v.y);
         const bool rr = interior(t - 1);
@@ -517,7 +364,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
       {
         const int q = t - 2;
         double2 d;
-        const double2 s2v = apply2<BAND>(k, rx, tvw, q, c0, jl, r2s, r1s, P2[s0], P2[s2], P2[s1], d);
+        const double2 s2v = apply_row<BAND>(k, rx, tvw, q, c0, jl, r2s, r1s, P2[s0], P2[s2], P2[s1], d);
         const double2 r1 = R1[e0];
         const double2 r2 = dd(r1.x - a2 * s2v.x, r1.y - a2 * s2v.y);
         const bool rr = interior(q);
@@ -552,7 +399,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
       {
         const int q = t - 3;
         double2 d;
-        const double2 qv = apply2<BAND>(k, rx, tvw, q, c0, jl, r3s, r2s, Z2[s1], Z2[s0], Z2[s2], d);
+        const double2 qv = apply_row<BAND>(k, rx, tvw, q, c0, jl, r3s, r2s, Z2[s1], Z2[s0], Z2[s2], d);
         const bool rr = interior(q);
         const double2 sr = S2[e1];
         const double2 u = dd((rr && lv0) ? qv.x * d.x : 0.0, (rr && lv1) ? qv.y * d.y : 0.0);
@@ -579,8 +426,8 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
         const int q = t - 4;
         if (q >= ib && q <= ie) {
           double2 d;
-          const double2 au = apply2<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, U[s2], U[s1], U[s0], d);
-          const double2 av = apply2<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, V[s2], V[s1], V[s0], d);
+          const double2 au = apply_row<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, U[s2], U[s1], U[s0], d);
+          const double2 av = apply_row<BAND>(k, rx, tvw, q, c0, jl, r4s, r3s, V[s2], V[s1], V[s0], d);
           const double2 u = U[s1], v = V[s1];
           sv[7] += u.x * au.x + u.y * au.y;              // (u,Au)
           sv[8] += u.x * av.x + u.y * av.y;              // (u,Av)
@@ -606,7 +453,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   const Term2 tm = sweep2_term(k, sc);
   __shared__ double sm[4 * NS];
   __shared__ int sflag;
-  __shared__ WaveTV2 tvs[kWPB];
+  __shared__ WaveTV<6> tvs[kWPB];
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   if (done) return;
@@ -623,7 +470,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   for (int n = 0; n < NS; ++n) acc[n] = 0.0;
   {  // band ring: defined contents (the never-written column 128 of b0 and the
      // slots garbage pipeline-fill rows read stay finite)
-    WaveTV2& tv = tvs[wid];
+    WaveTV<6>& tv = tvs[wid];
     for (int i = lane; i < 6 * 128; i += 64) (&tv.a0r[0][0])[i] = 0.0;
     for (int i = lane; i < 6 * 130; i += 64) (&tv.b0r[0][0])[i] = 0.0;
   }

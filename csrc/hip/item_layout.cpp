@@ -77,7 +77,7 @@ void DeviceSolver::setup_items() {
   // PE_OVERLAP=1 / 0 forces it on / off.
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = false;
-  if (fused_ && !two_ && comm_->size() > 1 && nb && !push_) {  // (the two-step sweep runs without the overlap)
+  if (fused_ && !sstep_ && comm_->size() > 1 && nb && !push_) {  // (the two-step sweep runs without the overlap)
     if (e) {
       overlap_ = std::atoi(e) != 0;
     } else {
@@ -418,7 +418,7 @@ void DeviceSolver::setup_resident() {
   resident_ = false;
   const char* e = std::getenv("PE_RESIDENT");
   if (e && std::atoi(e) == 0) return;
-  if (!fused_ || two_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0)
+  if (!fused_ || sstep_ || comm_->size() != 1 || blk_.Px * blk_.Py != 1 || overlap_ || k.stamps || opt_.variant != 0)
     return;
   const int nx = int(blk_.nx);
   int cus = 256;

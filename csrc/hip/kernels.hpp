@@ -55,9 +55,16 @@ struct DevState {
   // so its wait is inside this one).
   unsigned long long xr_wait;
   unsigned long long xr_n;
-  // Two-step sweep (fused2.hip): the 20 unweighted sums of sweep k in
-  // fs2[k & 1] (layout: fused2.hip, sweep2_scalars).
+  // Multi-step sweeps: the unweighted sums of sweep k in fs2[k & 1] — 20
+  // (two-step, layout: fused2.hip, sweep2_scalars) or 19 (three-step:
+  // fused3.hip, sweep3_scalars).
   double fs2[2][24];
+  // Three-step sweep: the coefficients of the last sweep {zc[3], α[3], β[3],
+  // cw[3]} and fixpend = 1 when it converged before its last iteration — the
+  // next launch then subtracts Σ cw_j p_j from w (cw_j = −α_j past the stop).
+  double sc3[12];
+  int fixpend;
+  int pad3;
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
@@ -172,9 +179,13 @@ struct KParams {
   // idles X µs (in ticks) before the cross-rank sum (T_MPI test hook)
   long long slow_ticks;
   // iterations per sweep: 1 single sweep (fused.hip kS), 2 two-step sweep
-  // (fused2.hip kS2: 4-deep halo, 120-column strips, 20 sums)
+  // (fused2.hip kS2: 4-deep halo, 120-column strips, 20 sums), 3 three-step
+  // sweep (fused3.hip kS3: 6-deep halo, 116-column strips, 19 sums)
   int steps;
-  int hdep;  // halo depth of the single-sweep layouts: 2 (kS), 4 (kS2); rows per side of a push message
+  int hdep;  // halo depth of the single-sweep layouts: 2 (kS), 4 (kS2), 6 (kS3); rows per side of a push message
+  // three-step sweep: > 0 → this launch applies at most mlimit iterations (a
+  // run of n iterations ends with a partial sweep when 3 ∤ n)
+  int mlimit;
 };
 constexpr int kFoldGroup = 64;
 
@@ -191,6 +202,9 @@ constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (
 constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
 constexpr int kNS2 = 20;         // two-step sweep: sums per sweep
 constexpr int kTImax2 = 48;      // two-step sweep: max rows per item (rows ib-4 .. ie+5 live one per lane)
+constexpr int kFSW3 = 116;       // three-step sweep: output columns per strip (6-column halo per side)
+constexpr int kNS3 = 19;         // three-step sweep: sums per sweep
+constexpr int kTImax3 = 64;      // three-step sweep: max rows per item
 
 // LDS-resident single sweep (resident.hip): small single-rank blocks run many
 // iterations in ONE launch.  The block is cut into tiles of one 124-column
@@ -281,6 +295,11 @@ int resident_blocks_S(const KParams& k, int wm);  // wm 0: deferring sweep, 2: a
 // item list only; launch_S dispatches here when k.steps == 2).
 void launch_S2(const KParams& k, int par, hipStream_t s);
 int resident_blocks_S2();
+// Three-step sweep (fused3.hip): one launch = iterations K+1..K+3 (or fewer:
+// k.mlimit, breakdown, cap), or the w fix-up of a sweep that converged early
+// (DevState::fixpend); launch_S dispatches here when k.steps == 3.
+void launch_S3(const KParams& k, int par, hipStream_t s);
+int resident_blocks_S3();
 // (k.ti / k.order select the kernel variant: set them first)
 int resident_blocks_classic(int variant);
 

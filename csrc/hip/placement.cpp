@@ -197,7 +197,7 @@ bool DeviceSolver::placement_search(bool retry) {
   // best-class threshold: the single sweep's 40 B/node at ≥ 4.9 TB/s (8192²:
   // ≤ 0.548 ms); the two-step sweep's 48 B/node per sweep at ≥ 4.7 TB/s
   // (8192²: its classes are 0.676-0.69 and 0.83-0.85 ms per sweep)
-  double fast_tbs = two_ ? 4.7 : 4.9, max_s = 0.3;
+  double fast_tbs = sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return true;
@@ -272,7 +272,7 @@ bool DeviceSolver::placement_search(bool retry) {
     // PE_PLACEMENT_FAST_TBS (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
     // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
     // 0.56-0.60 ms placements when better ones were a try or two further.)
-    const double bps = two_ ? 48.0 : 40.0;  // streamed bytes per node and sweep
+    const double bps = sstep_ ? 48.0 : 40.0;  // streamed bytes per node and sweep
     const double tbs = bps * pts / (double(c[t].ms) / 6.0 * 1e-3) / 1e12;
     if (tbs >= fast_tbs) {
       fast = true;
@@ -299,7 +299,7 @@ bool DeviceSolver::placement_search(bool retry) {
   // a retry appends its candidates (its first is the first round's pick, re-timed)
   placement_best_ = int(placement_ms_.size() + best);
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
-  return fast || (two_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
+  return fast || (sstep_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
 }
 
 // Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE

@@ -1,0 +1,202 @@
+// Shared device pieces of the multi-iteration sweeps (fused2.hip: two
+// iterations per pass, fused3.hip: three): the per-lane helpers of the row
+// march, the boundary-band coefficient ring in LDS and the 5-point operator
+// on a lane's two columns.  Both kernels march one wave64 strip down the rows
+// of an item with a pipeline of stages; each stage applies the operator to a
+// row of a vector the previous stage produced, j-neighbours through DPP lane
+// shifts, i-neighbours from rotating register rings.
+#pragma once
+
+#include "kcommon.hpp"
+
+// (the including sweeps are built with fast contraction; so are these helpers)
+#pragma clang fp contract(fast)
+
+namespace pe {
+namespace dev {
+namespace {
+
+__device__ __forceinline__ double2 dd(double a, double b) { return make_double2(a, b); }
+__device__ __forceinline__ int2 cload_i2(const int2* p) {
+  const long long v = cload(reinterpret_cast<const long long*>(p));
+  return make_int2(int(v), int(v >> 32));
+}
+
+// A wave-uniform double in scalar registers (the scalars of a sweep are a
+// pure function of the state every lane read: pin them to SGPRs so the long
+// marches keep their VGPRs for the row rings).
+__device__ __forceinline__ double uni(double x) {
+  const long long v = __double_as_longlong(x);
+  const unsigned lo = unsigned(__builtin_amdgcn_readfirstlane(int(unsigned(v))));
+  const unsigned hi = unsigned(__builtin_amdgcn_readfirstlane(int(v >> 32)));
+  return __longlong_as_double((long long)((unsigned long long)hi << 32 | lo));
+}
+
+__device__ __forceinline__ void hist_put(const KParams& k, long long kiter, double d) {
+  if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = d;
+}
+
+typedef double v2d __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st2nt(double* p, double2 v) {
+  __builtin_nontemporal_store(v2d{v.x, v.y}, reinterpret_cast<v2d*>(p));
+}
+__device__ __forceinline__ double2 ldnt(const double* p) {
+  const v2d t = __builtin_nontemporal_load(reinterpret_cast<const v2d*>(p));
+  return make_double2(t.x, t.y);
+}
+
+// Per-wave LDS of a multi-iteration march: the tables a boundary-band row
+// evaluates its coefficients from — the strip's row-table entries (per
+// column) and the item's column-table entries and row classes (per row, rows
+// segbase .. segbase+63) — and a ring of the face coefficients of the last
+// RING rows (band items only).  A row is evaluated ONCE, when it enters the
+// pipeline (its first stage): its vertical-face a0 and horizontal-face b0 per
+// column go to a ring slot; the stages that apply the operator to a band row
+// read a0 of the row and of the row below it (= its a1), b0 of the column and
+// of the next one (= its b1, written by the neighbouring lane) and form 1/D
+// from them (dinv_faces: the bits of the evaluation).  Plain rows keep the
+// select path and no ring reads.  In LDS rather than lanes: the marches would
+// spill.
+template <int RING>
+struct WaveTV {
+  double sA[128], eA[128], hB[130];
+  int4 rc[64];
+  double half[65], sB[64], eB[64];
+  double a0r[RING][128];
+  double b0r[RING][130];  // (column 128: read by lane 63 for its b1, never written)
+  static constexpr int kRing = RING;
+};
+
+struct RowCtx {
+  int2 rcv;      // interior interval of row segbase + lane (lane l ↔ row segbase + l)
+  unsigned long long genmask;
+  int segbase;
+};
+
+// Stage rows below the item's first row (pipeline fill) are garbage rows
+// whose results are never used: the lane index is wrapped, not trusted.
+__device__ __forceinline__ void row_in(const RowCtx& rx, int q, int c0, bool& in0, bool& in1, bool& gen) {
+  const int l = (q - rx.segbase) & 63;
+  const int lo = __builtin_amdgcn_readlane(rx.rcv.x, l), hi = __builtin_amdgcn_readlane(rx.rcv.y, l);
+  in0 = c0 >= lo && c0 <= hi;
+  in1 = c0 + 1 >= lo && c0 + 1 <= hi;
+  gen = (rx.genmask >> l) & 1ull;
+}
+
+__device__ __forceinline__ double lap(const KParams& k, double f, double pm, double p0, double pn, double pl,
+                                      double pr) {
+  return f * (((p0 - pm) - (pn - p0)) * k.ih1sq + ((p0 - pl) - (pr - p0)) * k.ih2sq);
+}
+
+// Row classes / column tables of rows base .. base+63 (one per lane) into the
+// lane registers (and, for band items with a boundary row in the window, the
+// wave's LDS tables); rows past `last` get an empty interior interval.
+template <bool BAND, class WT>
+__device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw, int base, int last, int J) {
+  const int lane = threadIdx.x & 63;
+  rx.segbase = base;
+  const int nr = last + 1 - base;
+  const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+  rx.rcv = make_int2(rc4.x, rc4.y);
+  rx.genmask = 0;
+  if (BAND) {
+    rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
+    if (rx.genmask != 0) {
+      const double* ctr = k.colT + (min(base + lane, last) + 1) * 4;
+      tvw.rc[lane] = rc4;
+      tvw.half[lane] = ctr[0];
+      tvw.sB[lane] = ctr[1];
+      tvw.eB[lane] = ctr[2];
+      if (lane == 63) tvw.half[64] = ctr[4];
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    }
+  }
+}
+
+// The strip's row-table entries (per column), once per band item.
+template <class WT>
+__device__ __forceinline__ void load_strip_tables(const KParams& k, WT& tvw, int c0) {
+  const int lane = threadIdx.x & 63, jl = 2 * lane;
+  const double* tb = k.rowT + (c0 + 1) * 4;
+  const double4 a = *reinterpret_cast<const double4*>(tb);
+  const double4 b = *reinterpret_cast<const double4*>(tb + 4);
+  tvw.sA[jl] = a.x;
+  tvw.eA[jl] = a.y;
+  tvw.hB[jl] = a.z;
+  tvw.sA[jl + 1] = b.x;
+  tvw.eA[jl + 1] = b.y;
+  tvw.hB[jl + 1] = b.z;
+  if (lane == 63) {
+    tvw.hB[128] = tb[10];
+    tvw.hB[129] = tb[14];
+  }
+}
+
+// First stage of a band item: row q's faces into ring slot `sl`; returns 1/D.
+template <class WT>
+__device__ __forceinline__ double2 enter_band(const KParams& k, const RowCtx& rx, WT& tv, int q, int c0, int jl,
+                                              int sl) {
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  double2 d, a0, b0;
+  if (gen) {
+    const int l = (q - rx.segbase) & 63;
+    const int4 r4 = tv.rc[l];
+    const RowCls rc{r4.x, r4.y, r4.z, r4.w};
+    const CT ct{tv.half[l], tv.half[l + 1], tv.sB[l], tv.eB[l]};
+    const CS x0 = cset_rc(k, rc, ct, c0, TV{tv.sA[jl], tv.eA[jl], tv.hB[jl], tv.hB[jl + 1]});
+    const CS x1 = cset_rc(k, rc, ct, c0 + 1, TV{tv.sA[jl + 1], tv.eA[jl + 1], tv.hB[jl + 1], tv.hB[jl + 2]});
+    d = dd(x0.d, x1.d);
+    a0 = dd(x0.a0, x1.a0);
+    b0 = dd(x0.b0, x1.b0);
+  } else {
+    const double f0 = in0 ? 1.0 : k.inv_eps, f1 = in1 ? 1.0 : k.inv_eps;
+    d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+    a0 = dd(f0, f1);
+    b0 = a0;
+  }
+  *reinterpret_cast<double2*>(&tv.a0r[sl][jl]) = a0;
+  *reinterpret_cast<double2*>(&tv.b0r[sl][jl]) = b0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return d;
+}
+
+// The 5-point operator at row q (ring slot sl, the row above it in slot sln)
+// for the lane's two columns; d = 1/D of the row.
+template <bool BAND, class WT>
+__device__ __forceinline__ double2 apply_row(const KParams& k, const RowCtx& rx, const WT& tv, int q, int c0, int jl,
+                                             int sl, int sln, const double2& um, const double2& u0, const double2& un,
+                                             double2& d) {
+  const double ul = dpp_shr1(u0.y), ur = dpp_shl1(u0.x);
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  if (BAND && gen) {
+    const double2 a0 = *reinterpret_cast<const double2*>(&tv.a0r[sl][jl]);
+    const double2 a1 = *reinterpret_cast<const double2*>(&tv.a0r[sln][jl]);
+    const double2 b0 = *reinterpret_cast<const double2*>(&tv.b0r[sl][jl]);
+    const double b2 = tv.b0r[sl][jl + 2];
+    const CS x0{a0.x, a1.x, b0.x, b0.y, dinv_faces(k, a0.x, a1.x, b0.x, b0.y)};
+    const CS x1{a0.y, a1.y, b0.y, b2, dinv_faces(k, a0.y, a1.y, b0.y, b2)};
+    d = dd(x0.d, x1.d);
+    return dd(stencil<false>(k, x0, um.x, u0.x, un.x, ul, u0.y), stencil<false>(k, x1, um.y, u0.y, un.y, u0.x, ur));
+  }
+  d = dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+  return dd(lap(k, in0 ? 1.0 : k.inv_eps, um.x, u0.x, un.x, ul, u0.y),
+            lap(k, in1 ? 1.0 : k.inv_eps, um.y, u0.y, un.y, u0.x, ur));
+}
+
+__device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx, int q, int c0) {
+  bool in0, in1, gen;
+  row_in(rx, q, c0, in0, in1, gen);
+  return dd(in0 ? k.dinv_in : k.dinv_out, in1 ? k.dinv_in : k.dinv_out);
+}
+
+__device__ __forceinline__ double dot2(const double2& a, const double2& b) { return a.x * b.x + a.y * b.y; }
+
+}  // namespace
+}  // namespace dev
+}  // namespace pe

@@ -164,7 +164,8 @@ class DeviceSolver {
   std::vector<Exchange> halo_plan() const;  // classic: the single phase
   bool fused() const { return fused_; }
   // two iterations per sweep (fused2.hip)
-  bool two_step() const { return two_; }
+  bool two_step() const { return sstep_; }     // a multi-iteration sweep (two- or three-step)
+  int sweep_steps() const { return steps_; }   // iterations per sweep launch: 1, 2 or 3
   bool segment_layout() const { return seg_layout_; }  // static layout of one tall segment per wave
   // LDS-resident single sweep (resident.hip): small single-rank blocks run
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
@@ -224,7 +225,7 @@ class DeviceSolver {
   void measure_exchange();  // sets exchange_us_ (collective)
   void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
   void set_items(int ti);   // item counts and persistent grids for `ti` rows per item
-  void enqueue_iteration(int par);
+  void enqueue_iteration(int par, int mlimit = 0);  // mlimit > 0: a partial three-step sweep
   void enqueue_fs_reduce(int par);  // cross-rank sum of sweep sums (no-op when the sweep does it)
   // after_sweep: the halo of `buf` was produced by a sweep (with the halo
   // push: import it); false for the initial state (the comm's exchange).
@@ -261,9 +262,10 @@ class DeviceSolver {
   SolveOptions opt_;
   hipStream_t stream_ = nullptr;
   bool fused_ = false;
-  bool two_ = false;      // two-step sweep (fused2.hip): 2 iterations per launch
-  int fsw_ = 124;         // output columns per strip (kFSW / kFSW2)
-  int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4)
+  bool sstep_ = false;    // multi-iteration sweep (fused2.hip / fused3.hip): steps_ iterations per launch
+  int steps_ = 1;         // iterations per sweep launch (1, 2, 3)
+  int fsw_ = 124;         // output columns per strip (kFSW / kFSW2 / kFSW3)
+  int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4 / 6)
   int64_t tab_lo_ = -1;   // first local index of the chord tables / row classes
   bool seg_layout_ = false;  // static layout of tall equal-cost segments, one per wave (setup_items)
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w

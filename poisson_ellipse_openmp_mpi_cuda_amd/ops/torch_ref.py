@@ -304,6 +304,112 @@ def two_step(prob: EllipseProblem, sweeps: int, device="cpu") -> TwoStepState:
     return TwoStepState(sweeps, sums, alphas, betas, diffs, r, p, w)
 
 
+@dataclass
+class ThreeStepState:
+    sweeps: int
+    sums: list    # per sweep j = 0 (S_0) .. J: the 19 unweighted sums (csrc/hip/fused3.hip layout)
+    alpha: list   # (α₁, α₂, α₃) per sweep j ≥ 1
+    beta: list    # (β₁, β₂, β₃)
+    diff: list    # ‖Δw‖ of its three iterations (late: from the sweep's own ‖p_i‖² sums)
+    r: torch.Tensor
+    p: torch.Tensor
+    w: torch.Tensor
+
+
+def three_step_moments(r, p, a, b, h1, h2, Dinv):
+    """The 16 D-moments of the basis around (r, p) (fused3.hip sums 0..15)."""
+    inner = lambda u, v: float((u[1:-1, 1:-1] * v[1:-1, 1:-1]).sum())  # noqa: E731  (unweighted)
+    A = lambda u: apply_A(u, a, b, h1, h2)  # noqa: E731
+    z = Dinv * r
+    s = A(p)
+    q = A(z)
+    u, v = Dinv * q, Dinv * s
+    Au, Av = A(u), A(v)
+    uu, vv = Dinv * Au, Dinv * Av
+    Auu, Avv = A(uu), A(vv)
+    return [inner(r, z), inner(z, q), inner(q, u), inner(u, Au), inner(Au, uu), inner(uu, Auu),
+            inner(z, s), inner(q, v), inner(u, Av), inner(Au, vv), inner(uu, Avv),
+            inner(p, s), inner(s, v), inner(v, Av), inner(Av, vv), inner(vv, Avv)]
+
+
+def _mform(xz, xp, mzz, mzp, mpp, sh):
+    s = 0.0
+    for i in range(3):
+        for j in range(3):
+            n = i + j + sh
+            s += xz[i] * (xz[j] * mzz[n] + 2.0 * xp[j] * mzp[n]) + xp[i] * xp[j] * mpp[n]
+    return s
+
+
+def three_step_scalars(R, gprev: float, K: int, hh: float, lim: int = 3):
+    """[(g, β, α)] of the (up to lim) iterations of the sweep after K from the
+    previous sweep's sums R — fused3.hip's sweep3_scalars (None past a breakdown)."""
+    mzz = R[0:6]
+    mzp = [0.0] + list(R[6:11])
+    mpp = [0.0] + list(R[11:16])
+    zz, zp = [1.0, 0.0, 0.0], [0.0, 0.0, 0.0]
+    pz, pp = [0.0, 0.0, 0.0], [1.0, 0.0, 0.0]
+    g = _mform(zz, zp, mzz, mzp, mpp, 0) * hh
+    out = []
+    for i in range(lim):
+        beta = 0.0 if K + i == 0 else g / gprev
+        pz = [zz[q] + beta * pz[q] for q in range(3)]
+        pp = [zp[q] + beta * pp[q] for q in range(3)]
+        den = _mform(pz, pp, mzz, mzp, mpp, 1) * hh
+        if not math.isfinite(den) or abs(den) < 1e-15:
+            break
+        alpha = g / den
+        out.append((g, beta, alpha))
+        gprev = g
+        if i + 1 < lim:
+            zz[2] -= alpha * pz[1]
+            zz[1] -= alpha * pz[0]
+            zp[2] -= alpha * pp[1]
+            zp[1] -= alpha * pp[0]
+            g = _mform(zz, zp, mzz, mzp, mpp, 0) * hh
+    return out
+
+
+def three_step(prob: EllipseProblem, sweeps: int, device="cpu") -> ThreeStepState:
+    """The three-iterations-per-sweep recurrence of csrc/hip/fused3.hip on the
+    reference operator (divisions): S_0, then `sweeps` full sweeps, each
+    advancing iterations K+1..K+3 with scalars from the previous sweep's 16
+    moments; the sweep's own ‖p_i‖² give the (late) ‖Δw‖.  Algebraically the
+    reference PCG (stage2-mpi/poisson_mpi_decomp.cpp:400-457)."""
+    a, b, B = assemble(prob, device)
+    h1, h2 = prob.h1, prob.h2
+    hh = h1 * h2
+    D = diag(a, b, h1, h2)
+    Dinv = torch.zeros_like(D)
+    m = D != 0
+    Dinv[m] = 1.0 / D[m]
+    A = lambda u: apply_A(u, a, b, h1, h2)  # noqa: E731
+    inner = lambda u, v: float((u[1:-1, 1:-1] * v[1:-1, 1:-1]).sum())  # noqa: E731
+    weighted = prob.norm == "weighted"
+    r = B.clone()
+    p = torch.zeros_like(B)
+    w = torch.zeros_like(B)
+    sums = [three_step_moments(r, p, a, b, h1, h2, Dinv) + [0.0, 0.0, 0.0]]
+    alphas, betas, diffs = [], [], []
+    gprev = 0.0
+    for j in range(1, sweeps + 1):
+        K = 3 * (j - 1)
+        sc = three_step_scalars(sums[-1], gprev, K, hh)
+        assert len(sc) == 3, "breakdown inside the reference sweeps"
+        norms = []
+        for (g, beta, alpha) in sc:
+            p = Dinv * r + beta * p
+            norms.append(inner(p, p))
+            r = r - alpha * A(p)
+            w = w + alpha * p
+            gprev = g
+        alphas.append(tuple(x[2] for x in sc))
+        betas.append(tuple(x[1] for x in sc))
+        diffs.append(tuple(abs(x[2]) * math.sqrt(n * hh if weighted else n) for x, n in zip(sc, norms)))
+        sums.append(three_step_moments(r, p, a, b, h1, h2, Dinv) + norms)
+    return ThreeStepState(sweeps, sums, alphas, betas, diffs, r, p, w)
+
+
 def error_vs_analytic(prob: EllipseProblem, w: torch.Tensor):
     """(L2 error in D, h-weighted; max error in D) against u = F(1-cx x²-cy y²)/(2cx+2cy)."""
     x, y = _grid(prob, w.device)

@@ -353,8 +353,8 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
     assert d["xr"] == (allreduce in ("p2p", "p2p-exchange", "p2p-dyn"))
     assert d["halo_push"] == (d["Py"] == 1 and allreduce in ("p2p", "p2p-dyn"))
-    # row slabs run the two-step sweep (4-deep halo: pushed, or exchanged), 2D blocks the single sweep
-    assert d["algo"] == ("two-step" if d["Py"] == 1 else "fused"), d["algo"]
+    # row slabs run the three-step sweep (6-deep halo: pushed, or exchanged), 2D blocks the single sweep
+    assert d["algo"] == ("three-step" if d["Py"] == 1 else "fused"), d["algo"]
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
@@ -430,7 +430,7 @@ def test_bench_halo_push_graphs(gpu, nproc):
     assert c["decomposition"]["Px"] == nproc and c["decomposition"]["Py"] == 1
     assert c["halo"] == "in-sweep xGMI push (graph-captured)", c
     assert c["allreduce"] == "in-sweep P2P over xGMI"
-    assert c["algo"].startswith("two-step")
+    assert c["algo"].startswith("three-step")
     assert d["valid"] and d["converged"] and abs(d["iters_converged"] - one.iters) <= 1
     assert d["l2_err"] == pytest.approx(one.l2_err, rel=1e-6)
 
@@ -506,7 +506,7 @@ def test_slow_rank_shows_in_tmpi(gpu):
 
     base, algo = run(None)
     slow, _ = run("slow@rank:1,us:300")
-    sums = 546 // 2 if algo == "two-step" else 546  # one cross-rank sum per sweep
+    sums = 546 // {"three-step": 3, "two-step": 2}.get(algo, 1)  # one cross-rank sum per sweep
     want = sums * 300e-6
     assert 0.7 * want <= slow - base <= 2.0 * want, (base, slow, algo)
 

@@ -100,3 +100,36 @@ def test_two_step_stop_test_matches_reference_history():
     two = torch_ref.two_step(prob, (ref.iters + 1) // 2)
     diffs = [d for pair in two.diff for d in pair][: ref.iters]
     np.testing.assert_allclose(diffs, ref.history, rtol=1e-7)
+
+
+@pytest.mark.parametrize("M,N", [(40, 40), (60, 90), (31, 17)])
+def test_three_step_recurrence_is_pcg(M, N):
+    """The three-iterations-per-sweep recurrence of csrc/hip/fused3.hip
+    (torch_ref.three_step: scalars of iterations K+1..K+3 from 16 D-moments of
+    z, p around r_K, p_K) against the single-sweep recurrence: same α, β, w to
+    rounding; its late ‖Δw‖ gives the reference's stop iteration."""
+    prob = EllipseProblem(M, N)
+    J = 8
+    three = torch_ref.three_step(prob, J)
+    one = torch_ref.single_sweep(prob, 3 * J)
+    for j in range(J):
+        for s in range(3):
+            assert three.alpha[j][s] == pytest.approx(one.alpha[3 * j + s], rel=1e-9)
+            assert three.beta[j][s] == pytest.approx(one.beta[3 * j + s], rel=1e-8, abs=1e-14)
+    scale = float(one.w.abs().max())
+    assert float((three.w - one.w).abs().max()) <= 1e-11 * scale
+    ref = torch_ref.pcg(prob)
+    diffs = [d for t in three.diff for d in t]
+    k = next((i + 1 for i, d in enumerate(diffs) if d < prob.tol), None)
+    if k is not None:
+        assert k == ref.iters
+
+
+def test_three_step_stop_test_matches_reference_history():
+    """‖Δw‖ of every iteration from the three-step sweep's own ‖p_i‖² sums
+    equals the reference loop's norm (rel 1e-7) up to convergence."""
+    prob = EllipseProblem(40, 40)
+    ref = torch_ref.pcg(prob, keep_history=True)
+    three = torch_ref.three_step(prob, (ref.iters + 2) // 3)
+    diffs = [d for t in three.diff for d in t][: ref.iters]
+    np.testing.assert_allclose(diffs, ref.history, rtol=1e-7)
