@@ -139,9 +139,10 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
   double pz[3] = {0.0, 0.0, 0.0}, pp[3] = {1.0, 0.0, 0.0};  // p_{i-1}
   double g = mform(zz, zp, mzz, mzp, mpp, 0) * hh;
   double gprev = st->gprev;
+  bool live = true;  // (fully unrolled, no early exit: the arrays stay in registers)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
-    if (i >= lim) break;
+    live = live && i < lim;
     const double beta = c.K + i == 0 ? 0.0 : g / gprev;
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
@@ -151,20 +152,21 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
     const double den = mform(pz, pp, mzz, mzp, mpp, 1) * hh;
     const bool tiny = fabs(den) < 1e-15;
     const bool bad = !isfinite(g) || !isfinite(den);
-    if (tiny || bad) {
+    if (live && (tiny || bad)) {
       c.brk = i + 1;
       c.bad = bad;
-      break;
+      live = false;
     }
-    const double alpha = g / den;
-    c.c.zc[i] = 1.0;
-    c.c.a[i] = alpha;
-    c.c.b[i] = beta;
-    c.c.cw[i] = alpha;
-    c.g[i] = g;
-    c.m = i + 1;
-    gprev = g;
-    if (i + 1 < lim) {  // z_i = z_{i-1} − α M p_i
+    if (live) {
+      const double alpha = g / den;
+      c.c.zc[i] = 1.0;
+      c.c.a[i] = alpha;
+      c.c.b[i] = beta;
+      c.c.cw[i] = alpha;
+      c.g[i] = g;
+      c.m = i + 1;
+      gprev = g;
+      // z_i = z_{i-1} − α M p_i
       zz[2] -= alpha * pz[1];
       zz[1] -= alpha * pz[0];
       zp[2] -= alpha * pp[1];
@@ -209,25 +211,25 @@ __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, 
   }
   const double hh = k.h1 * k.h2;
   int stop = 0, status = 0;
-  for (int i = 0; i < c.m; ++i) {
-    const double n2 = fmax(t[16 + i], 0.0);
-    const double d = k.weighted ? fabs(c.c.a[i]) * sqrt(n2 * hh) : fabs(c.c.a[i]) * sqrt(n2);
-    hist_put(k, c.K + i + 1, d);
-    st->last_diff = d;
-    st->alpha = c.c.a[i];
-    st->beta = c.c.b[i];
-    st->rz_cur = c.g[i];
-    st->gprev = c.g[i];
-    st->iter = c.K + i + 1;
-    if (!isfinite(d)) {
-      status = 4;
-      stop = i + 1;
-      break;
-    }
-    if (k.check_tol && d < k.tol) {
-      status = 1;
-      stop = i + 1;
-      break;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (stop == 0 && i < c.m) {
+      const double n2 = fmax(t[16 + i], 0.0);
+      const double d = k.weighted ? fabs(c.c.a[i]) * sqrt(n2 * hh) : fabs(c.c.a[i]) * sqrt(n2);
+      hist_put(k, c.K + i + 1, d);
+      st->last_diff = d;
+      st->alpha = c.c.a[i];
+      st->beta = c.c.b[i];
+      st->rz_cur = c.g[i];
+      st->gprev = c.g[i];
+      st->iter = c.K + i + 1;
+      if (!isfinite(d)) {
+        status = 4;
+        stop = i + 1;
+      } else if (k.check_tol && d < k.tol) {
+        status = 1;
+        stop = i + 1;
+      }
     }
   }
   if (stop == 0) {
@@ -238,13 +240,323 @@ __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, 
       status = 3;
     }
   } else if (stop < c.m && status == 1) {  // w holds the later iterations' terms: the next launch subtracts them
-    for (int j = stop; j < c.m; ++j) st->sc3[9 + j] = -c.c.a[j];
+#pragma unroll
+    for (int j = 1; j < 3; ++j)
+      if (j >= stop && j < c.m) st->sc3[9 + j] = -c.c.a[j];
     st->fixpend = 1;
   }
   if (status) {
     st->status = status;
     st->done = 1;
   }
+}
+
+// Item kinds (list entry flags): band items (a boundary-band row in the
+// window: coefficients from the chord tables, LDS face ring), uniform items
+// (kUniBit: every row of the window lies wholly inside or wholly outside the
+// interior in this strip — the row's coefficients are three scalars) and
+// mixed plain items (per-lane interior tests).
+enum { kMixed = 0, kBand = 1, kUniform = 2 };
+
+// Lane / item constants of one march.
+struct M3Ctx {
+  const double* Xm;   // input rows, at column -5
+  double* Ym;         // output rows
+  double* Wm;         // w rows
+  const double* hrd;  // PUSH: receive buffer of the parity this sweep reads
+  int64_t pitch, poff, wp;
+  int J, c0, jl, ib, ie, t0, tmax, nx, par;
+  unsigned off;
+  bool lv0, lv1, o0, o1, fix;
+  double lf0, lf1;    // lv0 / lv1 as 1.0 / 0.0 (uniform items of the edge strips)
+  double oih1, oih2;  // inv_eps / h1², inv_eps / h2² (uniform exterior rows)
+  double ih1, ih2, din, dout;  // 1/h1², 1/h2², 1/D interior / exterior (copies: a select between
+                               // kernel-argument fields compiles to a scalar load per use)
+  int rlo, rhi;       // local rows of the global interior: rlo ≤ q ≤ rhi
+  unsigned offb, offpb, offwb;  // lane byte offsets: r plane, p plane (x rows), w rows
+  double zc1, zc2, zc3, a1, a2, a3, b1, b2, b3, w1, w2, w3;
+};
+
+// The march's register state: prefetch rings and the stage row rings.
+struct M3Rings {
+  double2 RQ[kS3XD], PQ[kS3XD], WQ[kS3WD];
+  double2 P1[3], RI[2], R1[2], P2[3], R2[2], P3[3], Z[3], S[2], U[3], V[3], UU[3], VV[3];
+  bool pushed;
+};
+
+// Row scalars of a uniform row: 1/h1², 1/h2² times the row's face
+// coefficient, and 1/D (0 outside the global interior rows).
+struct URow {
+  double ih1, ih2, d;
+};
+
+template <bool STEADY>
+__device__ __forceinline__ URow urow(const KParams& k, const M3Ctx& c, const RowCtx& rx, int q) {
+  const int l = (q - rx.segbase) & 63;
+  const bool in = (rx.allin >> l) & 1ull;
+  URow r;
+  r.ih1 = in ? c.ih1 : c.oih1;
+  r.ih2 = in ? c.ih2 : c.oih2;
+  r.d = in ? c.din : c.dout;
+  if constexpr (!STEADY) {
+    if (!(q >= c.rlo && q <= c.rhi)) r.d = 0.0;
+  }
+  return r;
+}
+
+// The 5-point operator of a uniform row on the lane's two columns.
+__device__ __forceinline__ double2 lapu(const URow& r, const double2& um, const double2& u0, const double2& un) {
+  const double ul = dpp_shr1(u0.y), ur = dpp_shl1(u0.x);
+  return dd(((u0.x - um.x) - (un.x - u0.x)) * r.ih1 + ((u0.x - ul) - (u0.y - u0.x)) * r.ih2,
+            ((u0.y - um.y) - (un.y - u0.y)) * r.ih1 + ((u0.y - u0.x) - (ur - u0.y)) * r.ih2);
+}
+
+template <bool PUSH>
+__device__ __forceinline__ double2 ldx3(const KParams& k, const M3Ctx& c, int t, unsigned o, unsigned ob) {
+  if constexpr (PUSH) {
+    if ((t < 1 && k.has[LEFT]) || (t > c.nx && k.has[RIGHT])) {
+      const double* h = c.hrd + int64_t(t < 1 ? t + H3 - 1 : t - c.nx + H3 - 1) * c.pitch + o;
+      return dd(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
+                __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+    }
+  }
+  return ld2(reinterpret_cast<const double*>(reinterpret_cast<const char*>(c.Xm + int64_t(t) * c.pitch) + ob));
+}
+
+// rows 1..6 → the LEFT neighbour's rows nx'+1..nx'+6; nx-5..nx → the RIGHT one's -5..0
+__device__ __forceinline__ void push_row3(const KParams& k, const M3Ctx& c, M3Rings& x, int q, const double2& r3,
+                                          const double2& p3) {
+  auto put = [&](double* base, int slot) {
+    double* d = base + int64_t(slot) * c.pitch + c.off;
+    if (c.o0) {
+      __hip_atomic_store(d, r3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d + c.poff, p3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    if (c.o1) {
+      __hip_atomic_store(d + 1, r3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d + 1 + c.poff, p3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+    x.pushed = true;
+  };
+  if (q <= H3 && k.hpush_lo[c.par] != nullptr) put(k.hpush_lo[c.par], q - 1);
+  if (q >= c.nx - H3 + 1 && k.hpush_hi[c.par] != nullptr) put(k.hpush_hi[c.par], q - (c.nx - H3 + 1));
+}
+
+// 16-byte store of the lane's two output columns (o0, o1: owned).
+template <bool EDGE>
+__device__ __forceinline__ void store2(const M3Ctx& c, double* p, const double2& v) {
+  if constexpr (!EDGE) {
+    if (c.o0) st2nt(p, v);  // (o1 == o0 away from the last strip)
+  } else {
+    if (c.o0 && c.o1) st2nt(p, v);
+    else if (c.o0) p[0] = v.x;
+  }
+}
+
+// One row step of the march: stage A at row t = t0 + n, B..G at rows
+// t-1..t-6.  JJ = n mod 6 fixes the register ring slots at compile time; bs
+// is the band face-ring slot of row t.  STEADY (uniform items): every stage
+// row lies inside the item — no row tests, no clamped loads.
+template <int KIND, bool PUSH, bool EDGE, bool STEADY, int JJ>
+__device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings& x, const RowCtx& rx, WaveTV3& tvw,
+                                      double (&sv)[NS], int n, int bs) {
+  constexpr bool BAND = KIND == kBand, UNI = KIND == kUniform;
+  constexpr int XD = kS3XD, WD = kS3WD;
+  // register ring slots: row t-d ↦ (JJ - d) mod 3 / mod 2
+  constexpr int m0 = JJ % 3, m1 = (JJ + 2) % 3, m2 = (JJ + 1) % 3;  // rows t, t-1, t-2 (t-3 ≡ t)
+  constexpr int e0 = JJ & 1, e1 = (JJ + 1) & 1;                      // rows t, t-1 (t-2 ≡ t)
+  constexpr int xs = JJ % XD, ws = JJ % WD;
+  const int t = c.t0 + n;
+  const int jl = c.jl, c0 = c.c0;
+  // row inside the item (steady: always — tested as "not a fix-up launch",
+  // which skips the sums there: the uniform branch keeps the compiler from
+  // interleaving the stages' sums, which costs ~200 VGPRs)
+  auto inr = [&](int q) { return STEADY ? !c.fix : (q >= c.ib && q <= c.ie); };
+  auto own = [&](int q) { return STEADY || (q >= c.ib && q <= c.ie); };  // (stores)
+  auto interior = [&](int q) { return q >= c.rlo && q <= c.rhi; };  // global interior row
+  // band ring slots (runtime, mod 7) of rows t .. t-6
+  int bsl[7];
+#pragma unroll
+  for (int d = 0; d < 7; ++d) bsl[d] = bs >= d ? bs - d : bs - d + kRing3;
+  // masked products z = D⁻¹·v (0 at global-boundary rows / columns)
+  auto zmask = [&](int q, const double2& v, const double2& d) -> double2 {
+    if constexpr (UNI) {  // d: the row scalar (interior rows folded in)
+      double2 z = dd(v.x * d.x, v.y * d.x);
+      if constexpr (EDGE) z = dd(z.x * c.lf0, z.y * c.lf1);
+      return z;
+    } else {
+      const bool rr = interior(q);
+      return dd((rr && c.lv0) ? v.x * d.x : 0.0, (rr && c.lv1) ? v.y * d.y : 0.0);
+    }
+  };
+  // the operator at row q (band ring slots sl, sln) and 1/D of the row
+  auto op = [&](int q, int sl, int sln, const double2& um, const double2& u0, const double2& un, double2& d) {
+    if constexpr (UNI) {
+      const URow r = urow<STEADY>(k, c, rx, q);
+      d = dd(r.d, r.d);
+      return lapu(r, um, u0, un);
+    } else {
+      return apply_row<BAND>(k, rx, tvw, q, c0, jl, sl, sln, um, u0, un, d);
+    }
+  };
+  // ---- A: row t ----
+  const double2 rin = x.RQ[xs], pin = x.PQ[xs], wrow = x.WQ[ws];
+  {
+    const int tn = STEADY ? t + XD : min(t + XD, c.tmax);
+    x.RQ[xs] = ldx3<PUSH>(k, c, tn, c.off, c.offb);
+    x.PQ[xs] = ldx3<PUSH>(k, c, tn, unsigned(c.poff) + c.off, c.offpb);
+    const int wr = STEADY ? t - 2 + WD : min(max(t - 2 + WD, c.ib), c.ie);
+    x.WQ[ws] = ldnt(reinterpret_cast<const double*>(reinterpret_cast<const char*>(c.Wm + int64_t(wr) * c.wp) + c.offwb));
+  }
+  {
+    double2 d;
+    if constexpr (UNI) {
+      const URow r = urow<STEADY>(k, c, rx, t);
+      d = dd(r.d, r.d);
+    } else {
+      d = BAND ? enter_band(k, rx, tvw, t, c0, jl, bsl[0]) : dinv_plain(k, rx, t, c0);
+    }
+    const double2 z = zmask(t, rin, d);
+    x.P1[m0] = dd(c.zc1 * z.x + c.b1 * pin.x, c.zc1 * z.y + c.b1 * pin.y);
+    x.RI[e0] = rin;
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);  // (stage by stage, as the row tests of the generic steps)
+  // ---- B: row t-1 ----
+  {
+    const int q = t - 1;
+    double2 d;
+    const double2 s1 = op(q, bsl[1], bsl[0], x.P1[m2], x.P1[m1], x.P1[m0], d);
+    const double2 ri = x.RI[e1];
+    const double2 r1 = dd(ri.x - c.a1 * s1.x, ri.y - c.a1 * s1.y);
+    const double2 z = zmask(q, r1, d);
+    const double2 p1 = x.P1[m1];
+    x.R1[e1] = r1;
+    x.P2[m1] = dd(c.zc2 * z.x + c.b2 * p1.x, c.zc2 * z.y + c.b2 * p1.y);
+    if (inr(q)) sv[16] += dot2(p1, p1);
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);
+  // ---- C: row t-2 (w) ----
+  {
+    const int q = t - 2;
+    double2 d;
+    const double2 s2 = op(q, bsl[2], bsl[1], x.P2[m0], x.P2[m2], x.P2[m1], d);
+    const double2 r1 = x.R1[e0];
+    const double2 r2 = dd(r1.x - c.a2 * s2.x, r1.y - c.a2 * s2.y);
+    const double2 z = zmask(q, r2, d);
+    const double2 p2 = x.P2[m2];
+    x.R2[e0] = r2;
+    const double2 p3 = dd(c.zc3 * z.x + c.b3 * p2.x, c.zc3 * z.y + c.b3 * p2.y);
+    x.P3[m2] = p3;
+    if (own(q)) {
+      const double2 p1 = x.P1[m2];
+      const double2 wv = dd(wrow.x + c.w1 * p1.x + c.w2 * p2.x + c.w3 * p3.x,
+                            wrow.y + c.w1 * p1.y + c.w2 * p2.y + c.w3 * p3.y);
+      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(reinterpret_cast<char*>(c.Wm + int64_t(q) * c.wp) + c.offwb), wv);
+    }
+    if (inr(q)) sv[17] += dot2(p2, p2);
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);
+  // ---- D: row t-3 (r, p outputs) ----
+  {
+    const int q = t - 3;
+    double2 d;
+    const double2 s3 = op(q, bsl[3], bsl[2], x.P3[m1], x.P3[m0], x.P3[m2], d);
+    const double2 r2 = x.R2[e1];
+    const double2 r3 = dd(r2.x - c.a3 * s3.x, r2.y - c.a3 * s3.y);
+    const double2 z = zmask(q, r3, d);
+    x.Z[m0] = z;
+    x.S[e1] = s3;
+    const double2 p3 = x.P3[m0];
+    if (own(q) && !c.fix) {
+      char* yr = reinterpret_cast<char*>(c.Ym + int64_t(q) * c.pitch);
+      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(yr + c.offb), r3);
+      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(yr + c.offpb), p3);
+      if constexpr (PUSH) push_row3(k, c, x, q, r3, p3);
+    }
+    if (inr(q)) {
+      sv[0] += dot2(r3, z);    // (r,z)
+      sv[6] += dot2(z, s3);    // (z,s)
+      sv[11] += dot2(p3, s3);  // (p,s)
+      sv[18] += dot2(p3, p3);  // ‖p₃‖²
+    }
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);
+  // ---- E: row t-4 ----
+  {
+    const int q = t - 4;
+    double2 d;
+    const double2 qv = op(q, bsl[4], bsl[3], x.Z[m2], x.Z[m1], x.Z[m0], d);
+    const double2 sr = x.S[e0];
+    const double2 u = zmask(q, qv, d);
+    const double2 v = zmask(q, sr, d);
+    x.U[m1] = u;
+    x.V[m1] = v;
+    if (inr(q)) {
+      sv[1] += dot2(x.Z[m1], qv);  // (z,q)
+      sv[2] += dot2(qv, u);        // (q,u)
+      sv[7] += dot2(qv, v);        // (q,v)
+      sv[12] += dot2(sr, v);       // (s,v)
+    }
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);
+  // ---- F: row t-5 ----
+  {
+    const int q = t - 5;
+    double2 d;
+    const double2 au = op(q, bsl[5], bsl[4], x.U[m0], x.U[m2], x.U[m1], d);
+    double2 d2;
+    const double2 av = op(q, bsl[5], bsl[4], x.V[m0], x.V[m2], x.V[m1], d2);
+    const double2 uu = zmask(q, au, d);
+    const double2 vv = zmask(q, av, d);
+    x.UU[m2] = uu;
+    x.VV[m2] = vv;
+    if (inr(q)) {
+      const double2 u = x.U[m2], v = x.V[m2];
+      sv[3] += dot2(u, au);    // (u,Au)
+      sv[8] += dot2(u, av);    // (u,Av)
+      sv[13] += dot2(v, av);   // (v,Av)
+      sv[4] += dot2(au, uu);   // (Au,ũ)
+      sv[9] += dot2(au, vv);   // (Au,ṽ)
+      sv[14] += dot2(av, vv);  // (Av,ṽ)
+    }
+  }
+  if (STEADY) __builtin_amdgcn_sched_barrier(0);
+  // ---- G: row t-6 ----
+  {
+    const int q = t - 6;
+    if (inr(q)) {
+      double2 d;
+      const double2 auu = op(q, bsl[6], bsl[5], x.UU[m1], x.UU[m0], x.UU[m2], d);
+      const double2 avv = op(q, bsl[6], bsl[5], x.VV[m1], x.VV[m0], x.VV[m2], d);
+      const double2 uu = x.UU[m0], vv = x.VV[m0];
+      sv[5] += dot2(uu, auu);   // (ũ,Aũ)
+      sv[10] += dot2(uu, avv);  // (ũ,Aṽ)
+      sv[15] += dot2(vv, avv);  // (ṽ,Aṽ)
+    }
+  }
+}
+
+// Six row steps (one period of the register rings).  Generic groups stop at
+// the item's last step.  Steady groups are straight-line code: a scheduling
+// barrier after each step keeps the scheduler from hoisting later steps'
+// work (it otherwise fills all 512 registers and spills).
+template <int KIND, bool PUSH, bool EDGE, bool STEADY>
+__device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings& x, const RowCtx& rx, WaveTV3& tvw,
+                                       double (&sv)[NS], int n0, int nsteps, int& bs) {
+  auto adv = [&]() { bs = bs == kRing3 - 1 ? 0 : bs + 1; };
+#define PE_STEP3(JJ)                                                              \
+  if (STEADY || n0 + JJ < nsteps) {                                               \
+    step3<KIND, PUSH, EDGE, STEADY, JJ>(k, c, x, rx, tvw, sv, n0 + JJ, bs);       \
+    adv();                                                                        \
+    if (STEADY) __builtin_amdgcn_sched_barrier(0);                                \
+  }
+  PE_STEP3(0)
+  PE_STEP3(1)
+  PE_STEP3(2)
+  PE_STEP3(3)
+  PE_STEP3(4)
+  PE_STEP3(5)
+#undef PE_STEP3
 }
 
 // The item march (one strip × rows ib..ie), accumulating this wave's sums.
@@ -258,247 +570,116 @@ __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, 
 // sum has a factor among z, p, u, v, ũ, ṽ, which are exactly 0 at the
 // global-boundary and padding columns, and the lanes that do not own their
 // columns (0..2, 61..63) are dropped once, at the end of the sweep.
-template <bool BAND, bool PUSH>
+template <int KIND, bool PUSH, bool EDGE>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
                                        WaveTV3& tvw, double (&sv)[NS]) {
   const int lane = threadIdx.x & 63;
   const int ny = int(k.ny);
-  const int64_t pitch = k.pitch, poff = k.poff, wp = k.wpitch;
-  const double* __restrict__ Xm = k.x[par ^ 1] - (H3 - 1);  // row pointers at column -5
-  double* __restrict__ Ym = k.x[par] - (H3 - 1);
-  double* __restrict__ Wm = k.w - (H3 - 1);
-  const int J = -(H3 - 1) + s * FSW3;
-  const int c0 = J + 2 * lane;
-  const int jl = 2 * lane;
-  const unsigned off = unsigned(c0 + H3 - 1);
-  const int64_t g0 = k.gj0 + c0;
-  const bool lv0 = c0 <= ny + H3 && g0 >= 1 && g0 <= k.N - 1;
-  const bool lv1 = c0 + 1 <= ny + H3 && g0 + 1 >= 1 && g0 + 1 <= k.N - 1;
+  M3Ctx c;
+  c.pitch = k.pitch;
+  c.poff = k.poff;
+  c.wp = k.wpitch;
+  c.Xm = k.x[par ^ 1] - (H3 - 1);  // row pointers at column -5
+  c.Ym = k.x[par] - (H3 - 1);
+  c.Wm = k.w - (H3 - 1);
+  c.J = -(H3 - 1) + s * FSW3;
+  c.c0 = c.J + 2 * lane;
+  c.jl = 2 * lane;
+  c.off = unsigned(c.c0 + H3 - 1);
+  const int64_t g0 = k.gj0 + c.c0;
+  c.lv0 = c.c0 <= ny + H3 && g0 >= 1 && g0 <= k.N - 1;
+  c.lv1 = c.c0 + 1 <= ny + H3 && g0 + 1 >= 1 && g0 + 1 <= k.N - 1;
+  c.lf0 = c.lv0 ? 1.0 : 0.0;
+  c.lf1 = c.lv1 ? 1.0 : 0.0;
   const bool inner = lane >= 3 && lane <= 60;
-  const bool o0 = inner && c0 >= 1 && c0 <= ny;
-  const bool o1 = inner && c0 + 1 >= 1 && c0 + 1 <= ny;
-  const double zc1 = cf.zc[0], zc2 = cf.zc[1], zc3 = cf.zc[2];
-  const double a1 = cf.a[0], a2 = cf.a[1], a3 = cf.a[2];
-  const double b1 = cf.b[0], b2 = cf.b[1], b3 = cf.b[2];
-  const double w1 = cf.cw[0], w2 = cf.cw[1], w3 = cf.cw[2];
+  c.o0 = inner && c.c0 >= 1 && c.c0 <= ny;
+  c.o1 = inner && c.c0 + 1 >= 1 && c.c0 + 1 <= ny;
+  c.fix = fix;
+  c.ib = ib;
+  c.ie = ie;
+  c.t0 = ib - H3;
+  c.tmax = ie + H3;
+  c.nx = int(k.nx);
+  c.par = par;
+  c.hrd = PUSH ? k.hrecv + int64_t(par ^ 1) * 2 * H3 * k.pitch : nullptr;
+  c.oih1 = uni(k.inv_eps * k.ih1sq);
+  c.oih2 = uni(k.inv_eps * k.ih2sq);
+  c.ih1 = k.ih1sq;
+  c.ih2 = k.ih2sq;
+  c.din = k.dinv_in;
+  c.dout = k.dinv_out;
+  c.rlo = int(max<int64_t>(1 - k.gi0, -(1 << 30)));
+  c.rhi = int(min<int64_t>(k.M - 1 - k.gi0, 1 << 30));
+  c.offb = c.off * 8u;
+  c.offpb = unsigned(c.off + k.poff) * 8u;
+  c.offwb = c.off * 8u;
+  // the 12 coefficients in VGPRs: the scalar file is the march's scarce one
+  // (row pointers, row scalars, loop state — spilled SGPRs cost a v_readlane
+  // per use), and a VGPR operand never hits the one-SGPR-per-VOP3 limit
+  c.zc1 = vreg(cf.zc[0]);
+  c.zc2 = vreg(cf.zc[1]);
+  c.zc3 = vreg(cf.zc[2]);
+  c.a1 = vreg(cf.a[0]);
+  c.a2 = vreg(cf.a[1]);
+  c.a3 = vreg(cf.a[2]);
+  c.b1 = vreg(cf.b[0]);
+  c.b2 = vreg(cf.b[1]);
+  c.b3 = vreg(cf.b[2]);
+  c.w1 = vreg(cf.cw[0]);
+  c.w2 = vreg(cf.cw[1]);
+  c.w3 = vreg(cf.cw[2]);
 
-  const int t0 = ib - H3;
   // Row classes / column tables of a 64-row window, reloaded every ~58 rows
   // on tall items (stage rows t-6 .. t and the column-table row t+1 inside).
   RowCtx rx;
-  auto load_seg = [&](int base) { load_rows<BAND>(k, rx, tvw, base, ie + H3 + 1, J); };
-  if (BAND) load_strip_tables(k, tvw, c0);
-  load_seg(t0);
-  auto interior = [&](int q) {  // global interior row
-    const int64_t gr = k.gi0 + q;
-    return gr >= 1 && gr <= k.M - 1;
-  };
-  const int nx = int(k.nx);
-  // receive buffer of the parity this sweep reads: [side][6 rows], rows from column -5
-  const double* hrd = PUSH ? k.hrecv + int64_t(par ^ 1) * 2 * H3 * pitch : nullptr;
-  auto ldx = [&](int t, unsigned o) -> double2 {
-    if constexpr (PUSH) {
-      if ((t < 1 && k.has[LEFT]) || (t > nx && k.has[RIGHT])) {
-        const double* h = hrd + int64_t(t < 1 ? t + H3 - 1 : t - nx + H3 - 1) * pitch + o;
-        return dd(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                  __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
-      }
-    }
-    return ld2(Xm + int64_t(t) * pitch + o);
-  };
-  bool pushed = false;
-  auto push_row = [&](int q, const double2& r3, const double2& p3) {
-    auto put = [&](double* base, int slot) {
-      double* d = base + int64_t(slot) * pitch + off;
-      if (o0) {
-        __hip_atomic_store(d, r3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(d + poff, p3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      if (o1) {
-        __hip_atomic_store(d + 1, r3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        __hip_atomic_store(d + 1 + poff, p3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      }
-      pushed = true;
-    };
-    // rows 1..6 → the LEFT neighbour's rows nx'+1..nx'+6; nx-5..nx → the RIGHT one's -5..0
-    if (q <= H3 && k.hpush_lo[par] != nullptr) put(k.hpush_lo[par], q - 1);
-    if (q >= nx - H3 + 1 && k.hpush_hi[par] != nullptr) put(k.hpush_hi[par], q - (nx - H3 + 1));
-  };
+  auto load_seg = [&](int base) { load_rows<KIND == kBand>(k, rx, tvw, base, ie + H3 + 1, c.J); };
+  if (KIND == kBand) load_strip_tables(k, tvw, c.c0);
+  load_seg(c.t0);
 
-  const int tmax = ie + H3;
-  // rows of loads in flight: x (r, p) XD, w WD (each 2 or 3: divides the unroll);
-  // w is consumed at stage C (row t-2)
+  M3Rings x;
+  x.pushed = false;
   constexpr int XD = kS3XD, WD = kS3WD;
-  double2 RQ[XD], PQ[XD], WQ[WD];
 #pragma unroll
   for (int q = 0; q < XD; ++q) {
-    const int t = min(t0 + q, tmax);
-    RQ[q] = ldx(t, off);
-    PQ[q] = ldx(t, poff + off);
+    const int t = min(c.t0 + q, c.tmax);
+    x.RQ[q] = ldx3<PUSH>(k, c, t, c.off, c.offb);
+    x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off, c.offpb);
   }
 #pragma unroll
-  for (int q = 0; q < WD; ++q) WQ[q] = ldnt(Wm + int64_t(min(max(t0 - 2 + q, ib), ie)) * wp + off);
-  double2 P1[3], RI[2], R1[2], P2[3], R2[2], P3[3], Z[3], S[2], U[3], V[3], UU[3], VV[3];
+  for (int q = 0; q < WD; ++q) x.WQ[q] = ldnt(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) P1[q] = P2[q] = P3[q] = Z[q] = U[q] = V[q] = UU[q] = VV[q] = dd(0.0, 0.0);
+  for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = dd(0.0, 0.0);
 #pragma unroll
-  for (int q = 0; q < 2; ++q) RI[q] = R1[q] = R2[q] = S[q] = dd(0.0, 0.0);
+  for (int q = 0; q < 2; ++q) x.RI[q] = x.R1[q] = x.R2[q] = x.S[q] = dd(0.0, 0.0);
 
-  const int nsteps = ie + H3 - t0 + 1;
+  const int nsteps = ie + H3 - c.t0 + 1;
+  const int rows = ie - ib + 1;
   int bs = 0;  // band ring slot of row t: (t - t0) mod 7
-  for (int g = 0; 6 * g < nsteps; ++g) {
-    if (t0 + 6 * g + 6 - rx.segbase > 63) load_seg(t0 + 6 * g - H3);  // tall items: next row window
-#pragma unroll
-    for (int jj = 0; jj < 6; ++jj) {
-      const int n = 6 * g + jj;
-      if (n >= nsteps) break;
-      const int t = t0 + n;
-      // register ring slots (compile-time): row t-d ↦ (jj - d) mod 3 / mod 2
-      const int m0 = jj % 3, m1 = (jj + 2) % 3, m2 = (jj + 1) % 3;  // rows t, t-1, t-2 (t-3 ≡ t)
-      const int e0 = jj & 1, e1 = (jj + 1) & 1;                      // rows t, t-1 (t-2 ≡ t)
-      // band ring slots (runtime, mod 7) of rows t .. t-6
-      int bsl[7];
-#pragma unroll
-      for (int d = 0; d < 7; ++d) bsl[d] = bs >= d ? bs - d : bs - d + kRing3;
-      // ---- A: row t ----
-      const int xs = jj % XD, ws = jj % WD;
-      const double2 rin = RQ[xs], pin = PQ[xs], wrow = WQ[ws];
-      {
-        const int tn = min(t + XD, tmax);
-        RQ[xs] = ldx(tn, off);
-        PQ[xs] = ldx(tn, poff + off);
-        WQ[ws] = ldnt(Wm + int64_t(min(max(t - 2 + WD, ib), ie)) * wp + off);
-      }
-      {
-        const double2 d = BAND ? enter_band(k, rx, tvw, t, c0, jl, bsl[0]) : dinv_plain(k, rx, t, c0);
-        const bool ri = interior(t);
-        const double z0 = (ri && lv0) ? rin.x * d.x : 0.0, z1 = (ri && lv1) ? rin.y * d.y : 0.0;
-        P1[m0] = dd(zc1 * z0 + b1 * pin.x, zc1 * z1 + b1 * pin.y);
-        RI[e0] = rin;
-      }
-      // ---- B: row t-1 ----
-      {
-        const int q = t - 1;
-        double2 d;
-        const double2 s1 = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[1], bsl[0], P1[m2], P1[m1], P1[m0], d);
-        const double2 ri = RI[e1];
-        const double2 r1 = dd(ri.x - a1 * s1.x, ri.y - a1 * s1.y);
-        const bool rr = interior(q);
-        const double z0 = (rr && lv0) ? r1.x * d.x : 0.0, z1 = (rr && lv1) ? r1.y * d.y : 0.0;
-        const double2 p1 = P1[m1];
-        R1[e1] = r1;
-        P2[m1] = dd(zc2 * z0 + b2 * p1.x, zc2 * z1 + b2 * p1.y);
-        if (q >= ib && q <= ie) sv[16] += dot2(p1, p1);
-      }
-      // ---- C: row t-2 (w) ----
-      {
-        const int q = t - 2;
-        double2 d;
-        const double2 s2 = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[2], bsl[1], P2[m0], P2[m2], P2[m1], d);
-        const double2 r1 = R1[e0];
-        const double2 r2 = dd(r1.x - a2 * s2.x, r1.y - a2 * s2.y);
-        const bool rr = interior(q);
-        const double z0 = (rr && lv0) ? r2.x * d.x : 0.0, z1 = (rr && lv1) ? r2.y * d.y : 0.0;
-        const double2 p2 = P2[m2];
-        R2[e0] = r2;
-        const double2 p3 = dd(zc3 * z0 + b3 * p2.x, zc3 * z1 + b3 * p2.y);
-        P3[m2] = p3;
-        if (q >= ib && q <= ie) {
-          const double2 p1 = P1[m2];
-          const double2 wv = dd(wrow.x + w1 * p1.x + w2 * p2.x + w3 * p3.x, wrow.y + w1 * p1.y + w2 * p2.y + w3 * p3.y);
-          double* wd = Wm + int64_t(q) * wp + off;
-          if (o0 && o1) st2nt(wd, wv);
-          else if (o0) wd[0] = wv.x;
-          sv[17] += dot2(p2, p2);
-        }
-      }
-      // ---- D: row t-3 (r, p outputs) ----
-      {
-        const int q = t - 3;
-        double2 d;
-        const double2 s3 = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[3], bsl[2], P3[m1], P3[m0], P3[m2], d);
-        const double2 r2 = R2[e1];
-        const double2 r3 = dd(r2.x - a3 * s3.x, r2.y - a3 * s3.y);
-        const bool rr = interior(q);
-        const double2 z = dd((rr && lv0) ? r3.x * d.x : 0.0, (rr && lv1) ? r3.y * d.y : 0.0);
-        Z[m0] = z;
-        S[e1] = s3;
-        if (q >= ib && q <= ie) {
-          const double2 p3 = P3[m0];
-          if (!fix) {
-            double* yr = Ym + int64_t(q) * pitch + off;
-            if (o0 && o1) {
-              st2nt(yr, r3);
-              st2nt(yr + poff, p3);
-            } else if (o0) {
-              yr[0] = r3.x;
-              yr[poff] = p3.x;
-            }
-            if constexpr (PUSH) push_row(q, r3, p3);
-          }
-          sv[0] += dot2(r3, z);   // (r,z)
-          sv[6] += dot2(z, s3);   // (z,s)
-          sv[11] += dot2(p3, s3); // (p,s)
-          sv[18] += dot2(p3, p3); // ‖p₃‖²
-        }
-      }
-      // ---- E: row t-4 ----
-      {
-        const int q = t - 4;
-        double2 d;
-        const double2 qv = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[4], bsl[3], Z[m2], Z[m1], Z[m0], d);
-        const bool rr = interior(q);
-        const double2 sr = S[e0];
-        const double2 u = dd((rr && lv0) ? qv.x * d.x : 0.0, (rr && lv1) ? qv.y * d.y : 0.0);
-        const double2 v = dd((rr && lv0) ? sr.x * d.x : 0.0, (rr && lv1) ? sr.y * d.y : 0.0);
-        U[m1] = u;
-        V[m1] = v;
-        if (q >= ib && q <= ie) {
-          sv[1] += dot2(Z[m1], qv); // (z,q)
-          sv[2] += dot2(qv, u);     // (q,u)
-          sv[7] += dot2(qv, v);     // (q,v)
-          sv[12] += dot2(sr, v);    // (s,v)
-        }
-      }
-      // ---- F: row t-5 ----
-      {
-        const int q = t - 5;
-        double2 d;
-        const double2 au = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[5], bsl[4], U[m0], U[m2], U[m1], d);
-        const double2 av = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[5], bsl[4], V[m0], V[m2], V[m1], d);
-        const bool rr = interior(q);
-        const double2 uu = dd((rr && lv0) ? au.x * d.x : 0.0, (rr && lv1) ? au.y * d.y : 0.0);
-        const double2 vv = dd((rr && lv0) ? av.x * d.x : 0.0, (rr && lv1) ? av.y * d.y : 0.0);
-        UU[m2] = uu;
-        VV[m2] = vv;
-        if (q >= ib && q <= ie) {
-          const double2 u = U[m2], v = V[m2];
-          sv[3] += dot2(u, au);    // (u,Au)
-          sv[8] += dot2(u, av);    // (u,Av)
-          sv[13] += dot2(v, av);   // (v,Av)
-          sv[4] += dot2(au, uu);   // (Au,ũ)
-          sv[9] += dot2(au, vv);   // (Au,ṽ)
-          sv[14] += dot2(av, vv);  // (Av,ṽ)
-        }
-      }
-      // ---- G: row t-6 ----
-      {
-        const int q = t - 6;
-        if (q >= ib && q <= ie) {
-          double2 d;
-          const double2 auu = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[6], bsl[5], UU[m1], UU[m0], UU[m2], d);
-          const double2 avv = apply_row<BAND>(k, rx, tvw, q, c0, jl, bsl[6], bsl[5], VV[m1], VV[m0], VV[m2], d);
-          const double2 uu = UU[m0], vv = VV[m0];
-          sv[5] += dot2(uu, auu);   // (ũ,Aũ)
-          sv[10] += dot2(uu, avv);  // (ũ,Aṽ)
-          sv[15] += dot2(vv, avv);  // (ṽ,Aṽ)
-        }
-      }
-      bs = bs == kRing3 - 1 ? 0 : bs + 1;
+  // steady groups (uniform items): stage rows t-6 .. t and the prefetched
+  // rows inside the item for all six steps (n ≥ 12, n ≤ rows + 4); the fill
+  // and drain groups around them test rows.  Three loops, not one with a
+  // branch: the merged ring state would cost a copy of every ring.
+  auto reload = [&](int n0) {
+    if (c.t0 + n0 + 6 - rx.segbase > 63) load_seg(c.t0 + n0 - H3);  // tall items: next row window
+  };
+  int n0 = 0;
+  const int nsteady_end = KIND == kUniform ? rows + 4 - 5 : -1;  // last steady group start
+  for (; n0 < nsteps && !(n0 >= 12 && n0 <= nsteady_end); n0 += 6) {
+    reload(n0);
+    group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+  }
+  if constexpr (KIND == kUniform) {
+    for (; n0 <= nsteady_end; n0 += 6) {
+      reload(n0);
+      group3<KIND, PUSH, EDGE, true>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+    }
+    for (; n0 < nsteps; n0 += 6) {
+      reload(n0);
+      group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
     }
   }
   if constexpr (PUSH) {
-    if (pushed) {  // delivered before this wave arrives anywhere
+    if (x.pushed) {  // delivered before this wave arrives anywhere
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -527,10 +708,20 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     const int2 e = cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
     if (rows == 0) continue;  // empty position of the static layout
-    const int s = e.y & 0xFFFFF, ib = e.x & kRowMask;
+    const int s = e.y & 0xFFFFF, ib = e.x & kRowMask3;
     const int ie = min(ib + rows - 1, int(k.nx));
-    if (e.x & kBandBit) march3<true, PUSH>(k, cf, fix, par, s, ib, ie, tv, acc);
-    else march3<false, PUSH>(k, cf, fix, par, s, ib, ie, tv, acc);
+    if (e.x & kBandBit) {
+      march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    } else if (e.x & kUniBit) {
+      // edge strips (a global-boundary or padding column in the window) mask z
+      const int c0 = -(H3 - 1) + s * FSW3 + 2 * int(threadIdx.x & 63);
+      const int64_t g0 = k.gj0 + c0;
+      const bool lv = c0 + 1 <= int(k.ny) + H3 && g0 >= 1 && g0 + 1 <= k.N - 1;
+      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false>(k, cf, fix, par, s, ib, ie, tv, acc);
+      else march3<kUniform, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    } else {
+      march3<kMixed, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    }
   }
 }
 

@@ -144,8 +144,27 @@ void DeviceSolver::setup_items() {
   };
   // {first row | band flag, strip | rows << 20}; the band flag selects the
   // kernel's coefficient path (rows ib-H .. ie+H include a boundary-band row)
+  // Three-step sweep: is every row of the item's window wholly interior or
+  // wholly non-interior in the strip's 128 columns (kUniBit: the kernel's
+  // uniform-row march)?  Rows with a band node are never uniform here: the
+  // band flag wins.
+  auto row_mixed = [&](int64_t q, int s) {
+    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
+    const int64_t t = q - tab_lo_;
+    if (t < 0 || t >= rows_tab) return true;
+    const int* r = &rowcls_host_[size_t(t) * 4];
+    const int64_t lo = std::max<int64_t>(J, r[0]), hi = std::min<int64_t>(J + 127, r[1]);
+    if (lo > hi) return false;                 // no interior column
+    return !(r[0] <= J && r[1] >= J + 127);    // some interior, some not
+  };
+  auto rows_uniform = [&](int64_t ib, int64_t ie, int s) {
+    for (int64_t q = ib - H; q <= ie + H; ++q)
+      if (row_gen(q, s) || row_mixed(q, s)) return false;
+    return true;
+  };
   auto entry = [&](int64_t ib, int64_t rows, int s) {
-    const int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
+    int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
+    if (flag == 0 && steps_ == 3 && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
   // outputs a neighbour needs: first in the layout under the overlap (they

@@ -198,6 +198,11 @@ constexpr int kTImax = 62;       // max rows per work item (rows ib-1..ie+1 live
 // (general march); clear → the plain unrolled march.
 constexpr int kBandBit = 1 << 30;
 constexpr int kRowMask = kBandBit - 1;
+// Three-step sweep only: kUniBit set when every row ib-6 .. ie+6 of the item
+// lies wholly inside or wholly outside the interior in its strip's window
+// (the kernel's uniform-row march: three scalars per row, no lane tests).
+constexpr int kUniBit = 1 << 29;
+constexpr int kRowMask3 = kUniBit - 1;
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
 constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
 constexpr int kNS2 = 20;         // two-step sweep: sums per sweep

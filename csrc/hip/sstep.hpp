@@ -32,6 +32,12 @@ __device__ __forceinline__ double uni(double x) {
   return __longlong_as_double((long long)((unsigned long long)hi << 32 | lo));
 }
 
+// A (uniform) value pinned to a VGPR from here on.
+__device__ __forceinline__ double vreg(double x) {
+  asm volatile("; vreg %0" : "+v"(x));
+  return x;
+}
+
 __device__ __forceinline__ void hist_put(const KParams& k, long long kiter, double d) {
   if (k.hist && kiter <= k.hist_n) k.hist[kiter - 1] = d;
 }
@@ -70,6 +76,7 @@ struct WaveTV {
 struct RowCtx {
   int2 rcv;      // interior interval of row segbase + lane (lane l ↔ row segbase + l)
   unsigned long long genmask;
+  unsigned long long allin;  // bit l: row segbase + l interior over the whole 128-column window
   int segbase;
 };
 
@@ -99,6 +106,7 @@ __device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw,
   const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
   rx.rcv = make_int2(rc4.x, rc4.y);
   rx.genmask = 0;
+  rx.allin = __ballot(lane < nr && rc4.x <= J && rc4.y >= J + 127);
   if (BAND) {
     rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
     if (rx.genmask != 0) {
