@@ -35,9 +35,13 @@
 // iterations (16 B / iteration, against 24 two-step and 40 single sweep) and
 // one 19-sum reduction per three iterations.
 //
-// Machine mapping (gfx950): fused2.hip's march with a 6-deep pipeline.  Each
-// wave64 strip loads 128 columns and outputs the middle 116 (lanes 3..60:
-// radius-6 dependence); rows march with seven stages in flight
+// Machine mapping (gfx950): fused2.hip's march with a 6-deep pipeline, ONE
+// column per lane: each wave64 strip loads 64 columns and outputs the middle
+// 52 (lanes 6..57: radius-6 dependence).  Two columns per lane (116 of 128)
+// needed ~380 VGPRs — one wave per SIMD, issue-bound at 53 % VALU and 3.3 TB/s
+// (8192²: 0.94 ms per sweep); one column halves the rings, so two waves share
+// a SIMD and hide each other's latencies.  Rows march with seven stages in
+// flight
 //   A  row t    p₁ = zc₁D⁻¹r + β₁p                          (loads of row t)
 //   B  row t−1  s₁ = Ap₁, r₁, z₁, p₂                         ‖p₁‖²
 //   C  row t−2  s₂ = Ap₂, r₂, z₂, p₃, w += Σ α_i p_i stored  ‖p₂‖²
@@ -65,7 +69,7 @@ namespace {
 
 constexpr int H3 = 6;
 constexpr int FSW3 = kFSW3;
-static_assert(FSW3 == 128 - 2 * H3, "three-step strip: 128 loaded columns, H3 halo columns per side");
+static_assert(FSW3 == 64 - 2 * H3, "three-step strip: 64 loaded columns (one per lane), H3 halo columns per side");
 #ifndef PE_S3_XD
 #define PE_S3_XD 3
 #endif
@@ -75,7 +79,7 @@ static_assert(FSW3 == 128 - 2 * H3, "three-step strip: 128 loaded columns, H3 ha
 constexpr int kS3XD = PE_S3_XD, kS3WD = PE_S3_WD;
 constexpr int NS = kNS3;
 constexpr int kRing3 = 7;  // band face ring: rows t-6 .. t
-using WaveTV3 = WaveTV<kRing3>;
+using WaveTV3 = WaveTV1<kRing3>;
 
 // Scalars of a sweep (iterations K+1 .. K+m).  Iteration i applies
 //   p_i = zc_i·z_{i-1} + β_i p_{i-1},  r_i = r_{i-1} − α_i A p_i
@@ -265,22 +269,21 @@ struct M3Ctx {
   double* Wm;         // w rows
   const double* hrd;  // PUSH: receive buffer of the parity this sweep reads
   int64_t pitch, poff, wp;
-  int J, c0, jl, ib, ie, t0, tmax, nx, par;
+  int J, c0, ib, ie, t0, tmax, nx, par;
   unsigned off;
-  bool lv0, lv1, o0, o1, fix;
-  double lf0, lf1;    // lv0 / lv1 as 1.0 / 0.0 (uniform items of the edge strips)
+  bool lv0, o0, fix;
+  double lf0;         // lv0 as 1.0 / 0.0 (uniform items of the edge strips)
   double oih1, oih2;  // inv_eps / h1², inv_eps / h2² (uniform exterior rows)
   double ih1, ih2, din, dout;  // 1/h1², 1/h2², 1/D interior / exterior (copies: a select between
                                // kernel-argument fields compiles to a scalar load per use)
   int rlo, rhi;       // local rows of the global interior: rlo ≤ q ≤ rhi
-  unsigned offb, offpb, offwb;  // lane byte offsets: r plane, p plane (x rows), w rows
   double zc1, zc2, zc3, a1, a2, a3, b1, b2, b3, w1, w2, w3;
 };
 
 // The march's register state: prefetch rings and the stage row rings.
 struct M3Rings {
-  double2 RQ[kS3XD], PQ[kS3XD], WQ[kS3WD];
-  double2 P1[3], RI[2], R1[2], P2[3], R2[2], P3[3], Z[3], S[2], U[3], V[3], UU[3], VV[3];
+  double RQ[kS3XD], PQ[kS3XD], WQ[kS3WD];
+  double P1[3], RI[2], R1[2], P2[3], R2[2], P3[3], Z[3], S[2], U[3], V[3], UU[3], VV[3];
   bool pushed;
 };
 
@@ -291,7 +294,7 @@ struct URow {
 };
 
 template <bool STEADY>
-__device__ __forceinline__ URow urow(const KParams& k, const M3Ctx& c, const RowCtx& rx, int q) {
+__device__ __forceinline__ URow urow(const M3Ctx& c, const RowCtx& rx, int q) {
   const int l = (q - rx.segbase) & 63;
   const bool in = (rx.allin >> l) & 1ull;
   URow r;
@@ -304,53 +307,38 @@ __device__ __forceinline__ URow urow(const KParams& k, const M3Ctx& c, const Row
   return r;
 }
 
-// The 5-point operator of a uniform row on the lane's two columns.
-__device__ __forceinline__ double2 lapu(const URow& r, const double2& um, const double2& u0, const double2& un) {
-  const double ul = dpp_shr1(u0.y), ur = dpp_shl1(u0.x);
-  return dd(((u0.x - um.x) - (un.x - u0.x)) * r.ih1 + ((u0.x - ul) - (u0.y - u0.x)) * r.ih2,
-            ((u0.y - um.y) - (un.y - u0.y)) * r.ih1 + ((u0.y - u0.x) - (ur - u0.y)) * r.ih2);
+// The 5-point operator of a uniform row on the lane's column.
+__device__ __forceinline__ double lapu(const URow& r, double um, double u0, double un) {
+  const double ul = dpp_shr1(u0), ur = dpp_shl1(u0);
+  return ((u0 - um) - (un - u0)) * r.ih1 + ((u0 - ul) - (ur - u0)) * r.ih2;
 }
 
 template <bool PUSH>
-__device__ __forceinline__ double2 ldx3(const KParams& k, const M3Ctx& c, int t, unsigned o, unsigned ob) {
+__device__ __forceinline__ double ldx3(const KParams& k, const M3Ctx& c, int t, unsigned o) {
   if constexpr (PUSH) {
     if ((t < 1 && k.has[LEFT]) || (t > c.nx && k.has[RIGHT])) {
       const double* h = c.hrd + int64_t(t < 1 ? t + H3 - 1 : t - c.nx + H3 - 1) * c.pitch + o;
-      return dd(__hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM),
-                __hip_atomic_load(h + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM));
+      return __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
-  return ld2(reinterpret_cast<const double*>(reinterpret_cast<const char*>(c.Xm + int64_t(t) * c.pitch) + ob));
+  return c.Xm[int64_t(t) * c.pitch + o];
 }
 
+__device__ __forceinline__ double ldnt1(const double* p) { return __builtin_nontemporal_load(p); }
+__device__ __forceinline__ void stnt1(double* p, double v) { __builtin_nontemporal_store(v, p); }
+
 // rows 1..6 → the LEFT neighbour's rows nx'+1..nx'+6; nx-5..nx → the RIGHT one's -5..0
-__device__ __forceinline__ void push_row3(const KParams& k, const M3Ctx& c, M3Rings& x, int q, const double2& r3,
-                                          const double2& p3) {
+__device__ __forceinline__ void push_row3(const KParams& k, const M3Ctx& c, M3Rings& x, int q, double r3, double p3) {
   auto put = [&](double* base, int slot) {
     double* d = base + int64_t(slot) * c.pitch + c.off;
     if (c.o0) {
-      __hip_atomic_store(d, r3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(d + c.poff, p3.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-    if (c.o1) {
-      __hip_atomic_store(d + 1, r3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-      __hip_atomic_store(d + 1 + c.poff, p3.y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d, r3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      __hip_atomic_store(d + c.poff, p3, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
     x.pushed = true;
   };
   if (q <= H3 && k.hpush_lo[c.par] != nullptr) put(k.hpush_lo[c.par], q - 1);
   if (q >= c.nx - H3 + 1 && k.hpush_hi[c.par] != nullptr) put(k.hpush_hi[c.par], q - (c.nx - H3 + 1));
-}
-
-// 16-byte store of the lane's two output columns (o0, o1: owned).
-template <bool EDGE>
-__device__ __forceinline__ void store2(const M3Ctx& c, double* p, const double2& v) {
-  if constexpr (!EDGE) {
-    if (c.o0) st2nt(p, v);  // (o1 == o0 away from the last strip)
-  } else {
-    if (c.o0 && c.o1) st2nt(p, v);
-    else if (c.o0) p[0] = v.x;
-  }
 }
 
 // One row step of the march: stage A at row t = t0 + n, B..G at rows
@@ -362,162 +350,149 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
                                       double (&sv)[NS], int n, int bs) {
   constexpr bool BAND = KIND == kBand, UNI = KIND == kUniform;
   constexpr int XD = kS3XD, WD = kS3WD;
+  const double zc1 = c.zc1, zc2 = c.zc2, zc3 = c.zc3, w1 = c.w1, w2 = c.w2, w3 = c.w3;
   // register ring slots: row t-d ↦ (JJ - d) mod 3 / mod 2
   constexpr int m0 = JJ % 3, m1 = (JJ + 2) % 3, m2 = (JJ + 1) % 3;  // rows t, t-1, t-2 (t-3 ≡ t)
   constexpr int e0 = JJ & 1, e1 = (JJ + 1) & 1;                      // rows t, t-1 (t-2 ≡ t)
   constexpr int xs = JJ % XD, ws = JJ % WD;
   const int t = c.t0 + n;
-  const int jl = c.jl, c0 = c.c0;
+  const int c0 = c.c0;
   // row inside the item (steady: always — tested as "not a fix-up launch",
   // which skips the sums there: the uniform branch keeps the compiler from
   // interleaving the stages' sums, which costs ~200 VGPRs)
   auto inr = [&](int q) { return STEADY ? !c.fix : (q >= c.ib && q <= c.ie); };
   auto own = [&](int q) { return STEADY || (q >= c.ib && q <= c.ie); };  // (stores)
-  auto interior = [&](int q) { return q >= c.rlo && q <= c.rhi; };  // global interior row
+  auto interior = [&](int q) { return q >= c.rlo && q <= c.rhi; };     // global interior row
   // band ring slots (runtime, mod 7) of rows t .. t-6
   int bsl[7];
 #pragma unroll
   for (int d = 0; d < 7; ++d) bsl[d] = bs >= d ? bs - d : bs - d + kRing3;
   // masked products z = D⁻¹·v (0 at global-boundary rows / columns)
-  auto zmask = [&](int q, const double2& v, const double2& d) -> double2 {
+  auto zmask = [&](int q, double v, double d) -> double {
     if constexpr (UNI) {  // d: the row scalar (interior rows folded in)
-      double2 z = dd(v.x * d.x, v.y * d.x);
-      if constexpr (EDGE) z = dd(z.x * c.lf0, z.y * c.lf1);
-      return z;
+      return EDGE ? (v * d) * c.lf0 : v * d;
     } else {
-      const bool rr = interior(q);
-      return dd((rr && c.lv0) ? v.x * d.x : 0.0, (rr && c.lv1) ? v.y * d.y : 0.0);
+      return (interior(q) && c.lv0) ? v * d : 0.0;
     }
   };
-  // the operator at row q (band ring slots sl, sln) and 1/D of the row
-  auto op = [&](int q, int sl, int sln, const double2& um, const double2& u0, const double2& un, double2& d) {
+  // the operator at row q (band ring slots sl, sln) and 1/D of the node
+  auto op = [&](int q, int sl, int sln, double um, double u0, double un, double& d) {
     if constexpr (UNI) {
-      const URow r = urow<STEADY>(k, c, rx, q);
-      d = dd(r.d, r.d);
+      const URow r = urow<STEADY>(c, rx, q);
+      d = r.d;
       return lapu(r, um, u0, un);
     } else {
-      return apply_row<BAND>(k, rx, tvw, q, c0, jl, sl, sln, um, u0, un, d);
+      return apply_row1<BAND>(k, rx, tvw, q, c0, sl, sln, um, u0, un, d);
     }
   };
   // ---- A: row t ----
-  const double2 rin = x.RQ[xs], pin = x.PQ[xs], wrow = x.WQ[ws];
+  const double rin = x.RQ[xs], pin = x.PQ[xs], wrow = x.WQ[ws];
   {
     const int tn = STEADY ? t + XD : min(t + XD, c.tmax);
-    x.RQ[xs] = ldx3<PUSH>(k, c, tn, c.off, c.offb);
-    x.PQ[xs] = ldx3<PUSH>(k, c, tn, unsigned(c.poff) + c.off, c.offpb);
+    x.RQ[xs] = ldx3<PUSH>(k, c, tn, c.off);
+    x.PQ[xs] = ldx3<PUSH>(k, c, tn, unsigned(c.poff) + c.off);
     const int wr = STEADY ? t - 2 + WD : min(max(t - 2 + WD, c.ib), c.ie);
-    x.WQ[ws] = ldnt(reinterpret_cast<const double*>(reinterpret_cast<const char*>(c.Wm + int64_t(wr) * c.wp) + c.offwb));
+    x.WQ[ws] = ldnt1(c.Wm + int64_t(wr) * c.wp + c.off);
   }
   {
-    double2 d;
-    if constexpr (UNI) {
-      const URow r = urow<STEADY>(k, c, rx, t);
-      d = dd(r.d, r.d);
-    } else {
-      d = BAND ? enter_band(k, rx, tvw, t, c0, jl, bsl[0]) : dinv_plain(k, rx, t, c0);
-    }
-    const double2 z = zmask(t, rin, d);
-    x.P1[m0] = dd(c.zc1 * z.x + c.b1 * pin.x, c.zc1 * z.y + c.b1 * pin.y);
+    double d;
+    if constexpr (UNI) d = urow<STEADY>(c, rx, t).d;
+    else d = BAND ? enter_band1(k, rx, tvw, t, c0, bsl[0]) : dinv_plain1(k, rx, t, c0);
+    const double z = zmask(t, rin, d);
+    x.P1[m0] = zc1 * z + c.b1 * pin;
     x.RI[e0] = rin;
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);  // (stage by stage, as the row tests of the generic steps)
   // ---- B: row t-1 ----
   {
     const int q = t - 1;
-    double2 d;
-    const double2 s1 = op(q, bsl[1], bsl[0], x.P1[m2], x.P1[m1], x.P1[m0], d);
-    const double2 ri = x.RI[e1];
-    const double2 r1 = dd(ri.x - c.a1 * s1.x, ri.y - c.a1 * s1.y);
-    const double2 z = zmask(q, r1, d);
-    const double2 p1 = x.P1[m1];
+    double d;
+    const double s1 = op(q, bsl[1], bsl[0], x.P1[m2], x.P1[m1], x.P1[m0], d);
+    const double r1 = x.RI[e1] - c.a1 * s1;
+    const double z = zmask(q, r1, d);
+    const double p1 = x.P1[m1];
     x.R1[e1] = r1;
-    x.P2[m1] = dd(c.zc2 * z.x + c.b2 * p1.x, c.zc2 * z.y + c.b2 * p1.y);
-    if (inr(q)) sv[16] += dot2(p1, p1);
+    x.P2[m1] = zc2 * z + c.b2 * p1;
+    if (inr(q)) sv[16] += p1 * p1;
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- C: row t-2 (w) ----
   {
     const int q = t - 2;
-    double2 d;
-    const double2 s2 = op(q, bsl[2], bsl[1], x.P2[m0], x.P2[m2], x.P2[m1], d);
-    const double2 r1 = x.R1[e0];
-    const double2 r2 = dd(r1.x - c.a2 * s2.x, r1.y - c.a2 * s2.y);
-    const double2 z = zmask(q, r2, d);
-    const double2 p2 = x.P2[m2];
+    double d;
+    const double s2 = op(q, bsl[2], bsl[1], x.P2[m0], x.P2[m2], x.P2[m1], d);
+    const double r2 = x.R1[e0] - c.a2 * s2;
+    const double z = zmask(q, r2, d);
+    const double p2 = x.P2[m2];
     x.R2[e0] = r2;
-    const double2 p3 = dd(c.zc3 * z.x + c.b3 * p2.x, c.zc3 * z.y + c.b3 * p2.y);
+    const double p3 = zc3 * z + c.b3 * p2;
     x.P3[m2] = p3;
-    if (own(q)) {
-      const double2 p1 = x.P1[m2];
-      const double2 wv = dd(wrow.x + c.w1 * p1.x + c.w2 * p2.x + c.w3 * p3.x,
-                            wrow.y + c.w1 * p1.y + c.w2 * p2.y + c.w3 * p3.y);
-      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(reinterpret_cast<char*>(c.Wm + int64_t(q) * c.wp) + c.offwb), wv);
-    }
-    if (inr(q)) sv[17] += dot2(p2, p2);
+    if (own(q) && c.o0) stnt1(c.Wm + int64_t(q) * c.wp + c.off, wrow + w1 * x.P1[m2] + w2 * p2 + w3 * p3);
+    if (inr(q)) sv[17] += p2 * p2;
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- D: row t-3 (r, p outputs) ----
   {
     const int q = t - 3;
-    double2 d;
-    const double2 s3 = op(q, bsl[3], bsl[2], x.P3[m1], x.P3[m0], x.P3[m2], d);
-    const double2 r2 = x.R2[e1];
-    const double2 r3 = dd(r2.x - c.a3 * s3.x, r2.y - c.a3 * s3.y);
-    const double2 z = zmask(q, r3, d);
+    double d;
+    const double s3 = op(q, bsl[3], bsl[2], x.P3[m1], x.P3[m0], x.P3[m2], d);
+    const double r3 = x.R2[e1] - c.a3 * s3;
+    const double z = zmask(q, r3, d);
     x.Z[m0] = z;
     x.S[e1] = s3;
-    const double2 p3 = x.P3[m0];
+    const double p3 = x.P3[m0];
     if (own(q) && !c.fix) {
-      char* yr = reinterpret_cast<char*>(c.Ym + int64_t(q) * c.pitch);
-      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(yr + c.offb), r3);
-      store2<EDGE || !UNI>(c, reinterpret_cast<double*>(yr + c.offpb), p3);
+      if (c.o0) {
+        double* yr = c.Ym + int64_t(q) * c.pitch + c.off;
+        stnt1(yr, r3);
+        stnt1(yr + c.poff, p3);
+      }
       if constexpr (PUSH) push_row3(k, c, x, q, r3, p3);
     }
     if (inr(q)) {
-      sv[0] += dot2(r3, z);    // (r,z)
-      sv[6] += dot2(z, s3);    // (z,s)
-      sv[11] += dot2(p3, s3);  // (p,s)
-      sv[18] += dot2(p3, p3);  // ‖p₃‖²
+      sv[0] += r3 * z;    // (r,z)
+      sv[6] += z * s3;    // (z,s)
+      sv[11] += p3 * s3;  // (p,s)
+      sv[18] += p3 * p3;  // ‖p₃‖²
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- E: row t-4 ----
   {
     const int q = t - 4;
-    double2 d;
-    const double2 qv = op(q, bsl[4], bsl[3], x.Z[m2], x.Z[m1], x.Z[m0], d);
-    const double2 sr = x.S[e0];
-    const double2 u = zmask(q, qv, d);
-    const double2 v = zmask(q, sr, d);
+    double d;
+    const double qv = op(q, bsl[4], bsl[3], x.Z[m2], x.Z[m1], x.Z[m0], d);
+    const double sr = x.S[e0];
+    const double u = zmask(q, qv, d);
+    const double v = zmask(q, sr, d);
     x.U[m1] = u;
     x.V[m1] = v;
     if (inr(q)) {
-      sv[1] += dot2(x.Z[m1], qv);  // (z,q)
-      sv[2] += dot2(qv, u);        // (q,u)
-      sv[7] += dot2(qv, v);        // (q,v)
-      sv[12] += dot2(sr, v);       // (s,v)
+      sv[1] += x.Z[m1] * qv;  // (z,q)
+      sv[2] += qv * u;        // (q,u)
+      sv[7] += qv * v;        // (q,v)
+      sv[12] += sr * v;       // (s,v)
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- F: row t-5 ----
   {
     const int q = t - 5;
-    double2 d;
-    const double2 au = op(q, bsl[5], bsl[4], x.U[m0], x.U[m2], x.U[m1], d);
-    double2 d2;
-    const double2 av = op(q, bsl[5], bsl[4], x.V[m0], x.V[m2], x.V[m1], d2);
-    const double2 uu = zmask(q, au, d);
-    const double2 vv = zmask(q, av, d);
+    double d, d2;
+    const double au = op(q, bsl[5], bsl[4], x.U[m0], x.U[m2], x.U[m1], d);
+    const double av = op(q, bsl[5], bsl[4], x.V[m0], x.V[m2], x.V[m1], d2);
+    const double uu = zmask(q, au, d);
+    const double vv = zmask(q, av, d);
     x.UU[m2] = uu;
     x.VV[m2] = vv;
     if (inr(q)) {
-      const double2 u = x.U[m2], v = x.V[m2];
-      sv[3] += dot2(u, au);    // (u,Au)
-      sv[8] += dot2(u, av);    // (u,Av)
-      sv[13] += dot2(v, av);   // (v,Av)
-      sv[4] += dot2(au, uu);   // (Au,ũ)
-      sv[9] += dot2(au, vv);   // (Au,ṽ)
-      sv[14] += dot2(av, vv);  // (Av,ṽ)
+      const double u = x.U[m2], v = x.V[m2];
+      sv[3] += u * au;    // (u,Au)
+      sv[8] += u * av;    // (u,Av)
+      sv[13] += v * av;   // (v,Av)
+      sv[4] += au * uu;   // (Au,ũ)
+      sv[9] += au * vv;   // (Au,ṽ)
+      sv[14] += av * vv;  // (Av,ṽ)
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
@@ -525,13 +500,13 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   {
     const int q = t - 6;
     if (inr(q)) {
-      double2 d;
-      const double2 auu = op(q, bsl[6], bsl[5], x.UU[m1], x.UU[m0], x.UU[m2], d);
-      const double2 avv = op(q, bsl[6], bsl[5], x.VV[m1], x.VV[m0], x.VV[m2], d);
-      const double2 uu = x.UU[m0], vv = x.VV[m0];
-      sv[5] += dot2(uu, auu);   // (ũ,Aũ)
-      sv[10] += dot2(uu, avv);  // (ũ,Aṽ)
-      sv[15] += dot2(vv, avv);  // (ṽ,Aṽ)
+      double d;
+      const double auu = op(q, bsl[6], bsl[5], x.UU[m1], x.UU[m0], x.UU[m2], d);
+      const double avv = op(q, bsl[6], bsl[5], x.VV[m1], x.VV[m0], x.VV[m2], d);
+      const double uu = x.UU[m0], vv = x.VV[m0];
+      sv[5] += uu * auu;   // (ũ,Aũ)
+      sv[10] += uu * avv;  // (ũ,Aṽ)
+      sv[15] += vv * avv;  // (ṽ,Aṽ)
     }
   }
 }
@@ -539,7 +514,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
 // Six row steps (one period of the register rings).  Generic groups stop at
 // the item's last step.  Steady groups are straight-line code: a scheduling
 // barrier after each step keeps the scheduler from hoisting later steps'
-// work (it otherwise fills all 512 registers and spills).
+// work into this one.
 template <int KIND, bool PUSH, bool EDGE, bool STEADY>
 __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings& x, const RowCtx& rx, WaveTV3& tvw,
                                        double (&sv)[NS], int n0, int nsteps, int& bs) {
@@ -569,7 +544,7 @@ __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings
 // Sums are taken over the item's rows without per-term column masks: every
 // sum has a factor among z, p, u, v, ũ, ṽ, which are exactly 0 at the
 // global-boundary and padding columns, and the lanes that do not own their
-// columns (0..2, 61..63) are dropped once, at the end of the sweep.
+// columns (0..5, 58..63) are dropped once, at the end of the sweep.
 template <int KIND, bool PUSH, bool EDGE>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
                                        WaveTV3& tvw, double (&sv)[NS]) {
@@ -583,17 +558,12 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   c.Ym = k.x[par] - (H3 - 1);
   c.Wm = k.w - (H3 - 1);
   c.J = -(H3 - 1) + s * FSW3;
-  c.c0 = c.J + 2 * lane;
-  c.jl = 2 * lane;
+  c.c0 = c.J + lane;
   c.off = unsigned(c.c0 + H3 - 1);
   const int64_t g0 = k.gj0 + c.c0;
   c.lv0 = c.c0 <= ny + H3 && g0 >= 1 && g0 <= k.N - 1;
-  c.lv1 = c.c0 + 1 <= ny + H3 && g0 + 1 >= 1 && g0 + 1 <= k.N - 1;
   c.lf0 = c.lv0 ? 1.0 : 0.0;
-  c.lf1 = c.lv1 ? 1.0 : 0.0;
-  const bool inner = lane >= 3 && lane <= 60;
-  c.o0 = inner && c.c0 >= 1 && c.c0 <= ny;
-  c.o1 = inner && c.c0 + 1 >= 1 && c.c0 + 1 <= ny;
+  c.o0 = lane >= H3 && lane < 64 - H3 && c.c0 >= 1 && c.c0 <= ny;
   c.fix = fix;
   c.ib = ib;
   c.ie = ie;
@@ -610,30 +580,24 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   c.dout = k.dinv_out;
   c.rlo = int(max<int64_t>(1 - k.gi0, -(1 << 30)));
   c.rhi = int(min<int64_t>(k.M - 1 - k.gi0, 1 << 30));
-  c.offb = c.off * 8u;
-  c.offpb = unsigned(c.off + k.poff) * 8u;
-  c.offwb = c.off * 8u;
-  // the 12 coefficients in VGPRs: the scalar file is the march's scarce one
-  // (row pointers, row scalars, loop state — spilled SGPRs cost a v_readlane
-  // per use), and a VGPR operand never hits the one-SGPR-per-VOP3 limit
-  c.zc1 = vreg(cf.zc[0]);
-  c.zc2 = vreg(cf.zc[1]);
-  c.zc3 = vreg(cf.zc[2]);
-  c.a1 = vreg(cf.a[0]);
-  c.a2 = vreg(cf.a[1]);
-  c.a3 = vreg(cf.a[2]);
-  c.b1 = vreg(cf.b[0]);
-  c.b2 = vreg(cf.b[1]);
-  c.b3 = vreg(cf.b[2]);
-  c.w1 = vreg(cf.cw[0]);
-  c.w2 = vreg(cf.cw[1]);
-  c.w3 = vreg(cf.cw[2]);
+  c.zc1 = cf.zc[0];
+  c.zc2 = cf.zc[1];
+  c.zc3 = cf.zc[2];
+  c.a1 = cf.a[0];
+  c.a2 = cf.a[1];
+  c.a3 = cf.a[2];
+  c.b1 = cf.b[0];
+  c.b2 = cf.b[1];
+  c.b3 = cf.b[2];
+  c.w1 = cf.cw[0];
+  c.w2 = cf.cw[1];
+  c.w3 = cf.cw[2];
 
   // Row classes / column tables of a 64-row window, reloaded every ~58 rows
   // on tall items (stage rows t-6 .. t and the column-table row t+1 inside).
   RowCtx rx;
-  auto load_seg = [&](int base) { load_rows<KIND == kBand>(k, rx, tvw, base, ie + H3 + 1, c.J); };
-  if (KIND == kBand) load_strip_tables(k, tvw, c.c0);
+  auto load_seg = [&](int base) { load_rows<KIND == kBand, WaveTV3, 64>(k, rx, tvw, base, ie + H3 + 1, c.J); };
+  if (KIND == kBand) load_strip_tables1(k, tvw, c.c0);
   load_seg(c.t0);
 
   M3Rings x;
@@ -642,15 +606,15 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
 #pragma unroll
   for (int q = 0; q < XD; ++q) {
     const int t = min(c.t0 + q, c.tmax);
-    x.RQ[q] = ldx3<PUSH>(k, c, t, c.off, c.offb);
-    x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off, c.offpb);
+    x.RQ[q] = ldx3<PUSH>(k, c, t, c.off);
+    x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off);
   }
 #pragma unroll
-  for (int q = 0; q < WD; ++q) x.WQ[q] = ldnt(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off);
+  for (int q = 0; q < WD; ++q) x.WQ[q] = ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off);
 #pragma unroll
-  for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = dd(0.0, 0.0);
+  for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = 0.0;
 #pragma unroll
-  for (int q = 0; q < 2; ++q) x.RI[q] = x.R1[q] = x.R2[q] = x.S[q] = dd(0.0, 0.0);
+  for (int q = 0; q < 2; ++q) x.RI[q] = x.R1[q] = x.R2[q] = x.S[q] = 0.0;
 
   const int nsteps = ie + H3 - c.t0 + 1;
   const int rows = ie - ib + 1;
@@ -714,9 +678,9 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
       march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     } else if (e.x & kUniBit) {
       // edge strips (a global-boundary or padding column in the window) mask z
-      const int c0 = -(H3 - 1) + s * FSW3 + 2 * int(threadIdx.x & 63);
+      const int c0 = -(H3 - 1) + s * FSW3 + int(threadIdx.x & 63);
       const int64_t g0 = k.gj0 + c0;
-      const bool lv = c0 + 1 <= int(k.ny) + H3 && g0 >= 1 && g0 + 1 <= k.N - 1;
+      const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
       if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false>(k, cf, fix, par, s, ib, ie, tv, acc);
       else march3<kUniform, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     } else {
@@ -726,7 +690,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
 }
 
 template <bool PUSH>
-__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(1))) void kS3(KParams k, int par) {
+__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
   const int fix = st->fixpend;
@@ -765,8 +729,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(1))) void kS
   {  // band ring: defined contents (the never-written column 128 of b0 and the
      // slots garbage pipeline-fill rows read stay finite)
     WaveTV3& tv = tvs[wid];
-    for (int i = lane; i < kRing3 * 128; i += 64) (&tv.a0r[0][0])[i] = 0.0;
-    for (int i = lane; i < kRing3 * 130; i += 64) (&tv.b0r[0][0])[i] = 0.0;
+    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
+    for (int i = lane; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
   }
   walk3<PUSH>(k, cf, fix != 0, rpar, tvs[wid], wid, acc);
   if (fix) {  // fix-up launch: w only; the last wave clears the request
@@ -776,7 +740,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(1))) void kS
     }
     return;
   }
-  if (lane < 3 || lane > 60)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
+  if (lane < H3 || lane >= 64 - H3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
 #pragma unroll
     for (int n = 0; n < NS; ++n) acc[n] = 0.0;
   block_reduce<NS, false>(acc, sm);

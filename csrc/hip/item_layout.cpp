@@ -117,15 +117,16 @@ void DeviceSolver::setup_items() {
   const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
   // per-item cost: rows ib-2 .. ie+2, band rows weighted
   const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
-  // Does local row q have a boundary-band node in strip s's 128 loaded
+  // Does local row q have a boundary-band node in strip s's loaded
   // columns?  (The kernel's has_gen on the same row-class table.)
-  const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step)
+  const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step, 6 three-step)
+  const int64_t Wc = steps_ == 3 ? 64 : 128;  // columns a wave strip loads (three-step: one per lane)
   auto row_gen = [&](int64_t q, int s) {
     const int64_t J = -(H - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;  // table index of local row q
     if (t < 0 || t >= rows_tab) return false;
     const int* r = &rowcls_host_[size_t(t) * 4];
-    const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + 127, r[3]);
+    const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + Wc - 1, r[3]);
     return lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
   };
   auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
@@ -145,7 +146,7 @@ void DeviceSolver::setup_items() {
   // {first row | band flag, strip | rows << 20}; the band flag selects the
   // kernel's coefficient path (rows ib-H .. ie+H include a boundary-band row)
   // Three-step sweep: is every row of the item's window wholly interior or
-  // wholly non-interior in the strip's 128 columns (kUniBit: the kernel's
+  // wholly non-interior in the strip's 64 columns (kUniBit: the kernel's
   // uniform-row march)?  Rows with a band node are never uniform here: the
   // band flag wins.
   auto row_mixed = [&](int64_t q, int s) {
@@ -153,9 +154,9 @@ void DeviceSolver::setup_items() {
     const int64_t t = q - tab_lo_;
     if (t < 0 || t >= rows_tab) return true;
     const int* r = &rowcls_host_[size_t(t) * 4];
-    const int64_t lo = std::max<int64_t>(J, r[0]), hi = std::min<int64_t>(J + 127, r[1]);
+    const int64_t lo = std::max<int64_t>(J, r[0]), hi = std::min<int64_t>(J + Wc - 1, r[1]);
     if (lo > hi) return false;                 // no interior column
-    return !(r[0] <= J && r[1] >= J + 127);    // some interior, some not
+    return !(r[0] <= J && r[1] >= J + Wc - 1);  // some interior, some not
   };
   auto rows_uniform = [&](int64_t ib, int64_t ie, int s) {
     for (int64_t q = ib - H; q <= ie + H; ++q)

@@ -207,7 +207,7 @@ constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (
 constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
 constexpr int kNS2 = 20;         // two-step sweep: sums per sweep
 constexpr int kTImax2 = 48;      // two-step sweep: max rows per item (rows ib-4 .. ie+5 live one per lane)
-constexpr int kFSW3 = 116;       // three-step sweep: output columns per strip (6-column halo per side)
+constexpr int kFSW3 = 52;        // three-step sweep: output columns per 64-column strip (one per lane, 6-column halo per side)
 constexpr int kNS3 = 19;         // three-step sweep: sums per sweep
 constexpr int kTImax3 = 64;      // three-step sweep: max rows per item
 

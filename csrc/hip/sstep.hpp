@@ -96,9 +96,9 @@ __device__ __forceinline__ double lap(const KParams& k, double f, double pm, dou
 }
 
 // Row classes / column tables of rows base .. base+63 (one per lane) into the
-// lane registers (and, for band items with a boundary row in the window, the
+// lane registers (strip window: WIN columns from J) (and, for band items with a boundary row in the window, the
 // wave's LDS tables); rows past `last` get an empty interior interval.
-template <bool BAND, class WT>
+template <bool BAND, class WT, int WIN = 128>
 __device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw, int base, int last, int J) {
   const int lane = threadIdx.x & 63;
   rx.segbase = base;
@@ -106,9 +106,9 @@ __device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw,
   const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
   rx.rcv = make_int2(rc4.x, rc4.y);
   rx.genmask = 0;
-  rx.allin = __ballot(lane < nr && rc4.x <= J && rc4.y >= J + 127);
+  rx.allin = __ballot(lane < nr && rc4.x <= J && rc4.y >= J + WIN - 1);
   if (BAND) {
-    rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + 127));
+    rx.genmask = __ballot(lane < nr && has_gen(RowCls{rc4.x, rc4.y, rc4.z, rc4.w}, J, J + WIN - 1));
     if (rx.genmask != 0) {
       const double* ctr = k.colT + (min(base + lane, last) + 1) * 4;
       tvw.rc[lane] = rc4;
@@ -204,6 +204,88 @@ __device__ __forceinline__ double2 dinv_plain(const KParams& k, const RowCtx& rx
 }
 
 __device__ __forceinline__ double dot2(const double2& a, const double2& b) { return a.x * b.x + a.y * b.y; }
+
+// ---- one column per lane (fused3.hip: 64-column strips) ----------------
+template <int RING>
+struct WaveTV1 {
+  double sA[64], eA[64], hB[66];
+  int4 rc[64];
+  double half[65], sB[64], eB[64];
+  double a0r[RING][64];
+  double b0r[RING][66];  // (column 64: read by lane 63 for its b1, never written)
+};
+
+// The strip's row-table entries (per column), once per band item.
+template <class WT>
+__device__ __forceinline__ void load_strip_tables1(const KParams& k, WT& tvw, int c0) {
+  const int lane = threadIdx.x & 63;
+  const double* tb = k.rowT + (c0 + 1) * 4;
+  tvw.sA[lane] = tb[0];
+  tvw.eA[lane] = tb[1];
+  tvw.hB[lane] = tb[2];
+  if (lane == 63) tvw.hB[64] = tb[6];
+}
+
+__device__ __forceinline__ void row_in1(const RowCtx& rx, int q, int c0, bool& in0, bool& gen) {
+  const int l = (q - rx.segbase) & 63;
+  const int lo = __builtin_amdgcn_readlane(rx.rcv.x, l), hi = __builtin_amdgcn_readlane(rx.rcv.y, l);
+  in0 = c0 >= lo && c0 <= hi;
+  gen = (rx.genmask >> l) & 1ull;
+}
+
+// First stage of a band item: row q's faces into ring slot `sl`; returns 1/D.
+template <class WT>
+__device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx, WT& tv, int q, int c0, int sl) {
+  const int lane = threadIdx.x & 63;
+  bool in0, gen;
+  row_in1(rx, q, c0, in0, gen);
+  double d, a0, b0;
+  if (gen) {
+    const int l = (q - rx.segbase) & 63;
+    const int4 r4 = tv.rc[l];
+    const RowCls rc{r4.x, r4.y, r4.z, r4.w};
+    const CT ct{tv.half[l], tv.half[l + 1], tv.sB[l], tv.eB[l]};
+    const CS x0 = cset_rc(k, rc, ct, c0, TV{tv.sA[lane], tv.eA[lane], tv.hB[lane], tv.hB[lane + 1]});
+    d = x0.d;
+    a0 = x0.a0;
+    b0 = x0.b0;
+  } else {
+    d = in0 ? k.dinv_in : k.dinv_out;
+    a0 = b0 = in0 ? 1.0 : k.inv_eps;
+  }
+  tv.a0r[sl][lane] = a0;
+  tv.b0r[sl][lane] = b0;
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  return d;
+}
+
+// The 5-point operator at row q (ring slot sl, the row above it in slot sln)
+// for the lane's column; d = 1/D of the node.
+template <bool BAND, class WT>
+__device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx, const WT& tv, int q, int c0, int sl,
+                                             int sln, double um, double u0, double un, double& d) {
+  const int lane = threadIdx.x & 63;
+  const double ul = dpp_shr1(u0), ur = dpp_shl1(u0);
+  bool in0, gen;
+  row_in1(rx, q, c0, in0, gen);
+  if (BAND && gen) {
+    const double a0 = tv.a0r[sl][lane], a1 = tv.a0r[sln][lane];
+    const double b0 = tv.b0r[sl][lane], b1 = tv.b0r[sl][lane + 1];
+    const CS x0{a0, a1, b0, b1, dinv_faces(k, a0, a1, b0, b1)};
+    d = x0.d;
+    return stencil<false>(k, x0, um, u0, un, ul, ur);
+  }
+  d = in0 ? k.dinv_in : k.dinv_out;
+  return lap(k, in0 ? 1.0 : k.inv_eps, um, u0, un, ul, ur);
+}
+
+__device__ __forceinline__ double dinv_plain1(const KParams& k, const RowCtx& rx, int q, int c0) {
+  bool in0, gen;
+  row_in1(rx, q, c0, in0, gen);
+  return in0 ? k.dinv_in : k.dinv_out;
+}
 
 }  // namespace
 }  // namespace dev
