@@ -288,7 +288,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (fused_ && ti_env == 0) ti = huge ? 18 : big ? 24 : 10;
   k.order = (fused_ && huge) ? 3 : 0;
   if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
-    if (ti_env == 0) ti = steps_ == 3 ? (big ? 48 : 32) : (big ? 40 : 24);
+    if (ti_env == 0) ti = steps_ == 3 ? (big ? 80 : 48) : (big ? 40 : 24);
     ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
@@ -326,9 +326,12 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // best height moves with the block: 1600×2400 16 rows 39.9 µs/iter vs 47.7
   // at 40, 2048² 24 rows, 4096² 32 rows 102.3 vs 108.7; 8192² and 16384²
   // within ±2 % over 24-48 rows: fixed 40 — one placement per grid,
-  // tools/ti_probe.py, profiles/r3_ti_probe.txt).
+  // tools/ti_probe.py, profiles/r3_ti_probe.txt).  Three-step sweep (12
+  // pipeline-fill rows per item): among {32 .. 96} (2400×3200 32 rows 45.7
+  // µs/iter vs 57.1 at 64, 1600×2400 and 2048² 48, 4096² 64); fixed 80 above
+  // (8192² 247.9 vs 253.2 at 64 and 268.6 at 48 — profiles/r3_three_ti.txt).
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
-  static constexpr int kTiCands3[5] = {24, 32, 40, 48, 64};
+  static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
   if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
@@ -594,12 +597,13 @@ void DeviceSolver::setup_halo_push() {
 
 void DeviceSolver::relayout(int ti, int order) {
   if (!fused_ || resident_) return;
-  ti = std::max(2, std::min(ti, 64));
+  ti = std::max(2, std::min(ti, steps_ == 3 ? dev::kTImax3 : 64));
   const int ord = (order == 0 || order == 3) ? order : kp_->order;  // static LPT list / dynamic per-XCD queue
-  // the item-sum slots and the fold buffer were sized at construction: a
-  // layout that needs more is refused before anything changes
+  // the item-sum slots of the dynamic order and the fold buffer were sized at
+  // construction: a layout that needs more is refused before anything
+  // changes (the static layout sums per block, not per item: any height)
   const int64_t nitems = int64_t(kp_->nstrips) * ((blk_.nx + ti - 1) / ti);
-  const int64_t need = (ord == 0 ? ti + 1 : 2) * nitems + 64;
+  const int64_t need = ord == 0 ? 0 : 2 * nitems + 64;
   if (need > nslot_cap_ || (kp_->fold && ord != 3))
     throw std::invalid_argument("relayout: " + std::to_string(ti) + " rows per item (order " + std::to_string(ord) +
                                 ") needs " + std::to_string(need) + " item-sum slots, " + std::to_string(nslot_cap_) +

@@ -209,7 +209,7 @@ constexpr int kNS2 = 20;         // two-step sweep: sums per sweep
 constexpr int kTImax2 = 48;      // two-step sweep: max rows per item (rows ib-4 .. ie+5 live one per lane)
 constexpr int kFSW3 = 52;        // three-step sweep: output columns per 64-column strip (one per lane, 6-column halo per side)
 constexpr int kNS3 = 19;         // three-step sweep: sums per sweep
-constexpr int kTImax3 = 64;      // three-step sweep: max rows per item
+constexpr int kTImax3 = 128;     // three-step sweep: max rows per item (row windows reload every ~58 rows)
 
 // LDS-resident single sweep (resident.hip): small single-rank blocks run many
 // iterations in ONE launch.  The block is cut into tiles of one 124-column
