@@ -322,11 +322,33 @@ void DeviceSolver::setup_items() {
       lay_mean_ += l / W;
     }
     lay_items_ = int(rounds);
+    // XCD-aware placement of the lists: the persistent grid's workgroup b runs
+    // on XCD b mod 8 (round-robin dispatch), and each XCD has its own L2.
+    // Consecutive lists hold neighbouring strips of the same rows (chunk-major
+    // LPT order), whose halo columns overlap: list w goes to a physical wave
+    // of XCD ⌊8w/W⌋, so each XCD marches a contiguous run of strips and the
+    // overlapped lines are fetched once into its L2 instead of once per XCD.
+    // Measured SLOWER (three-step 8192²: 3759 / 3778 it/s vs 4023 / 4031 with
+    // list w on physical wave w, alternating runs on one box —
+    // profiles/r3_three_ti.txt): opt-in PE_XCD_MAP=1.
+    std::vector<int> phys(static_cast<size_t>(W));
+    {
+      const bool xmap = std::getenv("PE_XCD_MAP") && std::atoi(std::getenv("PE_XCD_MAP")) == 1;
+      const int nb = W / dev::kWPB;
+      size_t i = 0;
+      if (xmap) {
+        for (int x = 0; x < 8; ++x)
+          for (int b = x; b < nb; b += 8)
+            for (int l = 0; l < dev::kWPB; ++l) phys[i++] = b * dev::kWPB + l;
+      } else {
+        for (int w = 0; w < W; ++w) phys[i++] = w;
+      }
+    }
     std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)
     for (int w = 0; w < W; ++w)
       for (size_t r = 0; r < per[size_t(w)].size(); ++r) {
         const Piece& p = pcs[size_t(per[size_t(w)][r])];
-        all[r * size_t(W) + size_t(w)] = entry(p.ib, p.rows, p.s);
+        all[r * size_t(W) + size_t(phys[size_t(w)])] = entry(p.ib, p.rows, p.s);
       }
     static_waves_ = W;
     nslot_cap_ = std::max<int>(nslot_cap_, int(all.size()));
