@@ -67,7 +67,7 @@ py::dict state_dict(const dev::DevState& s) {
     f2.append(py::tuple(v));
   }
   d["fs2"] = py::tuple(f2);
-  d["fixpend"] = s.fixpend;
+  d["late3"] = s.late3;
   py::list c3;
   for (int n = 0; n < 12; ++n) c3.append(s.sc3[n]);
   d["sc3"] = py::tuple(c3);

@@ -1076,7 +1076,7 @@ void DeviceSolver::wait_event(hipEvent_t ev) {
 
 void DeviceSolver::enqueue_wflush() {
   if (!fused_) return;
-  if (steps_ == 3) {  // a three-step sweep that converged early: its w fix-up (no-op otherwise)
+  if (steps_ == 3) {  // the last sweep's pending stop tests (and its w fix-up when it converged early)
     KParams kk = *kp_;
     kk.mlimit = -1;
     dev::launch_S(kk, par_, stream_);

@@ -21,12 +21,14 @@
 //
 // (μ_0 of zp / pp never enters: z_{K+i} has p-components of degree ≥ 1.)
 // The stop test of iteration K+i, |α_i|‖p_i‖, uses ‖p_i‖² summed by the
-// sweep that forms p_i (sums 16..18) — "late": a sweep that converges on its
-// first or second iteration has already added the later α_j p_j to w, and
-// the next launch subtracts them again (fix-up mode: the same march over the
-// same inputs with the saved scalars, w -= α_j p_j only).  Breakdown (|den| <
-// 1e-15) and the iteration cap are known before the sweep: the sweep applies
-// only the iterations before them (an identity step is zc = 0, β = 1, α = 0).
+// sweep that forms p_i (sums 16..18) — "late": the NEXT launch decides it
+// (the sums are global only after the sweep's reduction), and when the sweep
+// converged on its first or second iteration, w already holds the later
+// α_j p_j: that launch subtracts them again (the same march over the same
+// inputs with the saved scalars, w -= α_j p_j only) instead of sweeping on.
+// Breakdown (|den| < 1e-15) and the iteration cap are known before the
+// sweep: it applies only the iterations before them (an identity step is
+// zc = 0, β = 1, α = 0).
 // So the iteration count and every terminal case keep the reference's
 // semantics (stage2-mpi/poisson_mpi_decomp.cpp:400-457); the moments are
 // summed in a different order, which is the only numerical difference.
@@ -181,19 +183,83 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
   return c;
 }
 
-// Iteration K+1 breaks down before its update: stop, w unchanged (one
-// thread, after every wave of the grid has read the state).
-__device__ __forceinline__ void sweep3_terminal(DevState* st, const Scal3& c) {
-  st->status = c.bad ? 4 : 2;
-  st->iter = c.K + 1;
+// Stop tests are resolved one launch late.  The ‖p_i‖² of a sweep's
+// iterations are among its own sums, which are global only after the
+// sweep's reduction — inside the sweep (one rank, or the in-sweep P2P sum)
+// or after it (the comm's allreduce of the sums) — so every launch first
+// decides, from the state alone (every wave gets the same bits), the stop
+// tests its predecessor left pending (DevState::late3 iterations ending at
+// st->iter, coefficients in sc3 = {zc, α, β, g}), then the breakdown / cap
+// that predecessor saw coming, and only then starts new iterations.  A
+// launch with mlimit < 0 (DeviceSolver::enqueue_wflush, after the host loop)
+// only resolves.
+struct Late3 {
+  int stop;    // 1..3: the pending iteration that stops the solve (0: none)
+  int status;  // its status: 1 converged, 4 non-finite ‖Δw‖
+};
+
+__device__ __forceinline__ double late_diff(const KParams& k, const DevState* st, int i) {
+  const double n2 = fmax(st->fs2[st->wpar][16 + i], 0.0), a = st->sc3[3 + i];
+  const double hh = k.h1 * k.h2;
+  return k.weighted ? fabs(a) * sqrt(n2 * hh) : fabs(a) * sqrt(n2);
+}
+
+__device__ __forceinline__ Late3 late3_test(const KParams& k, const DevState* st) {
+  Late3 r{0, 0};
+  const int m = st->late3;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (r.stop == 0 && i < m) {
+      const double d = late_diff(k, st, i);
+      if (!isfinite(d)) {
+        r.stop = i + 1;
+        r.status = 4;
+      } else if (k.check_tol && d < k.tol) {
+        r.stop = i + 1;
+        r.status = 1;
+      }
+    }
+  }
+  return r;
+}
+
+// History and reported scalars of the first n pending iterations (one thread).
+__device__ __forceinline__ void late3_record(const KParams& k, DevState* st, int n) {
+  const long long K0 = st->iter - st->late3;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    if (i < n) {
+      const double d = late_diff(k, st, i);
+      hist_put(k, K0 + i + 1, d);
+      st->last_diff = d;
+      st->alpha = st->sc3[3 + i];
+      st->beta = st->sc3[6 + i];
+      st->rz_cur = st->sc3[9 + i];
+    }
+  }
+}
+
+// Terminal state (one thread, after every wave of the grid has read the
+// state): the pending iterations' records up to `upto`, then iteration
+// `iter` with `status`.
+__device__ __forceinline__ void sweep3_stop(const KParams& k, DevState* st, int upto, long long iter, int status) {
+  late3_record(k, st, upto);
+  st->iter = iter;
+  st->status = status;
+  st->late3 = 0;
+  st->brk3 = 0;
   st->done = 1;
   st->wpend = 0;
 }
 
-// State update after a full sweep (one thread; sums t[] global): the late
-// stop tests of the m applied iterations, then breakdown / cap.
+// State update after a full sweep (one thread; sums t[] global or, with the
+// comm's allreduce after the sweep, this rank's): the previous sweep's
+// pending records (its stop tests passed at this launch's entry), then this
+// sweep's sums, coefficients and tentative iteration count; its own stop
+// tests are pending until the next launch.
 __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, int par, const Scal3& c,
                                                 const double (&t)[NS]) {
+  if (!c.first) late3_record(k, st, st->late3);
 #pragma unroll
   for (int n = 0; n < NS; ++n) st->fs2[par][n] = t[n];
   // fault hooks (PE_FAULT_INJECT): the sums of the sweep completing iteration F
@@ -211,48 +277,18 @@ __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, 
     st->sc3[i] = c.c.zc[i];
     st->sc3[3 + i] = c.c.a[i];
     st->sc3[6 + i] = c.c.b[i];
-    st->sc3[9 + i] = 0.0;
-  }
-  const double hh = k.h1 * k.h2;
-  int stop = 0, status = 0;
-#pragma unroll
-  for (int i = 0; i < 3; ++i) {
-    if (stop == 0 && i < c.m) {
-      const double n2 = fmax(t[16 + i], 0.0);
-      const double d = k.weighted ? fabs(c.c.a[i]) * sqrt(n2 * hh) : fabs(c.c.a[i]) * sqrt(n2);
-      hist_put(k, c.K + i + 1, d);
-      st->last_diff = d;
+    st->sc3[9 + i] = c.g[i];
+    if (i + 1 == c.m) {
       st->alpha = c.c.a[i];
       st->beta = c.c.b[i];
       st->rz_cur = c.g[i];
       st->gprev = c.g[i];
-      st->iter = c.K + i + 1;
-      if (!isfinite(d)) {
-        status = 4;
-        stop = i + 1;
-      } else if (k.check_tol && d < k.tol) {
-        status = 1;
-        stop = i + 1;
-      }
     }
   }
-  if (stop == 0) {
-    if (c.brk) {
-      st->iter = c.K + c.brk;
-      status = c.bad ? 4 : 2;
-    } else if (c.K + c.m >= k.max_iter) {
-      status = 3;
-    }
-  } else if (stop < c.m && status == 1) {  // w holds the later iterations' terms: the next launch subtracts them
-#pragma unroll
-    for (int j = 1; j < 3; ++j)
-      if (j >= stop && j < c.m) st->sc3[9 + j] = -c.c.a[j];
-    st->fixpend = 1;
-  }
-  if (status) {
-    st->status = status;
-    st->done = 1;
-  }
+  st->iter = c.K + c.m;
+  st->late3 = c.m;
+  st->brk3 = c.brk ? c.K + c.brk : 0;
+  st->bad3 = c.bad ? 1 : 0;
 }
 
 // Item kinds (list entry flags): band items (a boundary-band row in the
@@ -693,51 +729,85 @@ template <bool PUSH>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
-  const int fix = st->fixpend;
   __shared__ double sm[4 * NS];
   __shared__ int sflag;
   __shared__ WaveTV3 tvs[kWPB];
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  if ((done || k.mlimit < 0) && !fix) return;  // (mlimit < 0: a fix-up-only launch)
+  if (done) return;
+  auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
+                            // the slots garbage pipeline-fill rows read stay finite)
+    WaveTV3& tv = tvs[wid];
+    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
+    for (int i = lane; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
+  };
+  // terminal paths: every wave has read the state before the last one to
+  // arrive writes it
+  auto finish = [&](int upto, long long iter, int status) {
+    if (arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
+      sweep3_stop(k, st, upto, iter, status);
+      __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  };
   double acc[NS];
 #pragma unroll
   for (int n = 0; n < NS; ++n) acc[n] = 0.0;
+  // 1. the previous sweep's pending stop tests
+  const int m0 = st->late3;
+  const long long K = st->iter, K0 = K - m0;
+  const Late3 lt = late3_test(k, st);
+  Coef3 cf;
   Scal3 sc = {};
-  if (fix) {
-    sc.first = false;
-    sc.m = 3;
+  bool fix = false;
+  int rpar = par;
+  if (lt.stop) {
+    if (!(lt.stop < m0 && lt.status == 1)) {
+      finish(lt.stop, K0 + lt.stop, lt.status);
+      return;
+    }
+    // converged before that sweep's last iteration: w holds the later
+    // iterations' α_j p_j — march the same inputs with the same coefficients
+    // again and subtract them (w only; one walk call site below: a second
+    // inlined copy of the marches costs the whole register budget)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      sc.c.zc[i] = st->sc3[i];
-      sc.c.a[i] = st->sc3[3 + i];
-      sc.c.b[i] = st->sc3[6 + i];
-      sc.c.cw[i] = st->sc3[9 + i];
+      cf.zc[i] = st->sc3[i];
+      cf.a[i] = st->sc3[3 + i];
+      cf.b[i] = st->sc3[6 + i];
+      cf.cw[i] = (i >= lt.stop && i < m0) ? -st->sc3[3 + i] : 0.0;
     }
+    fix = true;
+    rpar = st->wpar;
   } else {
-    sc = sweep3_scalars(k, st, par);
-    if (sc.m == 0 && !sc.first) {  // iteration K+1 breaks down before its update
-      if (arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
-        sweep3_terminal(st, sc);
+    // 2. the breakdown / cap that sweep saw coming
+    if (st->brk3) {
+      finish(m0, st->brk3, st->bad3 ? 4 : 2);
+      return;
+    }
+    if (m0 > 0 && K >= k.max_iter) {
+      finish(m0, K, 3);
+      return;
+    }
+    if (k.mlimit < 0) {  // a resolve-only launch: record the pending iterations
+      if (m0 > 0 && arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
+        late3_record(k, st, m0);
+        st->late3 = 0;
         __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }
-  }
-  const Coef3 cf = uni3(sc.c);
-  const int rpar = fix ? st->wpar : par;  // the fix-up re-reads the converging sweep's inputs
-  {  // band ring: defined contents (the never-written column 128 of b0 and the
-     // slots garbage pipeline-fill rows read stay finite)
-    WaveTV3& tv = tvs[wid];
-    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
-    for (int i = lane; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
-  }
-  walk3<PUSH>(k, cf, fix != 0, rpar, tvs[wid], wid, acc);
-  if (fix) {  // fix-up launch: w only; the last wave clears the request
-    if (arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
-      st->fixpend = 0;
-      __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // 3. this sweep's iterations
+    sc = sweep3_scalars(k, st, par);
+    if (sc.m == 0 && !sc.first) {  // iteration K+1 breaks down before its update
+      finish(m0, K + 1, sc.bad ? 4 : 2);
+      return;
     }
+    cf = sc.c;
+  }
+  zero_ring();
+  walk3<PUSH>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  if (fix) {
+    finish(lt.stop, K0 + lt.stop, lt.status);
     return;
   }
   if (lane < H3 || lane >= 64 - H3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns

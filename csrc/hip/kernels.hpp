@@ -59,12 +59,14 @@ struct DevState {
   // (two-step, layout: fused2.hip, sweep2_scalars) or 19 (three-step:
   // fused3.hip, sweep3_scalars).
   double fs2[2][24];
-  // Three-step sweep: the coefficients of the last sweep {zc[3], α[3], β[3],
-  // cw[3]} and fixpend = 1 when it converged before its last iteration — the
-  // next launch then subtracts Σ cw_j p_j from w (cw_j = −α_j past the stop).
+  // Three-step sweep (fused3.hip): the last sweep's coefficients {zc[3],
+  // α[3], β[3], g[3]}; late3 of its iterations (ending at iter) still await
+  // their stop tests (decided by the next launch from fs2[wpar]); brk3 > 0:
+  // the iteration that breaks down after them (bad3: non-finite scalars).
   double sc3[12];
-  int fixpend;
-  int pad3;
+  long long brk3;
+  int late3;
+  int bad3;
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
@@ -300,9 +302,10 @@ int resident_blocks_S(const KParams& k, int wm);  // wm 0: deferring sweep, 2: a
 // item list only; launch_S dispatches here when k.steps == 2).
 void launch_S2(const KParams& k, int par, hipStream_t s);
 int resident_blocks_S2();
-// Three-step sweep (fused3.hip): one launch = iterations K+1..K+3 (or fewer:
-// k.mlimit, breakdown, cap), or the w fix-up of a sweep that converged early
-// (DevState::fixpend); launch_S dispatches here when k.steps == 3.
+// Three-step sweep (fused3.hip): one launch = the previous launch's pending
+// stop tests (and, when it converged early, its w fix-up), then iterations
+// K+1..K+3 (or fewer: k.mlimit > 0, breakdown, cap; none: k.mlimit < 0);
+// launch_S dispatches here when k.steps == 3.
 void launch_S3(const KParams& k, int par, hipStream_t s);
 int resident_blocks_S3();
 // (k.ti / k.order select the kernel variant: set them first)
