@@ -399,6 +399,9 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   auto inr = [&](int q) { return STEADY ? !c.fix : (q >= c.ib && q <= c.ie); };
   auto own = [&](int q) { return STEADY || (q >= c.ib && q <= c.ie); };  // (stores)
   auto interior = [&](int q) { return q >= c.rlo && q <= c.rhi; };     // global interior row
+  // pipeline fill: stage d (B = 1 … F = 5) first feeds a needed row at step
+  // 2d (G's rows are tested by inr): skip it before — its rows are never used
+  auto live = [&](int d) { return STEADY || n >= 2 * d; };
   // band ring slots (runtime, mod 7) of rows t .. t-6
   int bsl[7];
 #pragma unroll
@@ -440,7 +443,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);  // (stage by stage, as the row tests of the generic steps)
   // ---- B: row t-1 ----
-  {
+  if (live(1)) {
     const int q = t - 1;
     double d;
     const double s1 = op(q, bsl[1], bsl[0], x.P1[m2], x.P1[m1], x.P1[m0], d);
@@ -453,7 +456,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- C: row t-2 (w) ----
-  {
+  if (live(2)) {
     const int q = t - 2;
     double d;
     const double s2 = op(q, bsl[2], bsl[1], x.P2[m0], x.P2[m2], x.P2[m1], d);
@@ -468,7 +471,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- D: row t-3 (r, p outputs) ----
-  {
+  if (live(3)) {
     const int q = t - 3;
     double d;
     const double s3 = op(q, bsl[3], bsl[2], x.P3[m1], x.P3[m0], x.P3[m2], d);
@@ -494,7 +497,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- E: row t-4 ----
-  {
+  if (live(4)) {
     const int q = t - 4;
     double d;
     const double qv = op(q, bsl[4], bsl[3], x.Z[m2], x.Z[m1], x.Z[m0], d);
@@ -512,7 +515,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- F: row t-5 ----
-  {
+  if (live(5)) {
     const int q = t - 5;
     double d, d2;
     const double au = op(q, bsl[5], bsl[4], x.U[m0], x.U[m2], x.U[m1], d);

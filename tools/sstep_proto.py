@@ -30,13 +30,30 @@ from poisson_ellipse_openmp_mpi_cuda_amd.ops.torch_ref import apply_A, assemble,
 
 
 def moments(r, p, A, Dinv, inner, s):
-    """mu[x][k] for x in (zz, zp, pp), k = 0 .. 2s-1 (NaN where not formed)."""
+    """mu[x][k] for x in (zz, zp, pp), k = 0 .. 2s-1 (NaN where not formed).
+    s <= 3: the pairs fused3.hip forms; larger s: (M^a x, D M^b y), a = k // 2."""
     z = Dinv * r
     sv = A(p)
+    nan = float("nan")
+    if s > 3:
+        D = torch.zeros_like(Dinv)
+        m = Dinv != 0
+        D[m] = 1.0 / Dinv[m]
+        Mz, Mp = [z], [p]
+        for _ in range(s):
+            Mz.append(Dinv * A(Mz[-1]))
+            Mp.append(Dinv * A(Mp[-1]))
+        mu = {"zz": [], "zp": [nan], "pp": [nan]}
+        for k in range(2 * s):
+            a, b = k // 2, k - k // 2
+            mu["zz"].append(inner(Mz[a], D * Mz[b]) if k else inner(r, z))
+            if k:
+                mu["zp"].append(inner(Mz[a], D * Mp[b]))
+                mu["pp"].append(inner(Mp[a], D * Mp[b]))
+        return mu
     q = A(z)
     u = Dinv * q
     v = Dinv * sv
-    nan = float("nan")
     zz = [inner(r, z), inner(z, q), inner(q, u)]
     zp = [nan, inner(z, sv), inner(q, v)]
     pp = [nan, inner(p, sv), inner(sv, v)]
