@@ -431,7 +431,9 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
     x.RQ[xs] = ldx3<PUSH>(k, c, tn, c.off);
     x.PQ[xs] = ldx3<PUSH>(k, c, tn, unsigned(c.poff) + c.off);
     const int wr = STEADY ? t - 2 + WD : min(max(t - 2 + WD, c.ib), c.ie);
-    x.WQ[ws] = ldnt1(c.Wm + int64_t(wr) * c.wp + c.off);
+    // (only the lanes that store w load it: the 12 halo lanes' columns are a
+    // neighbouring strip's, and their lines would be fetched for nothing)
+    x.WQ[ws] = c.o0 ? ldnt1(c.Wm + int64_t(wr) * c.wp + c.off) : 0.0;
   }
   {
     double d;
@@ -649,7 +651,8 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
     x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off);
   }
 #pragma unroll
-  for (int q = 0; q < WD; ++q) x.WQ[q] = ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off);
+  for (int q = 0; q < WD; ++q)
+    x.WQ[q] = c.o0 ? ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off) : 0.0;
 #pragma unroll
   for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = 0.0;
 #pragma unroll
