@@ -17,9 +17,10 @@ reference's stage 4 runs as N MPI ranks on N GPUs,
 stage4-mpi+cuda/poisson_mpi_cuda2.cu:986-990).
 
 A *step* is one full PCG iteration of the global solve on N GPUs (the
-single-sweep kernel with its 7 sums summed over ranks inside the sweep over
-xGMI P2P, and the halo rows — row-slab blocks — pushed by the same sweep into
-the neighbours' receive buffers, or exchanged through RCCL otherwise).  The
+three-step sweep advances three per launch, its 19 sums summed over ranks
+inside the sweep over xGMI P2P, and the halo rows — row-slab blocks — pushed
+by the same sweep into the neighbours' receive buffers, or exchanged through
+RCCL otherwise; K steps with 3 ∤ K end with a partial sweep).  The
 timed region runs exactly K steps from the start of a fresh solve (w⁰ = 0, as
 the reference) with the convergence test switched off so every step does full
 work; it is bracketed by a barrier + device synchronise on both sides and the
@@ -73,8 +74,11 @@ def parse_args(argv):
     ap.add_argument("--seed", type=int, default=1234, help="random-init w0 seed")
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused", "two-step", "three-step"))
-    ap.add_argument("--launch", default="graph", choices=("graph", "eager"),
-                    help="timed steps replayed from instantiated hipGraphs (default) or launched eagerly")
+    # eager by default: a 20-step window launched eagerly took 5.29-5.41 ms
+    # against 5.30-5.85 ms replayed from its chunk graph (the first replay of
+    # a window sometimes paid ~0.5 ms more: profiles/r3_window.txt)
+    ap.add_argument("--launch", default="eager", choices=("graph", "eager"),
+                    help="timed steps launched eagerly (default) or replayed from instantiated hipGraphs")
     return ap.parse_args(argv)
 
 
@@ -221,8 +225,9 @@ def main(argv=None) -> int:
           "placement_chosen": solver.placement_choice, "construct_s": round(solver.construct_s, 3)}
     ranks_info = gather(me)
 
-    # warmup: first-touch / RCCL connections, then instantiate every chunk
-    # graph the timed run will launch (no capture inside the timed region)
+    # warmup: first-touch / RCCL connections, then (--launch graph)
+    # instantiate every chunk graph the timed run will launch (no capture
+    # inside the timed region)
     use_graph = a.launch == "graph"
     solver.reset()
     if a.warmup > 0:

@@ -85,12 +85,19 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     auto slabs = [&](int64_t m) {
       return comm_->size() > 1 && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= m && prob_.N - 1 >= m;
     };
+    // 2-D splits (three-step only): the 6-deep halo through the comm's
+    // exchange — y strips packed after the sweep, then the x rows with their
+    // halo columns (corners) — from blocks of >= 12 rows and columns each
+    auto grid2d = [&](int64_t m) {
+      return comm_->size() > 1 && blk_.Py > 1 && (prob_.M - 1) / blk_.Px >= m && (prob_.N - 1) / blk_.Py >= m;
+    };
     const bool two_ok = fused_ && (single(8) || slabs(8));
-    const bool three_ok = fused_ && (single(8) || slabs(12));
+    const bool three_ok = fused_ && (single(8) || slabs(12) || grid2d(12));
     if (opt_.algo == 3 && !two_ok)
       throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
     if (opt_.algo == 4 && !three_ok)
-      throw std::invalid_argument("three-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 12 rows");
+      throw std::invalid_argument(
+          "three-step sweep: single-rank blocks of >= 8 x 8 nodes, row slabs of >= 12 rows or 2-D blocks of >= 12 x 12");
     // auto: every single-rank block the LDS-resident kernel cannot hold
     // (1x MI355X, fresh processes, T_solver two-step vs single sweep:
     // 1600×2400 0.110 vs 0.127 s, 2048² 0.113 vs 0.133, 4096² 0.378 vs 0.584,
@@ -109,7 +116,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
                           ntr * ns <= dev::kResMaxTiles;
       }
     }
-    bool auto_ms = slabs(8) || !resident_likely;
+    bool auto_ms = slabs(8) || grid2d(12) || !resident_likely;
     if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
     int want = 3;
     if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
@@ -158,7 +165,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     walt_ = static_cast<double*>(field_alloc(sizeof(double) * wsize_, alloc_mode_));
     mark("field allocs");
     set_fused_fields(fields_, xalt_, walt_);
-    hsize_ = std::max<int64_t>(1, nx) * 4;
+    hsize_ = std::max<int64_t>(1, nx) * 2 * hdep_;  // y strips: hdep columns of r and p per owned row
     // (multi-step: rows -hdep .. nx+hdep+2, columns -hdep .. fsw·strips+hdep+3)
     rows_hi = sstep_ ? nx + hdep_ + 2 : nx + 3;
     cols_hi = sstep_ ? fsw_ * strips + hdep_ + 3 : dev::kFSW * strips + 3;
@@ -774,8 +781,10 @@ std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
   if (!fused_) return {HaloPhase{halo_plan(), false}};
   const KParams& k = *kp_;
   std::vector<HaloPhase> ph(2);
-  // Phase 0: y strips (4 values per owned row: r and p of two columns).
-  const int64_t c = 4 * blk_.nx;
+  // Phase 0: y strips (2·hdep values per owned row: r and p of hdep columns;
+  // the single sweep stores them from inside the sweep, the multi-step
+  // sweeps' are packed after it — enqueue_exchange).
+  const int64_t c = 2 * int64_t(hdep_) * blk_.nx;
   if (blk_.has(DOWN)) ph[0].ex.push_back(Exchange{DOWN, blk_.nbr[DOWN], k.send_dn, const_cast<double*>(k.recv_dn), c});
   if (blk_.has(UP)) ph[0].ex.push_back(Exchange{UP, blk_.nbr[UP], k.send_up, const_cast<double*>(k.recv_up), c});
   ph[0].unpack = blk_.has(DOWN) || blk_.has(UP);
@@ -797,6 +806,7 @@ void DeviceSolver::enqueue_exchange(int buf, bool after_sweep) {
   // halo push: the sweep that wrote `buf` has pushed its edge rows into the
   // neighbours' receive buffers, from which the next sweep reads them
   if (push_ && after_sweep) return;
+  if (sstep_ && after_sweep) dev::launch_pack(*kp_, buf, stream_);  // (no-op without a y neighbour)
   for (const HaloPhase& ph : halo_phases(buf)) {
     comm_->exchange(ph.ex, stream_);
     if (ph.unpack) dev::launch_unpack(*kp_, buf, stream_);

@@ -1128,44 +1128,48 @@ __global__ void kWaitSig(DevState* st, unsigned long long target) {
   }
 }
 
-// y-direction halo strips of buffer b (one thread per owned row).
+// y-direction halo strips of buffer b (one thread per owned row): the hdep
+// owned columns next to each y neighbour, r then p — columns 1..h → DOWN
+// (its ny'+1..ny'+h), ny-h+1..ny → UP (its 1-h..0).
 __global__ void kPack(KParams k, int b) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x + 1;
   if (i > k.nx) return;
+  const int h = k.hdep;
   const double* x = k.x[b] + i * k.pitch;
   if (k.has[DOWN]) {
-    double* sb = k.send_dn + (i - 1) * 4;
-    sb[0] = x[1];
-    sb[1] = x[2];
-    sb[2] = x[k.poff + 1];
-    sb[3] = x[k.poff + 2];
+    double* sb = k.send_dn + (i - 1) * 2 * h;
+    for (int m = 0; m < h; ++m) {
+      sb[m] = x[1 + m];
+      sb[h + m] = x[k.poff + 1 + m];
+    }
   }
   if (k.has[UP]) {
-    double* sb = k.send_up + (i - 1) * 4;
-    sb[0] = x[k.ny - 1];
-    sb[1] = x[k.ny];
-    sb[2] = x[k.poff + k.ny - 1];
-    sb[3] = x[k.poff + k.ny];
+    double* sb = k.send_up + (i - 1) * 2 * h;
+    for (int m = 0; m < h; ++m) {
+      sb[m] = x[k.ny - h + 1 + m];
+      sb[h + m] = x[k.poff + k.ny - h + 1 + m];
+    }
   }
 }
 
 __global__ void kUnpack(KParams k, int b) {
   const int64_t i = int64_t(blockIdx.x) * blockDim.x + threadIdx.x + 1;
   if (i > k.nx) return;
+  const int h = k.hdep;
   double* x = k.x[b] + i * k.pitch;
   if (k.has[DOWN]) {
-    const double* rb = k.recv_dn + (i - 1) * 4;
-    x[-1] = rb[0];
-    x[0] = rb[1];
-    x[k.poff - 1] = rb[2];
-    x[k.poff] = rb[3];
+    const double* rb = k.recv_dn + (i - 1) * 2 * h;
+    for (int m = 0; m < h; ++m) {
+      x[1 - h + m] = rb[m];
+      x[k.poff + 1 - h + m] = rb[h + m];
+    }
   }
   if (k.has[UP]) {
-    const double* rb = k.recv_up + (i - 1) * 4;
-    x[k.ny + 1] = rb[0];
-    x[k.ny + 2] = rb[1];
-    x[k.poff + k.ny + 1] = rb[2];
-    x[k.poff + k.ny + 2] = rb[3];
+    const double* rb = k.recv_up + (i - 1) * 2 * h;
+    for (int m = 0; m < h; ++m) {
+      x[k.ny + 1 + m] = rb[m];
+      x[k.poff + k.ny + 1 + m] = rb[h + m];
+    }
   }
 }
 

@@ -308,6 +308,7 @@ struct M3Ctx {
   int J, c0, ib, ie, t0, tmax, nx, par;
   unsigned off;
   bool lv0, o0, fix;
+  bool scol;          // the lane's column is not past ny (2-D blocks: past ny are the UP neighbour's)
   double lf0;         // lv0 as 1.0 / 0.0 (uniform items of the edge strips)
   double oih1, oih2;  // inv_eps / h1², inv_eps / h2² (uniform exterior rows)
   double ih1, ih2, din, dout;  // 1/h1², 1/h2², 1/D interior / exterior (copies: a select between
@@ -398,6 +399,14 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   // interleaving the stages' sums, which costs ~200 VGPRs)
   auto inr = [&](int q) { return STEADY ? !c.fix : (q >= c.ib && q <= c.ie); };
   auto own = [&](int q) { return STEADY || (q >= c.ib && q <= c.ie); };  // (stores)
+  // sums of the item's rows; lane-tested kinds drop columns past ny (an UP
+  // neighbour's, in the last strip of a 2-D block: never a uniform item) by a
+  // select, not a branch — the stages' DPP neighbour reads need every lane
+  // active (a disabled source lane reads as 0)
+  auto put = [&](int n, double v) {
+    if constexpr (UNI) sv[n] += v;
+    else sv[n] += c.scol ? v : 0.0;
+  };
   auto interior = [&](int q) { return q >= c.rlo && q <= c.rhi; };     // global interior row
   // pipeline fill: stage d (B = 1 … F = 5) first feeds a needed row at step
   // 2d (G's rows are tested by inr): skip it before — its rows are never used
@@ -454,7 +463,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
     const double p1 = x.P1[m1];
     x.R1[e1] = r1;
     x.P2[m1] = zc2 * z + c.b2 * p1;
-    if (inr(q)) sv[16] += p1 * p1;
+    if (inr(q)) put(16, p1 * p1);
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- C: row t-2 (w) ----
@@ -469,7 +478,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
     const double p3 = zc3 * z + c.b3 * p2;
     x.P3[m2] = p3;
     if (own(q) && c.o0) stnt1(c.Wm + int64_t(q) * c.wp + c.off, wrow + w1 * x.P1[m2] + w2 * p2 + w3 * p3);
-    if (inr(q)) sv[17] += p2 * p2;
+    if (inr(q)) put(17, p2 * p2);
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- D: row t-3 (r, p outputs) ----
@@ -491,10 +500,10 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
       if constexpr (PUSH) push_row3(k, c, x, q, r3, p3);
     }
     if (inr(q)) {
-      sv[0] += r3 * z;    // (r,z)
-      sv[6] += z * s3;    // (z,s)
-      sv[11] += p3 * s3;  // (p,s)
-      sv[18] += p3 * p3;  // ‖p₃‖²
+      put(0, r3 * z);    // (r,z)
+      put(6, z * s3);    // (z,s)
+      put(11, p3 * s3);  // (p,s)
+      put(18, p3 * p3);  // ‖p₃‖²
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
@@ -509,10 +518,10 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
     x.U[m1] = u;
     x.V[m1] = v;
     if (inr(q)) {
-      sv[1] += x.Z[m1] * qv;  // (z,q)
-      sv[2] += qv * u;        // (q,u)
-      sv[7] += qv * v;        // (q,v)
-      sv[12] += sr * v;       // (s,v)
+      put(1, x.Z[m1] * qv);  // (z,q)
+      put(2, qv * u);        // (q,u)
+      put(7, qv * v);        // (q,v)
+      put(12, sr * v);       // (s,v)
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
@@ -528,12 +537,12 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
     x.VV[m2] = vv;
     if (inr(q)) {
       const double u = x.U[m2], v = x.V[m2];
-      sv[3] += u * au;    // (u,Au)
-      sv[8] += u * av;    // (u,Av)
-      sv[13] += v * av;   // (v,Av)
-      sv[4] += au * uu;   // (Au,ũ)
-      sv[9] += au * vv;   // (Au,ṽ)
-      sv[14] += av * vv;  // (Av,ṽ)
+      put(3, u * au);    // (u,Au)
+      put(8, u * av);    // (u,Av)
+      put(13, v * av);   // (v,Av)
+      put(4, au * uu);   // (Au,ũ)
+      put(9, au * vv);   // (Au,ṽ)
+      put(14, av * vv);  // (Av,ṽ)
     }
   }
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
@@ -545,9 +554,9 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
       const double auu = op(q, bsl[6], bsl[5], x.UU[m1], x.UU[m0], x.UU[m2], d);
       const double avv = op(q, bsl[6], bsl[5], x.VV[m1], x.VV[m0], x.VV[m2], d);
       const double uu = x.UU[m0], vv = x.VV[m0];
-      sv[5] += uu * auu;   // (ũ,Aũ)
-      sv[10] += uu * avv;  // (ũ,Aṽ)
-      sv[15] += vv * avv;  // (ṽ,Aṽ)
+      put(5, uu * auu);   // (ũ,Aũ)
+      put(10, uu * avv);  // (ũ,Aṽ)
+      put(15, vv * avv);  // (ṽ,Aṽ)
     }
   }
 }
@@ -605,6 +614,7 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   c.lv0 = c.c0 <= ny + H3 && g0 >= 1 && g0 <= k.N - 1;
   c.lf0 = c.lv0 ? 1.0 : 0.0;
   c.o0 = lane >= H3 && lane < 64 - H3 && c.c0 >= 1 && c.c0 <= ny;
+  c.scol = c.c0 <= ny;
   c.fix = fix;
   c.ib = ib;
   c.ie = ie;

@@ -165,7 +165,11 @@ void DeviceSolver::setup_items() {
   };
   auto entry = [&](int64_t ib, int64_t rows, int s) {
     int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
-    if (flag == 0 && steps_ == 3 && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
+    // (not the last strip of a block with an UP neighbour: its output lanes
+    // past ny hold that neighbour's columns, which only the lane-tested
+    // march keeps out of the sums)
+    const bool cut = (blk_.has(UP) && int64_t(s + 1) * fsw_ > blk_.ny);
+    if (flag == 0 && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
   // outputs a neighbour needs: first in the layout under the overlap (they

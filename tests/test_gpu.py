@@ -338,6 +338,8 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce.split("-")[0],
                PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1",
                PE_HALO="exchange" if allreduce == "p2p-exchange" else "push")
+    if overlap == "1":  # the boundary / interior overlap is a single-sweep feature
+        env["PE_STEPS"] = "1"
     if allreduce == "p2p-dyn":
         env["PE_ORDER"] = "3"
         env["PE_FOLD"] = "1"
@@ -353,12 +355,41 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
     assert d["xr"] == (allreduce in ("p2p", "p2p-exchange", "p2p-dyn"))
     assert d["halo_push"] == (d["Py"] == 1 and allreduce in ("p2p", "p2p-dyn"))
-    # row slabs run the three-step sweep (6-deep halo: pushed, or exchanged), 2D blocks the single sweep
-    assert d["algo"] == ("three-step" if d["Py"] == 1 else "fused"), d["algo"]
+    # every split runs the three-step sweep (6-deep halo: pushed by the sweep on
+    # row slabs, else exchanged — 2-D blocks pack their y strips after the
+    # sweep); PE_STEPS=1 keeps the single sweep and its overlap
+    assert d["algo"] == ("fused" if overlap == "1" else "three-step"), d["algo"]
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
     np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("nproc,decomp,allreduce", [(2, "1x2", "p2p"), (4, "2x2", "rccl"), (6, "2x3", "p2p")])
+def test_multi_process_2d_three_step(gpu, nproc, decomp, allreduce):
+    """2-D splits run the three-step sweep through the exchange: 6 columns of
+    r and p per owned row packed after each sweep (kPack), exchanged and
+    unpacked, then the x rows with their halo columns (the corners come from
+    the diagonal rank).  300×437: every block's last strip has output lanes
+    past ny, i.e. in the UP neighbour's columns, which the lane-tested march
+    keeps out of the sums (item_layout never flags those items uniform).
+    Iteration count and gathered w match one process."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="60")
+    outp = os.path.join(ROOT, "gpurun_out", f"mp3_w_{nproc}_{decomp}.npy")
+    os.makedirs(os.path.dirname(outp), exist_ok=True)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+           "poisson_ellipse_openmp_mpi_cuda_amd", "--json", "--quiet", "--decomp", decomp, "--dump", outp, "300", "437"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["ranks"] == nproc and d["Py"] > 1 and d["algo"] == "three-step", d
+    assert not d["halo_push"]
+    one = solve(EllipseProblem(300, 437), backend="hip", return_w=True)
+    assert abs(d["iters"] - one.iters) <= 1
+    np.testing.assert_allclose(np.load(outp), one.w, rtol=0, atol=1e-9)
 
 
 def test_halo_push_selftest_failure_falls_back(gpu):
