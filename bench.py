@@ -312,7 +312,7 @@ def main(argv=None) -> int:
             "distinct_gpus": len(pcis),
             "ranks": ranks_info,
             "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
-            "halo": ("in-sweep xGMI push (graph-captured)" if solver.halo_push else
+            "halo": ("in-sweep xGMI push" + (" (graph-captured)" if use_graph else "") if solver.halo_push else
                      ("exchange: " + comm.name)) if world > 1 else "none",
             "overlap": bool(solver.overlap),
             "exchange_us_measured": round(solver.exchange_us, 2),

@@ -453,7 +453,8 @@ def test_bench_halo_push_graphs(gpu, nproc):
     env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(nproc), "--steps", "40", "--warmup", "4", "--grid", str(M), str(N), "--decomp", "rows"]
+           "--gpus", str(nproc), "--steps", "40", "--warmup", "4", "--grid", str(M), str(N), "--decomp", "rows",
+           "--launch", "graph"]
     out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert out.returncode == 0, out.stderr[-3000:]
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
