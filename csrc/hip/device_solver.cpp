@@ -1078,8 +1078,10 @@ void DeviceSolver::wait_event(hipEvent_t ev) {
       throw std::runtime_error("watchdog: device made no progress for " + std::to_string(watchdog_s_) +
                                " s (communicator aborted)");
     }
-    // spin for the first 2 ms (a bench's closing wait stays exact), then poll
-    if (secs(t0, clk::now()) > 2e-3) std::this_thread::sleep_for(std::chrono::microseconds(20));
+    // spin (yielding) for the first 250 ms, then poll every 20 µs: a sleeping
+    // poll detects the end late by up to a scheduler tick, and a bench's
+    // closing wait of a 5 ms window used to span the 2 ms the spin lasted
+    if (secs(t0, clk::now()) > 0.25) std::this_thread::sleep_for(std::chrono::microseconds(20));
     else std::this_thread::yield();
   }
 }
