@@ -91,8 +91,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     auto grid2d = [&](int64_t m) {
       return comm_->size() > 1 && blk_.Py > 1 && (prob_.M - 1) / blk_.Px >= m && (prob_.N - 1) / blk_.Py >= m;
     };
+    // virtual ranks on one device (device_solve_group: no comm, a split block;
+    // the group driver exchanges the halos and sums the sweeps' sums)
+    auto vgroup = [&](int64_t m) {
+      return comm_->size() == 1 && blk_.Px * blk_.Py > 1 && (prob_.M - 1) / blk_.Px >= m &&
+             (prob_.N - 1) / blk_.Py >= m;
+    };
     const bool two_ok = fused_ && (single(8) || slabs(8));
-    const bool three_ok = fused_ && (single(8) || slabs(12) || grid2d(12));
+    const bool three_ok = fused_ && (single(8) || slabs(12) || grid2d(12) || vgroup(12));
     if (opt_.algo == 3 && !two_ok)
       throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
     if (opt_.algo == 4 && !three_ok)
@@ -116,7 +122,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
                           ntr * ns <= dev::kResMaxTiles;
       }
     }
-    bool auto_ms = slabs(8) || grid2d(12) || !resident_likely;
+    bool auto_ms = slabs(8) || grid2d(12) || vgroup(12) || !resident_likely;
     if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
     int want = 3;
     if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
@@ -825,6 +831,7 @@ void DeviceSolver::import_halos() {
 double* DeviceSolver::red_F_dev() { return st_->red_F; }
 double* DeviceSolver::red_G_dev() { return st_->red_G; }
 double* DeviceSolver::fs_dev(int par) { return st_->fs[par]; }
+double* DeviceSolver::fs2_dev(int par) { return st_->fs2[par]; }
 double* DeviceSolver::err_dev() { return st_->err; }
 
 void DeviceSolver::enqueue_init() {
@@ -1425,17 +1432,23 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
     s.push_back(std::make_unique<DeviceSolver>(P, blks.back(), nullptr, opt));
   }
   const bool fused = s[0]->fused();
+  // multi-step sweeps (three-step on blocks of >= 12 x 12): one launch per
+  // `steps` iterations, the exchange after each, the kNS3 sums summed here
+  const int steps = s[0]->sweep_steps();
+  const bool ms = s[0]->two_step();
+  const int nsum = steps == 3 ? dev::kNS3 : steps == 2 ? dev::kNS2 : 7;
   std::vector<hipEvent_t> ev(ranks);
   for (auto& e : ev) PE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // Device pointer tables for the cross-rank reduction kernel:
-  // [red_F | red_G | err | fs0 | fs1] × ranks.
+  // [red_F | red_G | err | fs0 | fs1] × ranks (multi-step: fs2[0] / fs2[1]
+  // in the fs slots).
   std::vector<double*> hp(5 * ranks);
   for (int r = 0; r < ranks; ++r) {
     hp[r] = s[r]->red_F_dev();
     hp[ranks + r] = s[r]->red_G_dev();
     hp[2 * ranks + r] = s[r]->err_dev();
-    hp[3 * ranks + r] = s[r]->fs_dev(0);
-    hp[4 * ranks + r] = s[r]->fs_dev(1);
+    hp[3 * ranks + r] = ms ? s[r]->fs2_dev(0) : s[r]->fs_dev(0);
+    hp[4 * ranks + r] = ms ? s[r]->fs2_dev(1) : s[r]->fs_dev(1);
   }
   double** dp = nullptr;
   PE_HIP_CHECK(hipMalloc(&dp, sizeof(double*) * 5 * ranks));
@@ -1457,7 +1470,10 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   };
   // Same halo phases as under RCCL; the transport is a D2D copy from the
   // peer's send region once the peer's stream has produced it.
-  auto exchange = [&](int buf) {
+  auto exchange = [&](int buf, bool after_sweep) {
+    // (multi-step sweeps do not store their y strips: packed here)
+    if (ms && after_sweep)
+      for (int r = 0; r < ranks; ++r) s[r]->enqueue_pack(buf);
     std::vector<std::vector<DeviceSolver::HaloPhase>> plan(ranks);
     for (int r = 0; r < ranks; ++r) plan[r] = s[r]->halo_phases(buf);
     for (size_t ph = 0; ph < plan[0].size(); ++ph) {
@@ -1480,12 +1496,12 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   for (int r = 0; r < ranks; ++r) s[r]->enqueue_init();
   if (fused) {
     for (int r = 0; r < ranks; ++r) s[r]->enqueue_pack(0);
-    exchange(0);
+    exchange(0, false);
     for (int r = 0; r < ranks; ++r) s[r]->enqueue_S(1);
-    exchange(1);
-    reduce(dp + 4 * ranks, 7, 0);
+    exchange(1, true);
+    reduce(dp + 4 * ranks, nsum, 0);
   } else {
-    exchange(0);
+    exchange(0, false);
     reduce(dp + ranks, 1, 0);
   }
   PE_HIP_CHECK(hipStreamSynchronize(s0));
@@ -1496,23 +1512,26 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   const int chunk = s[0]->chunk();
   DevState hs;
   int64_t k = 0;
+  int64_t nsweep = 0;  // launches (parity)
   for (;;) {
-    for (int it = 0; it < chunk; ++it, ++k) {
-      const int par = int(k & 1);
+    for (int it = 0; it < chunk; it += steps, k += steps, ++nsweep) {
+      const int par = int(nsweep & 1);
       if (fused) {
+        // (multi-step: the sweep applies min(steps, cap - K) iterations and
+        // resolves its predecessor's stop tests itself)
         for (int r = 0; r < ranks; ++r) s[r]->enqueue_S(par);
-        exchange(par);
-        reduce(dp + (3 + par) * ranks, 7, 0);
+        exchange(par, true);
+        reduce(dp + (3 + par) * ranks, nsum, 0);
         continue;
       }
       for (int r = 0; r < ranks; ++r) s[r]->enqueue_F(par);
       reduce(dp, 2, 0);
       for (int r = 0; r < ranks; ++r) s[r]->enqueue_G(par);
-      exchange(0);
+      exchange(0, false);
       reduce(dp + ranks, 1, 0);
     }
     s[0]->read_state(&hs);
-    if (hs.done || k >= cap) break;
+    if (hs.done || k >= cap + (ms ? steps : 0)) break;
   }
   for (int r = 0; r < ranks; ++r) s[r]->synchronize();
   res.t.iterate = secs(t_loop, clk::now());
@@ -1560,7 +1579,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   PE_HIP_CHECK(hipFree(dp));
   for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
   res.backend = "hip-group";
-  res.algo = fused ? "fused" : "classic";
+  res.algo = steps == 3 ? "three-step" : steps == 2 ? "two-step" : fused ? "fused" : "classic";
   res.Px = pg.Px;
   res.Py = pg.Py;
   res.t.solver = secs(t_start, clk::now());

@@ -151,6 +151,7 @@ class DeviceSolver {
   double* red_F_dev();
   double* red_G_dev();
   double* fs_dev(int par);
+  double* fs2_dev(int par);  // multi-step sweeps' sums (kNS2 / kNS3 of them)
   double* err_dev();
   // Halo exchange as ordered phases; after a phase with `unpack` set the
   // received y strips are scattered into buffer `buf` (single-sweep layout:

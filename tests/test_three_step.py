@@ -194,3 +194,29 @@ def test_three_step_is_auto_default(gpu, monkeypatch):
     assert solve(prob, backend="hip").algo == "three-step"
     monkeypatch.setenv("PE_STEPS", "2")
     assert solve(prob, backend="hip").algo == "two-step"
+
+
+@pytest.mark.parametrize("ranks,decomp", [(2, "1x2"), (4, "2x2"), (6, "2x3"), (3, "rows")])
+def test_three_step_virtual_ranks(gpu, ranks, decomp):
+    """Virtual ranks on one GPU (backend hip-group) run the three-step sweep
+    on blocks of >= 12 x 12: the group driver packs and exchanges the 6-deep
+    halos after every sweep and sums the 19 sums over the blocks; the last
+    strip of a block with an UP neighbour keeps that neighbour's columns out
+    of its sums.  Same iteration count and w as one block."""
+    prob = EllipseProblem(300, 437)
+    one = solve(prob, backend="hip", return_w=True, algo=THREE)
+    grp = solve(prob, backend="hip-group", ranks=ranks, decomp=decomp, return_w=True)
+    assert grp.algo == "three-step" and grp.Px * grp.Py == ranks
+    assert abs(grp.iters - one.iters) <= 1 and grp.converged
+    np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-9)
+
+
+@pytest.mark.parametrize("cap", [7, 8, 9])
+def test_three_step_virtual_ranks_cap(gpu, cap):
+    """An iteration cap inside a sweep: the group stops on it like one block."""
+    prob = EllipseProblem(300, 437)
+    prob.max_iter = cap
+    one = solve(prob, backend="hip", return_w=True, algo=THREE)
+    grp = solve(prob, backend="hip-group", ranks=4, decomp="2x2", return_w=True)
+    assert grp.algo == "three-step" and grp.iters == one.iters == cap and not grp.converged
+    np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-12 * np.abs(one.w).max())
