@@ -301,7 +301,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (fused_ && ti_env == 0) ti = huge ? 18 : big ? 24 : 10;
   k.order = (fused_ && huge) ? 3 : 0;
   if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
-    if (ti_env == 0) ti = steps_ == 3 ? (big ? 80 : 48) : (big ? 40 : 24);
+    // (three-step beyond 2²⁶ nodes: 128 rows — 16384² 978 vs 999 µs/iteration
+    // at 80, one placement, profiles/r3_ti_final.txt)
+    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 128 : big ? 80 : 48) : (big ? 40 : 24);
     ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
