@@ -84,6 +84,9 @@ def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, ove
     assert d["comm"].endswith("rccl")
     assert d["comm"].startswith("p2p-allreduce") == (allreduce == "p2p")
     assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p" and halo == "push")
+    # every block of 600×840 keeps >= 12 rows and columns: three-step everywhere
+    # (row slabs push their halos, 2-D blocks exchange them through RCCL)
+    assert d["algo"] == "three-step", d["algo"]
     assert abs(d["iters"] - single.iters) <= 1
     np.testing.assert_allclose(np.load(outp), single.w, rtol=0, atol=1e-9)
 
