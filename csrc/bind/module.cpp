@@ -72,6 +72,10 @@ py::dict state_dict(const dev::DevState& s) {
   for (int n = 0; n < 12; ++n) c3.append(s.sc3[n]);
   d["sc3"] = py::tuple(c3);
   d["wait_s"] = double(s.xr_wait) * 1e-8;
+  d["wpar"] = s.wpar;
+  d["res"] = py::make_tuple(s.res[0], s.res[1], s.res[2], s.res[3]);
+  d["k0"] = s.k0;
+  d["fixj"] = s.fixj;
   return d;
 }
 
@@ -183,6 +187,11 @@ PYBIND11_MODULE(_native, m) {
       .def_readonly("backend", &SolveResult::backend)
       .def_readonly("algo", &SolveResult::algo)
       .def_readonly("resident_fallback", &SolveResult::resident_fallback)
+      .def_readonly("res_true", &SolveResult::res_true)
+      .def_readonly("res_rec", &SolveResult::res_rec)
+      .def_readonly("res_gap", &SolveResult::res_gap)
+      .def_readonly("b_norm", &SolveResult::b_norm)
+      .def_readonly("restarts", &SolveResult::restarts)
       .def_property_readonly("timers", [](const SolveResult& r) { return timers_dict(r.t); });
 
   m.def("format_result_legacy", &format_result_legacy);
@@ -440,6 +449,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("segment_layout", &DeviceSolver::segment_layout)
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
+      .def_property_readonly("layout_cuts", &DeviceSolver::layout_cuts)
       .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def_property_readonly("halo_push", &DeviceSolver::halo_push,
                              "halo rows pushed by the sweep over xGMI (no exchange call; graph-capturable)")

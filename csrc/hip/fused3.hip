@@ -149,7 +149,7 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     live = live && i < lim;
-    const double beta = c.K + i == 0 ? 0.0 : g / gprev;
+    const double beta = c.K + i == st->k0 ? 0.0 : g / gprev;  // (k0: 0, or a restart's iteration)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       pz[q] = zz[q] + beta * pz[q];
@@ -242,8 +242,10 @@ __device__ __forceinline__ void late3_record(const KParams& k, DevState* st, int
 // Terminal state (one thread, after every wave of the grid has read the
 // state): the pending iterations' records up to `upto`, then iteration
 // `iter` with `status`.
-__device__ __forceinline__ void sweep3_stop(const KParams& k, DevState* st, int upto, long long iter, int status) {
+__device__ __forceinline__ void sweep3_stop(const KParams& k, DevState* st, int upto, long long iter, int status,
+                                            int fixj = 0) {
   late3_record(k, st, upto);
+  st->fixj = fixj;
   st->iter = iter;
   st->status = status;
   st->late3 = 0;
@@ -715,17 +717,35 @@ __device__ __forceinline__ Coef3 uni3(const Coef3& c) {
   return u;
 }
 
+__device__ __forceinline__ unsigned long long rtc3() {
+  unsigned long long t;  // one asm statement: never merged or moved by the compiler
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
 // Walk this wave's positions of the static item list.
-template <bool PUSH>
+// STAMP — diagnostic build (PE_STAMPS=1, tools/stamp_probe.py): lane 0 of
+// every wave records s_memrealtime at its entry and exit and at the start and
+// end of every item into k.stamps (the single sweep's layout: per position
+// {start, end, wave | strip << 32, first row | rows << 32 | kind << 48}, kind
+// 1 band, 2 uniform, 0 mixed; then per wave {entry, exit}).  Never the
+// production kernel.
+template <bool PUSH, bool STAMP>
 __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fix, int par, WaveTV3& tv, int wid,
                                       double (&acc)[NS]) {
   const int W = k.lwaves;
-  for (int pos = int(blockIdx.x) * kWPB + wid; pos < k.nslots; pos += W) {
+  const int gwave = int(blockIdx.x) * kWPB + wid;
+  const bool l0 = (threadIdx.x & 63) == 0;
+  if constexpr (STAMP) {
+    if (l0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave] = rtc3();
+  }
+  for (int pos = gwave; pos < k.nslots; pos += W) {
     const int2 e = cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
     if (rows == 0) continue;  // empty position of the static layout
     const int s = e.y & 0xFFFFF, ib = e.x & kRowMask3;
     const int ie = min(ib + rows - 1, int(k.nx));
+    const unsigned long long t_item = STAMP ? rtc3() : 0ull;
     if (e.x & kBandBit) {
       march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     } else if (e.x & kUniBit) {
@@ -738,10 +758,23 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     } else {
       march3<kMixed, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     }
+    if constexpr (STAMP) {
+      if (l0) {
+        const unsigned long long kind = (e.x & kBandBit) ? 1ull : (e.x & kUniBit) ? 2ull : 0ull;
+        unsigned long long* d = k.stamps + 4 * int64_t(pos);
+        d[0] = t_item;
+        d[1] = rtc3();
+        d[2] = (unsigned long long)gwave | ((unsigned long long)s << 32);
+        d[3] = (unsigned long long)ib | ((unsigned long long)(ie - ib + 1) << 32) | (kind << 48);
+      }
+    }
+  }
+  if constexpr (STAMP) {
+    if (l0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc3();
   }
 }
 
-template <bool PUSH>
+template <bool PUSH, bool STAMP = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
@@ -750,7 +783,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   __shared__ WaveTV3 tvs[kWPB];
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  if (done) return;
+  const bool replay = k.mlimit == kReplay3;
+  if (done && !replay) return;
   auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
                             // the slots garbage pipeline-fill rows read stay finite)
     WaveTV3& tv = tvs[wid];
@@ -759,9 +793,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   };
   // terminal paths: every wave has read the state before the last one to
   // arrive writes it
-  auto finish = [&](int upto, long long iter, int status) {
+  auto finish = [&](int upto, long long iter, int status, int fixj = 0) {
     if (arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
-      sweep3_stop(k, st, upto, iter, status);
+      sweep3_stop(k, st, upto, iter, status, fixj);
       __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   };
@@ -776,7 +810,23 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   Scal3 sc = {};
   bool fix = false;
   int rpar = par;
-  if (lt.stop) {
+  if (replay) {
+    // After a fix-up (the solve stopped at iteration j of its last sweep):
+    // march the last sweep's inputs again with its first j iterations and
+    // identity steps after them (zc = 0, β = 1, α = 0), w untouched, storing
+    // (r_j, p_j) into x[wpar] — the recurrence's r of the returned w.  No
+    // sums, no state update.
+    const int j = st->fixj;
+    if (j == 0) return;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      cf.zc[i] = i < j ? st->sc3[i] : 0.0;
+      cf.a[i] = i < j ? st->sc3[3 + i] : 0.0;
+      cf.b[i] = i < j ? st->sc3[6 + i] : 1.0;
+      cf.cw[i] = 0.0;
+    }
+    rpar = st->wpar;
+  } else if (lt.stop) {
     if (!(lt.stop < m0 && lt.status == 1)) {
       finish(lt.stop, K0 + lt.stop, lt.status);
       return;
@@ -821,9 +871,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     cf = sc.c;
   }
   zero_ring();
-  walk3<PUSH>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  walk3<PUSH, STAMP>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  if (replay) return;
   if (fix) {
-    finish(lt.stop, K0 + lt.stop, lt.status);
+    finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);
     return;
   }
   if (lane < H3 || lane >= 64 - H3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
@@ -860,7 +911,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
 }  // namespace
 
 void launch_S3(const KParams& k, int par, hipStream_t s) {
-  if (k.push) hipLaunchKernelGGL(kS3<true>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+  if (k.stamps && !k.push) hipLaunchKernelGGL((kS3<false, true>), dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+  else if (k.push) hipLaunchKernelGGL(kS3<true>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
   else hipLaunchKernelGGL(kS3<false>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
 }
 

@@ -290,11 +290,113 @@ void DeviceSolver::setup_items() {
         }
       }
     }
-    const int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
-    std::vector<std::vector<int>> per(static_cast<size_t>(W));
-    std::vector<double> load(static_cast<size_t>(W), 0.0);
-    std::vector<int> order;
+    // Three-step sweep: a filling layout instead.  The sweep's time per row
+    // step depends on the item's kind — a boundary-band item ≈2.2×, a mixed
+    // one ≈1.3× a uniform one (tools/stamp_probe.py, profiles/r4_stamps.txt)
+    // — and the LPT layout below, with whole items, leaves some waves one item
+    // more than the rest (8192²: 8 or 9 items of 92 row steps, wave busy
+    // time max/mean 1.08) or a single band item longer than every other
+    // wave's work (8-rank slab block: 1.33).  Here an item costs its steps ×
+    // its kind's factor + the overhead, every wave is filled up to the fair
+    // share T, and the item that would overflow the least-loaded wave is cut:
+    // the rows that fit go there, the rest goes back into the queue (each cut
+    // re-reads 2H fill rows, which T accounts for).  Largest first, ties in
+    // chunk-major order, so each round of positions still covers a compact
+    // window of rows.  PE_LAYOUT=lpt keeps the LPT layout.
+    const bool fill = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1) &&
+                      !(std::getenv("PE_LAYOUT") && std::string(std::getenv("PE_LAYOUT")) == "lpt");
+    int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
+    std::vector<std::vector<int>> per;
+    std::vector<double> load;
     int nbnd = 0;
+    if (fill) {
+      double fband = 2.2, fmixed = 1.3;
+      if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
+      if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
+      auto pcost = [&](int64_t ib, int64_t rows, int sx) {
+        const int2 e = entry(ib, rows, sx);
+        const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
+        return double(rows + 2 * H) * f + overhead;
+      };
+      std::vector<Piece> whole;
+      double total = 0.0;
+      for (int ch = 0; ch < nchunks; ++ch)
+        for (int sx = 0; sx < k.nstrips; ++sx) {
+          const int64_t ib = 1 + int64_t(ch) * k.ti, n = std::min<int64_t>(ib + k.ti - 1, blk_.nx) - ib + 1;
+          whole.push_back(Piece{ib, n, sx, pcost(ib, n, sx), is_boundary(ib, ib + n - 1, sx)});
+          total += whole.back().cost;
+        }
+      const int64_t minr = 8;  // shortest cut piece (its 2H fill rows cost more than it)
+      const double minc = double(minr + 2 * H) + overhead;
+      W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(total / minc)) / dev::kWPB) * dev::kWPB);
+      const double cut_cost = double(2 * H) + overhead;  // a cut's extra (uniform) row steps
+      int cuts = 0;
+      for (int pass = 0; pass < 4; ++pass) {
+        const double T = (total + cuts * cut_cost) / W;
+        pcs.clear();
+        per.assign(size_t(W), {});
+        load.assign(size_t(W), 0.0);
+        nbnd = 0;
+        int ncut = 0;
+        struct QE {
+          double cost;
+          int seq;
+          Piece p;
+          bool operator<(const QE& o) const { return cost < o.cost || (cost == o.cost && seq > o.seq); }
+        };
+        std::priority_queue<QE> q;
+        for (int i = 0; i < int(whole.size()); ++i) {
+          const Piece& p = whole[size_t(i)];
+          if (p.bnd) {  // boundary pieces: positions 0, 1, … in order (first round)
+            per[size_t(nbnd % W)].push_back(int(pcs.size()));
+            load[size_t(nbnd % W)] += p.cost;
+            pcs.push_back(p);
+            ++nbnd;
+          } else {
+            q.push(QE{p.cost, i, p});
+          }
+        }
+        using LW = std::pair<double, int>;
+        std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
+        for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
+        while (!q.empty()) {
+          QE e = q.top();
+          q.pop();
+          const LW t = heap.top();
+          heap.pop();
+          const double room = T - t.first;
+          Piece give = e.p;
+          if (e.p.cost > room && room >= minc && e.p.rows >= 2 * minr) {
+            // the most rows of e.p that fit the room (binary search; cost grows with rows)
+            int64_t lo = minr, hi = e.p.rows - minr, best = 0;
+            while (lo <= hi) {
+              const int64_t mid = (lo + hi) / 2;
+              if (pcost(e.p.ib, mid, e.p.s) <= room) {
+                best = mid;
+                lo = mid + 1;
+              } else {
+                hi = mid - 1;
+              }
+            }
+            if (best > 0) {
+              give = Piece{e.p.ib, best, e.p.s, pcost(e.p.ib, best, e.p.s), false};
+              const Piece rest{e.p.ib + best, e.p.rows - best, e.p.s, pcost(e.p.ib + best, e.p.rows - best, e.p.s), false};
+              q.push(QE{rest.cost, e.seq, rest});
+              ++ncut;
+            }
+          }
+          per[size_t(t.second)].push_back(int(pcs.size()));
+          pcs.push_back(give);
+          heap.push(LW{t.first + give.cost, t.second});
+        }
+        if (ncut == cuts) break;
+        cuts = ncut;
+      }
+      lay_cuts_ = cuts;
+    } else {
+    per.assign(size_t(W), {});
+    load.assign(size_t(W), 0.0);
+    std::vector<int> order;
     for (int i = 0; i < int(pcs.size()); ++i) {
       if (pcs[size_t(i)].bnd) {  // boundary pieces: positions 0, 1, … in order
         per[size_t(nbnd % W)].push_back(i);
@@ -314,6 +416,8 @@ void DeviceSolver::setup_items() {
       heap.pop();
       per[size_t(t.second)].push_back(i);
       heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
+    }
+    lay_cuts_ = 0;
     }
     size_t rounds = 0;
     for (const auto& v : per) rounds = std::max(rounds, v.size());

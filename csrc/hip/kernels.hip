@@ -487,6 +487,92 @@ __global__ __launch_bounds__(TJ) void kError(KParams k) {
   }
 }
 
+// True-residual check of a single-sweep-layout solve (DeviceSolver::residual_pass):
+// ρ = B − A w on the owned nodes, w read from the p-plane of x[bw] (kWtoP
+// copied it there and the sweep's halo exchange filled its halo), the
+// recurrence's r from the r-plane of x[st->wpar] (with_r).  Unweighted sums
+// into st->res = {Σρ², Σr², Σ(ρ − r)², ΣB²}, block partials summed
+// in block order (deterministic).  store: ρ → the r-plane of x[bw] (the
+// three-step restart's r⁰; this kernel reads no r there).
+__global__ __launch_bounds__(TJ) void kResid(KParams k, int bw, int with_r, int store) {
+  __shared__ double sm[16];
+  __shared__ int sflag;
+  DevState* st = k.st;
+  const int64_t n = k.nx * k.ny;
+  const double* wv = k.x[bw] + k.poff;
+  const double* xr = k.x[with_r ? st->wpar : bw];
+  double a[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int64_t idx = int64_t(blockIdx.x) * TJ + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * TJ) {
+    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
+    const double x = k.A1 + (k.gi0 + li) * k.h1, y = k.A2 + (k.gj0 + lj) * k.h2;
+    const CS c = cset_mem<false>(k, li, lj);
+    const int64_t at = li * k.pitch + lj;
+    const double B = in_ellipse(x, y, k.cx, k.cy) ? k.F : 0.0;
+    const double rho = B - stencil<false>(k, c, wv[at - k.pitch], wv[at], wv[at + k.pitch], wv[at - 1], wv[at + 1]);
+    a[0] += rho * rho;
+    a[3] += B * B;
+    if (with_r) {
+      const double r = xr[at];
+      a[1] += r * r;
+      a[2] += (rho - r) * (rho - r);
+    }
+    if (store) k.x[bw][at] = rho;
+  }
+  block_reduce<4, false>(a, sm);
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) k.partial[4 * size_t(blockIdx.x) + q] = a[q];
+  if (arrive_last(&st->ticket[3], gridDim.x, &sflag)) {
+    double t[4];
+    reduce_partials<4>(k.partial, gridDim.x, t, sm);
+    if (threadIdx.x == 0) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) st->res[q] = t[q];
+      __hip_atomic_store(&st->ticket[3], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// w (owned nodes) → the p-plane of x[b] (kResid's operand).
+__global__ __launch_bounds__(TJ) void kWtoP(KParams k, int b) {
+  const int64_t n = k.nx * k.ny;
+  double* dst = k.x[b] + k.poff;
+  for (int64_t idx = int64_t(blockIdx.x) * TJ + threadIdx.x; idx < n; idx += int64_t(gridDim.x) * TJ) {
+    const int64_t li = idx / k.ny + 1, lj = idx % k.ny + 1;
+    dst[li * k.pitch + lj] = k.w[li * k.wpitch + lj];
+  }
+}
+
+// p-plane of x[b] ← 0 over every allocated row and column (halos included):
+// rows 1-hdep .. nx+hdep+2, columns 1-hdep .. poff-hdep.
+__global__ __launch_bounds__(TJ) void kZeroP(KParams k, int b) {
+  const int64_t h = k.hdep, rows = k.nx + 2 * h + 2, cols = k.poff;
+  double* base = k.x[b] + k.poff - (h - 1) * k.pitch - (h - 1);
+  for (int64_t idx = int64_t(blockIdx.x) * TJ + threadIdx.x; idx < rows * cols; idx += int64_t(gridDim.x) * TJ)
+    base[(idx / cols) * k.pitch + idx % cols] = 0.0;
+}
+
+// Three-step restart (residual replacement): the solve goes on from the
+// current iteration with a fresh recurrence — S_0 next (started = 0), no
+// pending stop tests, and β = 0 for the iteration after k0 (fused3.hip).
+__global__ void kRestart3(KParams k) {
+  DevState* st = k.st;
+  st->done = 0;
+  st->status = 0;
+  st->started = 0;
+  st->late3 = 0;
+  st->brk3 = 0;
+  st->bad3 = 0;
+  st->wpend = 0;
+  st->fixj = 0;
+  st->k0 = st->iter;
+}
+
+// PE_FAULT_INJECT=drift@iter:K (test hook): w(li, lj) += v behind the
+// recurrence's back — its r no longer is B − A w, which the end-of-solve
+// residual check must see (and the three-step solve restart from).
+__global__ void kPokeW(KParams k, int64_t li, int64_t lj, double v) { k.w[li * k.wpitch + lj] += v; }
+
 __global__ void kGroupReduce(double* const* bufs, int nranks, int n, int is_max) {
   const int i = threadIdx.x;
   if (i >= n) return;
@@ -595,6 +681,20 @@ void launch_copy_words(void* dst, const void* src, size_t bytes, bool to_host, h
 
 void launch_error(const KParams& k, hipStream_t s) {
   hipLaunchKernelGGL(kError, dim3(flat_blocks(k)), dim3(TJ), 0, s, k);
+}
+
+void launch_resid(const KParams& k, int bw, bool with_r, bool store, hipStream_t s) {
+  hipLaunchKernelGGL(kResid, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, bw, with_r ? 1 : 0, store ? 1 : 0);
+}
+void launch_w_to_p(const KParams& k, int b, hipStream_t s) {
+  hipLaunchKernelGGL(kWtoP, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, b);
+}
+void launch_zero_p(const KParams& k, int b, hipStream_t s) {
+  hipLaunchKernelGGL(kZeroP, dim3(flat_blocks(k)), dim3(TJ), 0, s, k, b);
+}
+void launch_restart3(const KParams& k, hipStream_t s) { hipLaunchKernelGGL(kRestart3, dim3(1), dim3(1), 0, s, k); }
+void launch_poke_w(const KParams& k, int64_t li, int64_t lj, double v, hipStream_t s) {
+  hipLaunchKernelGGL(kPokeW, dim3(1), dim3(1), 0, s, k, li, lj, v);
 }
 
 void launch_group_reduce(double* const* bufs, int nranks, int n, int is_max, hipStream_t s) {

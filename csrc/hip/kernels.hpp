@@ -67,6 +67,18 @@ struct DevState {
   long long brk3;
   int late3;
   int bad3;
+  // End-of-solve true-residual check (kResid): unweighted sums over the
+  // owned nodes {Σρ², Σr², Σ(ρ − r)², ΣB²} of ρ = B − A w (the returned w)
+  // and r the recurrence's residual of the same iterate (three-step).
+  double res[4];
+  // Three-step restart (residual replacement): β of iteration k0 + 1 is 0.
+  long long k0;
+  // Three-step fix-up: the iterations of the last sweep it kept (0: the
+  // solve ended on a sweep's last iteration — no fix-up).  The replay launch
+  // (mlimit == kReplay3) then recomputes x[wpar] = (r, p) of that iterate,
+  // so the end-of-solve residual check compares w with ITS r.
+  int fixj;
+  int pad4;
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
@@ -190,6 +202,8 @@ struct KParams {
   int mlimit;
 };
 constexpr int kFoldGroup = 64;
+// KParams::mlimit of the three-step replay launch (DevState::fixj)
+constexpr int kReplay3 = -2;
 
 constexpr int kTJ = 256;         // threads per block (4 wave64s)
 constexpr int kWPB = 4;          // waves per block
@@ -254,6 +268,13 @@ void launch_init(const KParams& k, int init_random, unsigned long long seed, dou
 void launch_F(const KParams& k, int par, int variant, hipStream_t s);
 void launch_G(const KParams& k, int par, int variant, hipStream_t s);
 void launch_error(const KParams& k, hipStream_t s);
+// True residual ρ = B − A w (w from the p-plane of x[bw], halo exchanged; r
+// from x[st->wpar] when with_r) → st->res; store: ρ → x[bw]'s r-plane.
+void launch_resid(const KParams& k, int bw, bool with_r, bool store, hipStream_t s);
+void launch_w_to_p(const KParams& k, int b, hipStream_t s);   // owned w → the p-plane of x[b]
+void launch_zero_p(const KParams& k, int b, hipStream_t s);   // the p-plane of x[b] ← 0 (halos included)
+void launch_restart3(const KParams& k, hipStream_t s);        // three-step restart state (kRestart3)
+void launch_poke_w(const KParams& k, int64_t li, int64_t lj, double v, hipStream_t s);  // fault hook
 // 4-byte-word copy by a kernel (bytes % 4 == 0); either side may be pinned
 // host memory (to_host: system-scope fence after the stores).
 void launch_copy_words(void* dst, const void* src, size_t bytes, bool to_host, hipStream_t s);

@@ -190,6 +190,7 @@ class DeviceSolver {
   // static layout: {most loaded wave, mean wave load, max items on a wave}
   // in row-step cost units (0s for a dynamic layout)
   std::vector<double> layout_load() const { return {lay_max_, lay_mean_, double(lay_items_)}; }
+  int layout_cuts() const { return lay_cuts_; }
   hipStream_t stream() const { return stream_; }
 
   // Checkpoint / resume of the full device state of this rank (raw fields,
@@ -233,6 +234,11 @@ class DeviceSolver {
   void enqueue_exchange(int buf, bool after_sweep = true);
   void setup_halo_push();  // collective: decides push_ identically on every rank
   void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
+  // End-of-solve true residual (single-sweep layouts): w → the p-plane of
+  // x[0], the sweep's halo exchange, then kResid into DevState::res
+  // (with_r: against the recurrence's r; store: ρ → x[0]'s r-plane) and the
+  // cross-rank sum of the four sums.
+  void residual_pass(bool with_r, bool store);
   void wait_event(hipEvent_t ev);  // event wait with transport-error polling + watchdog
   void enqueue_chunk(int iters, int sample_iters = 0);
   // Sampled phase timing (Timers): hipEvent pairs around the phases of the
@@ -302,6 +308,12 @@ class DeviceSolver {
   int par_ = 0;  // parity of the next iteration (x / p ping-pong)
   double watchdog_s_ = 0;   // PE_WATCHDOG_S: abort if a chunk makes no progress this long (0 = off)
   bool fault_stall_ = false;  // PE_FAULT_INJECT=stall: pretend the device never finishes (watchdog test)
+  // PE_FAULT_INJECT=drift@iter:K,amp:X — w(M/2, N/2) += X once the host has
+  // enqueued iteration K (the residual check's test hook)
+  long long fault_drift_ = 0;
+  double fault_drift_amp_ = 1e-6;
+  // three-step restart threshold on ‖B − A w − r‖_E / ‖B‖_E (PE_RESID_GAP)
+  double gap_bound_ = 1e-6;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t ev_sync_ = nullptr;  // synchronize() under the watchdog
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
@@ -319,6 +331,7 @@ class DeviceSolver {
   std::vector<int> ti_rows_;      // the candidates timed
   double lay_max_ = 0, lay_mean_ = 0;  // static layout: heaviest / mean wave load (row steps)
   int lay_items_ = 0;                  // static layout: most items on one wave
+  int lay_cuts_ = 0;                   // three-step filling layout: items cut to fill the waves
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;
   bool resident_fallback_ = false;  // a resident launch aborted (status 5): switched to the streaming sweep

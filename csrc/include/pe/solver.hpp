@@ -103,6 +103,13 @@ struct SolveResult {
   std::string backend;
   std::string algo;      // device: "fused" (single-sweep) or "classic"
   bool resident_fallback = false;  // device: a resident launch aborted, the solve finished on the streaming sweep
+  // End-of-solve true-residual check (device single-sweep-layout paths; -1:
+  // not computed): E-norms ‖B − A w‖ of the returned w, ‖B‖ and (three-step)
+  // the recurrence's ‖r‖ of the same iterate and the relative gap
+  // ‖B − A w − r‖ / ‖B‖; how many times the gap restarted the three-step
+  // recurrence from w (residual replacement).
+  double res_true = -1, res_rec = -1, res_gap = -1, b_norm = -1;
+  int restarts = 0;
 };
 
 // ---- CPU backends (reference stage0..3 equivalents) -----------------------

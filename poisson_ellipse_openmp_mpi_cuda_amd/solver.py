@@ -59,6 +59,14 @@ class SolveReport:
     xr: bool = False  # the sweep sums its scalars over ranks itself (P2P transport, no allreduce launch)
     halo_push: bool = False  # the sweep pushes its edge rows to the neighbours over xGMI (no exchange call)
     resident_fallback: bool = False  # a resident launch aborted (barrier timeout); the solve finished streaming
+    # end-of-solve true-residual check (device single-sweep-layout paths, -1: not computed): E-norm of
+    # B - A w for the returned w, ||B||, and (three-step) the recurrence's ||r|| of the same iterate, the
+    # gap ||B - A w - r|| / ||B||, and the restarts (residual replacement) the gap triggered
+    res_true: float = -1.0
+    res_rec: float = -1.0
+    res_gap: float = -1.0
+    b_norm: float = -1.0
+    restarts: int = 0
 
     @property
     def iters_per_s(self) -> float:
@@ -104,7 +112,10 @@ def _report(backend, prob, res, ranks, threads, init, w=None, rank=0) -> SolveRe
         max_err=float(res.max_err), max_outside=float(res.max_outside), init=init, w=w, rank=rank,
         algo=str(getattr(res, "algo", "")), nonfinite=bool(getattr(res, "nonfinite", False)),
         history=list(res.history) if len(res.history) else None,
-        resident_fallback=bool(getattr(res, "resident_fallback", False)))
+        resident_fallback=bool(getattr(res, "resident_fallback", False)),
+        res_true=float(getattr(res, "res_true", -1.0)), res_rec=float(getattr(res, "res_rec", -1.0)),
+        res_gap=float(getattr(res, "res_gap", -1.0)),
+        b_norm=float(getattr(res, "b_norm", -1.0)), restarts=int(getattr(res, "restarts", 0)))
 
 
 def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: int = 1, decomp: str | None = None,

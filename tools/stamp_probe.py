@@ -105,6 +105,25 @@ def summarise(st: np.ndarray, nitems: int, nw: int) -> str:
     band = (geo >> 48) == 1
     if band.any():
         out.append(f"  band items: {band.sum()}  duration median {np.median(dur[band]):6.2f} us; others {np.median(dur[~band]):6.2f} us")
+    # per item kind (three-step sweep: 0 mixed, 1 band, 2 uniform): time per row step
+    # of the march (rows + 2*halo fill steps) -> the layout's cost model
+    rows = (geo >> 32) & 0xFFFF
+    kind = geo >> 48
+    halo = int(os.environ.get("PROBE_HALO", "6"))
+    for kd, name in ((2, "uniform"), (0, "mixed"), (1, "band")):
+        m = kind == kd
+        if m.any():
+            per = dur[m] / (rows[m] + 2 * halo)
+            # least squares dur = a * steps + b
+            A = np.stack([rows[m] + 2 * halo, np.ones(m.sum())], 1).astype(float)
+            coef = np.linalg.lstsq(A, dur[m], rcond=None)[0] if m.sum() > 2 else (float("nan"), float("nan"))
+            out.append(f"  kind {name:7s}: {m.sum():6d} items  us per row step median {np.median(per):6.3f} p90 {pct(per, 90):6.3f}"
+                       f"  fit {coef[0]:6.3f} us/step + {coef[1]:6.2f} us")
+    wl = np.zeros(int(it[:, 2].max()) + 1)
+    np.add.at(wl, it[:, 2], dur)
+    wl = wl[wl > 0]
+    out.append(f"  wave item time: max {wl.max():7.1f}  mean {wl.mean():7.1f}  = {wl.max() / wl.mean():5.3f};"
+               f" p10 {pct(wl, 10):7.1f} p90 {pct(wl, 90):7.1f} us")
     out.append(step_timeline(steps))
     return "\n".join(out)
 
