@@ -222,7 +222,13 @@ def main(argv=None) -> int:
     me = {"rank": rank, "local_rank": local, "device": dev, "pci_bus_id": nat.device_pci_bus_id(dev),
           "block": [blk.nx, blk.ny],
           "placement_ms_per_sweep": [round(x, 4) for x in solver.placement_ms],
-          "placement_chosen": solver.placement_choice, "construct_s": round(solver.construct_s, 3)}
+          "placement_chosen": solver.placement_choice, "construct_s": round(solver.construct_s, 3),
+          # first cross-device run diagnostics: peer access toward every rank
+          # (1/0, -1 same device), the neighbours, what each self-tested
+          # transport set-up decided and what the sweep finally uses
+          "neighbors": {d: int(blk.nbr[i]) for i, d in enumerate(("left", "right", "down", "up")) if blk.nbr[i] >= 0},
+          "peer_access": {str(r): int(v) for r, v in enumerate(solver.peer_access)},
+          "p2p_sum_setup": nat.p2p_setup_status(), "halo_push": solver.push_status, "sums": solver.xr_status}
     ranks_info = gather(me)
 
     # warmup: first-touch / RCCL connections, then (--launch graph)

@@ -102,6 +102,9 @@ int main(int argc, char** argv) {
               << P.M << ", N=" << P.N << std::endl;
 
   SolveResult r;
+  // rank 0's transport diagnostics (first cross-device run: what each
+  // self-tested set-up decided, peer access toward every rank)
+  std::string diag = "\"halo_push\": \"off: one rank\", \"sums\": \"none\"";
   if (vranks > 1) {
     r = device_solve_group(P, process_grid_from_spec(decomp, vranks, P.M, P.N), opt);
   } else {
@@ -118,6 +121,12 @@ int main(int argc, char** argv) {
     // (SolveResult) + teardown (the frees), as the reference's time_solver
     // (poisson_mpi_cuda2.cu:1010-1016)
     auto solver = std::make_unique<DeviceSolver>(P, blk, comm.get(), opt);
+    {
+      std::string pa;
+      for (int v : solver->peer_access()) pa += (pa.empty() ? "" : ", ") + std::to_string(v);
+      diag = "\"p2p_sum_setup\": \"" + p2p_setup_status() + "\", \"halo_push\": \"" + solver->push_status() +
+             "\", \"sums\": \"" + solver->xr_status() + "\", \"peer_access\": [" + pa + "]";
+    }
     r = solver->solve();
     const auto t_free = std::chrono::steady_clock::now();
     solver.reset();
@@ -132,12 +141,12 @@ int main(int argc, char** argv) {
                   "\"t_reduce\": %.6f, \"timer_samples\": %.0f, "
                   "\"iters_per_s\": %.3f, \"l2_err\": %.6e, \"max_err\": %.6e, \"max_outside\": %.6e, \"total\": %.6f, "
                   "\"algo\": \"%s\", \"res_true\": %.6e, \"res_rec\": %.6e, \"res_gap\": %.6e, "
-                  "\"b_norm\": %.6e, \"restarts\": %d}\n",
+                  "\"b_norm\": %.6e, \"restarts\": %d, %s}\n",
                   P.M, P.N, size * vranks, r.Px, r.Py, (long long)r.iters, r.converged ? "true" : "false", r.t.solver,
                   r.t.setup, r.t.construct, r.t.iterate, r.t.gpu, r.t.dot, r.t.dot_fused ? "true" : "false", r.t.copy,
                   r.t.halo, r.t.reduce, r.t.sampled, r.iters / std::max(1e-12, r.t.iterate), r.l2_err, r.max_err,
                   r.max_outside, total, r.algo.c_str(), r.res_true, r.res_rec, r.res_gap, r.b_norm,
-                  r.restarts);
+                  r.restarts, diag.c_str());
     } else {
       std::cout << format_result_legacy(P, r, size, "stage4");
       std::printf("   Process grid %dx%d | iters/s ~ %.1f | L2 error in D ~ %.6e | max error in D ~ %.6e\n", r.Px, r.Py,

@@ -195,6 +195,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("timers", [](const SolveResult& r) { return timers_dict(r.t); });
 
   m.def("format_result_legacy", &format_result_legacy);
+  m.def("p2p_setup_status", []() { return p2p_setup_status(); },
+        "the last P2P transport set-up of this process: not attempted / ok / fallback: why");
 
   // ---- CPU backends ------------------------------------------------------
   m.def(
@@ -450,6 +452,10 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("layout_cuts", &DeviceSolver::layout_cuts)
+      .def_property_readonly("peer_access", &DeviceSolver::peer_access,
+                             "hipDeviceCanAccessPeer toward each rank's device (1/0; -1 same device)")
+      .def_property_readonly("push_status", &DeviceSolver::push_status, "halo push: on / off: why / fallback: why")
+      .def_property_readonly("xr_status", &DeviceSolver::xr_status, "transport of the per-sweep sums")
       .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def_property_readonly("halo_push", &DeviceSolver::halo_push,
                              "halo rows pushed by the sweep over xGMI (no exchange call; graph-capturable)")

@@ -103,6 +103,17 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
                   h.variant == opt_.variant && h.i0 == blk_.i0 && h.j0 == blk_.j0 && h.nx == blk_.nx &&
                   h.ny == blk_.ny && h.state_bytes == int64_t(sizeof(DevState)) &&
                   h.field_bytes == int64_t(field_bytes) && h.halo_bytes == int64_t(sizeof(double) * hsize_ * 4);
+  const int mine = sstep_ ? steps_ : fused_ ? 1 : 0;
+  if (!ok && std::memcmp(h.magic, "PECKPT1", 8) == 0 && h.fused != mine) {
+    // the usual mismatch: a checkpoint of another sweep layout (e.g. one
+    // written before the default became the three-step sweep)
+    static const char* algo[4] = {"classic", "fused", "two-step", "three-step"};
+    const int hf = int(h.fused);
+    std::fclose(f);
+    throw std::runtime_error("resume: " + path + " has the " + (hf >= 0 && hf < 4 ? algo[hf] : "?") +
+                             " layout (steps=" + std::to_string(hf) + "), this solver runs " + algo[mine] +
+                             " (steps=" + std::to_string(mine) + "); pass --algo " + (hf >= 0 && hf < 4 ? algo[hf] : "?"));
+  }
   if (!ok) {
     std::fclose(f);
     throw std::runtime_error("resume: " + path + " does not match this problem / block / algorithm");

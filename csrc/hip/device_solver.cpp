@@ -136,6 +136,28 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   mark("start");
   PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
   mark("stream");
+  // Peer access of this rank's device toward every rank's (first cross-device
+  // run diagnostics: the halo push and the in-sweep sums map peers' memory):
+  // 1 / 0 hipDeviceCanAccessPeer, -1 the same device.
+  if (comm_->size() > 1) {
+    const int P = comm_->size();
+    int mydev = 0;
+    PE_HIP_CHECK(hipGetDevice(&mydev));
+    std::vector<double> ids(size_t(P), -1.0);
+    ids[size_t(comm_->rank())] = double(mydev);
+    comm_->host_max(ids.data(), P, stream_);
+    peer_access_.assign(size_t(P), -1);
+    for (int r = 0; r < P; ++r) {
+      const int d = int(ids[size_t(r)]);
+      if (d == mydev || d < 0) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, mydev, d) != hipSuccess) {
+        (void)hipGetLastError();
+        can = 0;
+      }
+      peer_access_[size_t(r)] = can;
+    }
+  }
   KParams& k = *kp_;
   std::memset(&k, 0, sizeof(KParams));
   const int64_t nx = blk_.nx, ny = blk_.ny;
@@ -463,13 +485,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // In-sweep cross-rank reduction (after the placement search, whose sweeps
   // are local and differ in number between ranks).  PE_XR=0 keeps the
   // separate allreduce launch.
+  xr_status_ = comm_->size() < 2 ? "none: one rank" : "allreduce launch (" + comm_->name() + ")";
   if (fused_ && comm_->size() > 1 && comm_->peer_sum()) {
     const char* e = std::getenv("PE_XR");
     if (!(e && std::atoi(e) == 0)) {
       k.xr = *comm_->peer_sum();
       k.xr.wait_acc = &st_->xr_wait;  // T_MPI of the in-sweep sum (DevState::xr_wait, xr_n)
+      xr_status_ = "in-sweep P2P over xGMI";
     }
   }
+  if (fused_ && comm_->size() > 1 && !comm_->peer_sum()) xr_status_ += "; P2P set-up " + p2p_setup_status();
   // In-kernel item-sum fold for dynamic sweeps, opt-in (PE_FOLD=1): it saves
   // the reduction kernel (≈10 µs + a launch gap per iteration at 8192²) but
   // its per-item publication (drained write-through stores + a returning
@@ -545,10 +570,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 // map_peer_buffers (collective) or none does.  PE_HALO=exchange opts out.
 void DeviceSolver::setup_halo_push() {
   push_ = false;
-  if (!fused_ || comm_->size() < 2 || !comm_->peer_sum() || blk_.Py != 1) return;
+  push_status_ = comm_->size() < 2 ? "off: one rank" : !fused_ ? "off: classic path" : !comm_->peer_sum()
+                 ? "off: no P2P transport (" + p2p_setup_status() + ")" : blk_.Py != 1 ? "off: 2-D blocks (RCCL exchange)"
+                 : "";
+  if (!push_status_.empty()) return;
+  push_status_ = "off: slabs thinner than 2 halo depths";
   if ((prob_.M - 1) / blk_.Px < 2 * hdep_) return;  // edge rows 1..h and nx-h+1..nx distinct
+  push_status_ = "off: PE_XR=0";
   if (const char* e = std::getenv("PE_XR"); e && std::atoi(e) == 0) return;
+  push_status_ = "off: PE_HALO=exchange";
   if (const char* e = std::getenv("PE_HALO"); e && std::string(e) == "exchange") return;
+  push_status_ = "fallback: the receive buffers could not be mapped on every rank";
   const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);  // [parity][side][hdep rows]
   void* buf = nullptr;
   if (hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
@@ -567,6 +599,7 @@ void DeviceSolver::setup_halo_push() {
   }
   hrecv_ = static_cast<double*>(buf);
   push_ = true;
+  push_status_ = "on";
   // Collective self-test of the path, in its own store / load forms: every
   // rank fills its neighbours' receive buffers with rank-coded values, the
   // ranks synchronise, every rank checks what arrived; all ranks keep the
@@ -609,6 +642,7 @@ void DeviceSolver::setup_halo_push() {
     comm_->barrier(stream_);
     if (fail[0] != 0.0) {
       if (blk_.rank == 0) std::fprintf(stderr, "[pe] halo push unavailable on this job (self-test), using the exchange\n");
+      push_status_ = hbad ? "fallback: self-test failed on this rank" : "fallback: self-test failed on a peer";
       comm_->unmap_peer_buffers(hpeers_);
       hpeers_.clear();
       PE_HIP_CHECK(hipFree(buf));
@@ -924,6 +958,7 @@ void DeviceSolver::enqueue_iteration(int par, int mlimit) {
     for (int x = 0; x < 8; ++x) ko.lnb[x] = ov_lnb_[x];
     ko.nblocks = std::max(ov_lnsh_, kp_->nblocks - ov_reserve_);
     ko.nblocks0 = std::max(ov_lnsh_, kp_->nblocks0 - ov_reserve_);
+    ko.mlimit = mlimit;
     ov_epoch_ += 1;
     const unsigned long long target = ov_epoch_ * (unsigned long long)(ov_nb_);
     mark_begin(kPhSweep, stream_);
@@ -942,6 +977,7 @@ void DeviceSolver::enqueue_iteration(int par, int mlimit) {
     } else {
       dev::launch_wait_sig(ko, target, hs_);  // the exchange starts once they are stored
       mark_begin(kPhHalo, hs_);
+      if (sstep_) dev::launch_pack(*kp_, par, hs_);  // (multi-step: y strips packed after the boundary items)
       for (const HaloPhase& ph : halo_phases(par)) {
         comm_->exchange(ph.ex, hs_);
         if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
@@ -1280,31 +1316,27 @@ SolveResult DeviceSolver::solve() {
         continue;
       }
       if (res_abort) {
-        // Resident fallback: the aborted launch wrote nothing back (and the
-        // chunk after it saw `done` and did nothing), so the device holds the
-        // state from before it.  Clear the abort, switch this solver to the
-        // streaming sweep and continue from that iteration.
+        // Resident fallback: a workgroup of a resident launch timed out at a
+        // grid barrier.  The aborted launch may still have written back part
+        // of the grid (a late workgroup passes the barrier the others gave up
+        // on), so its state is not resumed: the solve starts over from its
+        // initial state (or its checkpoint) on the streaming sweep.
         res_abort = false;
         DevState s0;
         read_state(&s0);
-        if (s0.status == 5) {
-          std::fprintf(stderr, "[pe] rank %d: resident kernel barrier timed out at iteration %lld; "
-                               "continuing with the streaming sweep\n", blk_.rank, (long long)s0.iter);
-          PE_HIP_CHECK(hipMemsetAsync(reinterpret_cast<char*>(st_) + offsetof(DevState, done), 0, 2 * sizeof(int),
-                                      stream_));
-          resident_ = false;
-          resident_fallback_ = true;
-          chunk_ = stream_chunk_;
-          par_ = int(s0.iter & 1);
-          enq = s0.iter;
-          // the drained records: keep the samples of the iterations that ran
-          harvest(recs_.size());
-          samples_.erase(std::remove_if(samples_.begin(), samples_.end(),
-                                        [&](const PhaseSample& x) { return x.iter >= s0.iter; }),
-                         samples_.end());
-          stop = false;
-          continue;
-        }
+        std::fprintf(stderr, "[pe] rank %d: resident kernel barrier timed out by iteration %lld; "
+                             "restarting the solve with the streaming sweep\n", blk_.rank, (long long)s0.iter);
+        resident_ = false;
+        resident_fallback_ = true;
+        chunk_ = stream_chunk_;
+        harvest(recs_.size());
+        samples_.clear();
+        if (!opt_.resume_path.empty()) load_checkpoint(opt_.resume_path + ".r" + std::to_string(blk_.rank));
+        else reset();
+        enq = start_iter;
+        sample_iter_ = start_iter;
+        stop = false;
+        continue;
       }
       break;
     }
@@ -1317,7 +1349,7 @@ SolveResult DeviceSolver::solve() {
     for (Flight& g : inflight) g.nrec -= std::min(g.nrec, done_recs);
     if (hst_[f.slot].done) {
       stop = true;
-      if (hst_[f.slot].status == 5 && resident_) res_abort = true;
+      if ((hst_[f.slot].status == 5 || hst_[f.slot].res_abort) && resident_) res_abort = true;
     }
     if (opt_.log_every > 0 && blk_.rank == 0 && hst_[f.slot].iter >= next_log) {  // chunk-granular progress log
       std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[f.slot].iter,
@@ -1359,6 +1391,7 @@ SolveResult DeviceSolver::solve() {
                  blk_.rank, res.res_gap, gap_bound_, (long long)hs.iter);
     dev::launch_zero_p(*kp_, 0, stream_);
     dev::launch_restart3(*kp_, stream_);
+    ov_epoch_ = 0;
     dev::launch_pack(*kp_, 0, stream_);
     enqueue_exchange(0, false);
     dev::launch_S(*kp_, 1, stream_);

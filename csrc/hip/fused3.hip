@@ -724,15 +724,23 @@ __device__ __forceinline__ unsigned long long rtc3() {
 }
 
 // Walk this wave's positions of the static item list.
-// STAMP — diagnostic build (PE_STAMPS=1, tools/stamp_probe.py): lane 0 of
-// every wave records s_memrealtime at its entry and exit and at the start and
-// end of every item into k.stamps (the single sweep's layout: per position
-// {start, end, wave | strip << 32, first row | rows << 32 | kind << 48}, kind
-// 1 band, 2 uniform, 0 mixed; then per wave {entry, exit}).  Never the
-// production kernel.
-template <bool PUSH, bool STAMP>
+// Kernel variants (separate instantiations, so the production march is the
+// plain one): kPlain; kStamp — diagnostic build (PE_STAMPS=1,
+// tools/stamp_probe.py): lane 0 of every wave records s_memrealtime at its
+// entry and exit and at the start and end of every item into k.stamps (the
+// single sweep's layout: per position {start, end, wave | strip << 32, first
+// row | rows << 32 | kind << 48}, kind 1 band, 2 uniform, 0 mixed; then per
+// wave {entry, exit}); kReplay — the end-of-solve replay (kReplay3); kSignal
+// — halo/interior overlap: the first k.lnb[0] positions of the static list
+// are boundary items (outputs a neighbour needs), each of which bumps st->sig
+// once its stores have left the wave (kWaitSig on the halo stream then
+// writes the L2s back and the exchange starts while interior items run).
+enum { kPlain = 0, kStamp = 1, kReplay = 2, kSignal = 3 };
+
+template <bool PUSH, int MODE>
 __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fix, int par, WaveTV3& tv, int wid,
                                       double (&acc)[NS]) {
+  constexpr bool STAMP = MODE == kStamp;
   const int W = k.lwaves;
   const int gwave = int(blockIdx.x) * kWPB + wid;
   const bool l0 = (threadIdx.x & 63) == 0;
@@ -758,6 +766,12 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     } else {
       march3<kMixed, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     }
+    if constexpr (MODE == kSignal) {
+      if (pos < k.lnb[0]) {  // a boundary item: count it once its stores have left (no L2 writeback here)
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (l0) __hip_atomic_fetch_add(&k.st->sig, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+    }
     if constexpr (STAMP) {
       if (l0) {
         const unsigned long long kind = (e.x & kBandBit) ? 1ull : (e.x & kUniBit) ? 2ull : 0ull;
@@ -774,7 +788,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   }
 }
 
-template <bool PUSH, bool STAMP = false>
+template <bool PUSH, int MODE = kPlain>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
@@ -783,7 +797,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   __shared__ WaveTV3 tvs[kWPB];
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
-  const bool replay = k.mlimit == kReplay3;
+  constexpr bool replay = MODE == kReplay;
   if (done && !replay) return;
   auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
                             // the slots garbage pipeline-fill rows read stay finite)
@@ -810,7 +824,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   Scal3 sc = {};
   bool fix = false;
   int rpar = par;
-  if (replay) {
+  if constexpr (replay) {
     // After a fix-up (the solve stopped at iteration j of its last sweep):
     // march the last sweep's inputs again with its first j iterations and
     // identity steps after them (zc = 0, β = 1, α = 0), w untouched, storing
@@ -871,7 +885,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     cf = sc.c;
   }
   zero_ring();
-  walk3<PUSH, STAMP>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
   if (replay) return;
   if (fix) {
     finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);
@@ -911,9 +925,19 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
 }  // namespace
 
 void launch_S3(const KParams& k, int par, hipStream_t s) {
-  if (k.stamps && !k.push) hipLaunchKernelGGL((kS3<false, true>), dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
-  else if (k.push) hipLaunchKernelGGL(kS3<true>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
-  else hipLaunchKernelGGL(kS3<false>, dim3(unsigned(k.nblocks)), dim3(TJ), 0, s, k, par);
+  const dim3 g(unsigned(k.nblocks)), b(TJ);
+  if (k.mlimit == kReplay3) {
+    if (k.push) hipLaunchKernelGGL((kS3<true, kReplay>), g, b, 0, s, k, par);
+    else hipLaunchKernelGGL((kS3<false, kReplay>), g, b, 0, s, k, par);
+  } else if (k.stamps && !k.push) {
+    hipLaunchKernelGGL((kS3<false, kStamp>), g, b, 0, s, k, par);
+  } else if (k.lnb[0] > 0 && !k.push) {
+    hipLaunchKernelGGL((kS3<false, kSignal>), g, b, 0, s, k, par);
+  } else if (k.push) {
+    hipLaunchKernelGGL((kS3<true, kPlain>), g, b, 0, s, k, par);
+  } else {
+    hipLaunchKernelGGL((kS3<false, kPlain>), g, b, 0, s, k, par);
+  }
 }
 
 int resident_blocks_S3() {

@@ -77,7 +77,9 @@ void DeviceSolver::setup_items() {
   // PE_OVERLAP=1 / 0 forces it on / off.
   const char* e = std::getenv("PE_OVERLAP");
   overlap_ = false;
-  if (fused_ && !sstep_ && comm_->size() > 1 && nb && !push_) {  // (the two-step sweep runs without the overlap)
+  // (the two-step sweep runs without the overlap; the three-step sweep's
+  // boundary items count themselves in its kSignal variant, fused3.hip)
+  if (fused_ && (!sstep_ || steps_ == 3) && comm_->size() > 1 && nb && !push_) {
     if (e) {
       overlap_ = std::atoi(e) != 0;
     } else {
@@ -178,9 +180,10 @@ void DeviceSolver::setup_items() {
   auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
     const int64_t J = -(H - 1) + int64_t(s) * fsw_;
     const int64_t jlo = std::max<int64_t>(1, J + H), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + H - 1);
+    // (the H owned rows / columns next to a neighbour: what the exchange sends)
     return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
-           ((blk_.has(LEFT) && ib <= 2) || (blk_.has(RIGHT) && ie >= blk_.nx - 1) || (blk_.has(DOWN) && jlo <= 2) ||
-            (blk_.has(UP) && jhi >= blk_.ny - 1));
+           ((blk_.has(LEFT) && ib <= H) || (blk_.has(RIGHT) && ie >= blk_.nx - H + 1) || (blk_.has(DOWN) && jlo <= H) ||
+            (blk_.has(UP) && jhi >= blk_.ny - H + 1));
   };
 
   if (k.order == 0) {
@@ -638,7 +641,11 @@ void DeviceSolver::setup_resident() {
   r.partials = res_buf_ + nedge;
   r.ctr = res_ctr_;
   r.fault_wg = -1;
-  if (const char* f = std::getenv("PE_FAULT_INJECT"); f && std::string(f) == "resbarrier") r.fault_wg = nwg - 1;
+  r.fault_late = 0;
+  if (const char* f = std::getenv("PE_FAULT_INJECT"); f && (std::string(f) == "resbarrier" || std::string(f) == "reslate")) {
+    r.fault_wg = nwg - 1;
+    r.fault_late = std::string(f) == "reslate" ? 1 : 0;
+  }
   resident_ = true;
 }
 

@@ -566,6 +566,7 @@ __global__ void kRestart3(KParams k) {
   st->wpend = 0;
   st->fixj = 0;
   st->k0 = st->iter;
+  st->sig = 0;  // (the host restarts its overlap epoch count with it)
 }
 
 // PE_FAULT_INJECT=drift@iter:K (test hook): w(li, lj) += v behind the

@@ -78,7 +78,10 @@ struct DevState {
   // (mlimit == kReplay3) then recomputes x[wpar] = (r, p) of that iterate,
   // so the end-of-solve residual check compares w with ITS r.
   int fixj;
-  int pad4;
+  // Resident kernel: a workgroup's grid-barrier wait timed out (sticky: set
+  // only by the aborting workgroups; the host falls back on it whatever the
+  // other workgroups wrote after them)
+  int res_abort;
 };
 
 // One-shot cross-rank sum over IPC-mapped receive buffers (peer_sum.hpp):
@@ -253,8 +256,11 @@ struct ResParams {
   unsigned long long* stamps;
   // PE_FAULT_INJECT=resbarrier: this workgroup never arrives at the first
   // grid barrier (-1: none) — the barrier times out, the launch aborts with
-  // status 5 and the solver must fall back to the streaming sweep
+  // status 5 and the solver must fall back to the streaming sweep.
+  // fault_late (PE_FAULT_INJECT=reslate): that workgroup arrives after the
+  // others have timed out instead, passes the barrier and writes its tile back
   int fault_wg;
+  int fault_late;
 };
 constexpr int kResStampIters = 64;
 constexpr int kResMaxTiles = 256;  // the per-iteration sum gather reads ≤ 4 × 64 tile partials

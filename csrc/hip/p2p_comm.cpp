@@ -25,6 +25,9 @@
 namespace pe {
 namespace {
 
+// What the last P2P set-up of this process decided (bench / CLI diagnostics).
+std::string g_p2p_status = "not attempted";
+
 class P2PAllreduceComm final : public DeviceComm {
  public:
   explicit P2PAllreduceComm(std::unique_ptr<DeviceComm> base) : base_(std::move(base)) {
@@ -34,7 +37,9 @@ class P2PAllreduceComm final : public DeviceComm {
     hipStream_t s = nullptr;
     PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
     bool ok = setup(P, me, s);
+    const bool mapped_here = ok;
     ok = agree(ok, s);
+    if (!ok) why_ = mapped_here ? "a peer could not map the receive buffers" : "this rank could not map the receive buffers";
     if (ok) {
       // test sum with a short timeout: rank r contributes r+1 (and -(r+1)):
       // exact in fp64, the same bits on every rank
@@ -49,7 +54,13 @@ class P2PAllreduceComm final : public DeviceComm {
       PE_HIP_CHECK(hipStreamSynchronize(s));
       PE_HIP_CHECK(hipFree(d));
       const double want = 0.5 * double(P) * double(P + 1);
-      ok = agree(h[0] == want && h[1] == -want, s);
+      bool good = h[0] == want && h[1] == -want;
+      // PE_FAULT_INJECT=p2ptest@rank:R — rank R's check fails (fallback test)
+      if (const char* e = std::getenv("PE_FAULT_INJECT"); e && std::string(e).rfind("p2ptest@rank:", 0) == 0 &&
+                                                          std::atoi(e + 13) == me)
+        good = false;
+      ok = agree(good, s);
+      if (!ok) why_ = good ? "self-test sum wrong on a peer" : "self-test sum wrong on this rank";
     }
     ps_.timeout_ticks = (long long)(timeout_s_ * 1e8);
     PE_HIP_CHECK(hipStreamDestroy(s));
@@ -62,6 +73,7 @@ class P2PAllreduceComm final : public DeviceComm {
     if (mine_) (void)hipFree(mine_);
   }
   bool ok() const { return ok_; }
+  const std::string& why() const { return why_; }
   std::unique_ptr<DeviceComm> release_base() { return std::move(base_); }
 
   int rank() const override { return base_->rank(); }
@@ -196,6 +208,7 @@ class P2PAllreduceComm final : public DeviceComm {
   dev::PeerSum ps_{};
   double timeout_s_ = 120.0;
   bool ok_ = false;
+  std::string why_;
 };
 
 }  // namespace
@@ -203,10 +216,16 @@ class P2PAllreduceComm final : public DeviceComm {
 std::unique_ptr<DeviceComm> make_p2p_allreduce_comm(std::unique_ptr<DeviceComm> base) {
   if (!base || base->size() == 1) return base;
   auto c = std::make_unique<P2PAllreduceComm>(std::move(base));
-  if (c->ok()) return c;
-  std::fprintf(stderr, "[pe] rank %d: P2P allreduce unavailable on this job, using %s\n", c->rank(),
-               c->name().c_str());
+  if (c->ok()) {
+    g_p2p_status = "ok";
+    return c;
+  }
+  g_p2p_status = "fallback: " + c->why();
+  std::fprintf(stderr, "[pe] rank %d: P2P allreduce unavailable on this job (%s), using %s\n", c->rank(),
+               c->why().c_str(), c->name().c_str());
   return c->release_base();
 }
+
+const std::string& p2p_setup_status() { return g_p2p_status; }
 
 }  // namespace pe

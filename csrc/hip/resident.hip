@@ -430,7 +430,12 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
       __syncthreads();
       stamp(4);
       if (wv == 0) {
-        if (lane == 0 && !(it == 0 && wg == rp.fault_wg))  // (fault hook: one workgroup never arrives)
+        if (it == 0 && wg == rp.fault_wg && rp.fault_late) {  // (fault hook: arrive after the others time out)
+          const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+          while ((long long)(__builtin_amdgcn_s_memrealtime() - t0) < rp.timeout_ticks + rp.timeout_ticks / 2)
+            __builtin_amdgcn_s_sleep(8);
+        }
+        if (lane == 0 && !(it == 0 && wg == rp.fault_wg && !rp.fault_late))  // (fault hook: one workgroup never arrives)
           __hip_atomic_fetch_add(rp.ctr + (wg & 7) * 32, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         const int x = lane & 7;
         const unsigned want = unsigned(it + 1) * unsigned((rp.nwg - x + 7) / 8);
@@ -451,10 +456,13 @@ __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
       __syncthreads();
       stamp(5);
     }
-    if (misc[1]) {  // a peer never arrived: abort the solve (status 5), nothing written back
+    if (misc[1]) {  // a peer never arrived: abort the solve (status 5).  A late peer may
+                    // still pass the barrier and write its tile back: the host restarts the
+                    // solve from scratch on the sticky res_abort, never resumes this state
       if (tid == 0) {
         st->status = 5;
         st->done = 1;
+        __hip_atomic_store(&st->res_abort, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
       return;
     }

@@ -97,6 +97,9 @@ std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double
 // One-shot P2P allreduce (IPC-mapped receive buffers, p2p.hip) for the
 // per-iteration sums; everything else through `base` (PE_ALLREDUCE=p2p).
 std::unique_ptr<DeviceComm> make_p2p_allreduce_comm(std::unique_ptr<DeviceComm> base);
+// The last make_p2p_allreduce_comm of this process: "not attempted", "ok" or
+// "fallback: <reason>" (its self-tests; bench / CLI diagnostics).
+const std::string& p2p_setup_status();
 std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,
                                                       CallbackHostComm::ExchangeFn exch,
                                                       CallbackHostComm::BarrierFn barrier);
@@ -191,6 +194,13 @@ class DeviceSolver {
   // in row-step cost units (0s for a dynamic layout)
   std::vector<double> layout_load() const { return {lay_max_, lay_mean_, double(lay_items_)}; }
   int layout_cuts() const { return lay_cuts_; }
+  // First cross-device run diagnostics: hipDeviceCanAccessPeer of this
+  // rank's device toward each rank's (1 / 0; -1 the same device; empty on
+  // one rank), why the halo push is on / off / fell back, and the transport
+  // of the per-sweep sums.
+  const std::vector<int>& peer_access() const { return peer_access_; }
+  const std::string& push_status() const { return push_status_; }
+  const std::string& xr_status() const { return xr_status_; }
   hipStream_t stream() const { return stream_; }
 
   // Checkpoint / resume of the full device state of this rank (raw fields,
@@ -332,6 +342,8 @@ class DeviceSolver {
   double lay_max_ = 0, lay_mean_ = 0;  // static layout: heaviest / mean wave load (row steps)
   int lay_items_ = 0;                  // static layout: most items on one wave
   int lay_cuts_ = 0;                   // three-step filling layout: items cut to fill the waves
+  std::vector<int> peer_access_;
+  std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;
   bool resident_fallback_ = false;  // a resident launch aborted (status 5): switched to the streaming sweep

@@ -58,6 +58,14 @@ class SolveReport:
     comm: str = ""  # device transport of a multi-rank HIP run (e.g. "rccl", "p2p-allreduce+rccl")
     xr: bool = False  # the sweep sums its scalars over ranks itself (P2P transport, no allreduce launch)
     halo_push: bool = False  # the sweep pushes its edge rows to the neighbours over xGMI (no exchange call)
+    # first cross-device run diagnostics (this rank's): the P2P transport's set-up ("ok" / "fallback: why"),
+    # the halo push's ("on" / "off: why" / "fallback: why"), the per-sweep sums' transport, and
+    # hipDeviceCanAccessPeer toward every rank's device (1 / 0, -1 same device)
+    overlap: bool = False  # the halo exchange runs on a second stream while the sweep's interior items run
+    p2p_sum_setup: str = ""
+    push_status: str = ""
+    sums: str = ""
+    peer_access: Optional[list] = None
     resident_fallback: bool = False  # a resident launch aborted (barrier timeout); the solve finished streaming
     # end-of-solve true-residual check (device single-sweep-layout paths, -1: not computed): E-norm of
     # B - A w for the returned w, ||B||, and (three-step) the recurrence's ||r|| of the same iterate, the
@@ -211,4 +219,9 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     rep.comm = comm.name if comm is not None else "self"
     rep.xr = bool(solver.xr)
     rep.halo_push = bool(solver.halo_push)
+    rep.overlap = bool(solver.overlap)
+    rep.p2p_sum_setup = str(nat.p2p_setup_status())
+    rep.push_status = str(solver.push_status)
+    rep.sums = str(solver.xr_status)
+    rep.peer_access = [int(v) for v in solver.peer_access]
     return rep

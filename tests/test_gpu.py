@@ -365,19 +365,24 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     np.testing.assert_allclose(w, one.w, rtol=0, atol=1e-9)
 
 
-@pytest.mark.parametrize("nproc,decomp,allreduce", [(2, "1x2", "p2p"), (4, "2x2", "rccl"), (6, "2x3", "p2p")])
-def test_multi_process_2d_three_step(gpu, nproc, decomp, allreduce):
+@pytest.mark.parametrize("nproc,decomp,allreduce,overlap", [(2, "1x2", "p2p", "0"), (4, "2x2", "rccl", "0"),
+                                                             (6, "2x3", "p2p", "0"), (4, "2x2", "p2p", "1"),
+                                                             (2, "1x2", "rccl", "1"), (6, "2x3", "p2p", "1")])
+def test_multi_process_2d_three_step(gpu, nproc, decomp, allreduce, overlap):
     """2-D splits run the three-step sweep through the exchange: 6 columns of
     r and p per owned row packed after each sweep (kPack), exchanged and
     unpacked, then the x rows with their halo columns (the corners come from
     the diagonal rank).  300×437: every block's last strip has output lanes
     past ny, i.e. in the UP neighbour's columns, which the lane-tested march
     keeps out of the sums (item_layout never flags those items uniform).
-    Iteration count and gathered w match one process."""
+    Iteration count and gathered w match one process.  PE_OVERLAP=1: the
+    boundary items (the 6 owned rows / columns next to a neighbour) run first
+    and count themselves (kS3's kSignal variant); pack + exchange + unpack run
+    on the halo stream while the interior items are computed."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="60")
-    outp = os.path.join(ROOT, "gpurun_out", f"mp3_w_{nproc}_{decomp}.npy")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="60", PE_OVERLAP=overlap)
+    outp = os.path.join(ROOT, "gpurun_out", f"mp3_w_{nproc}_{decomp}_{overlap}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
@@ -386,7 +391,7 @@ def test_multi_process_2d_three_step(gpu, nproc, decomp, allreduce):
     assert out.returncode == 0, out.stderr[-3000:]
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Py"] > 1 and d["algo"] == "three-step", d
-    assert not d["halo_push"]
+    assert not d["halo_push"] and d["overlap"] == (overlap == "1")
     one = solve(EllipseProblem(300, 437), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     np.testing.assert_allclose(np.load(outp), one.w, rtol=0, atol=1e-9)
@@ -408,6 +413,30 @@ def test_halo_push_selftest_failure_falls_back(gpu):
     assert d["ranks"] == 3 and d["Py"] == 1 and d["xr"] and not d["halo_push"]
     assert d["iters"] == 546
     assert "halo push unavailable" in out.stderr
+    # rank 0's own diagnostics say why (the failure was rank 1's)
+    assert d["push_status"] == "fallback: self-test failed on a peer" and d["p2p_sum_setup"] == "ok"
+    assert d["sums"] == "in-sweep P2P over xGMI"
+
+
+def test_p2p_selftest_failure_falls_back(gpu):
+    """A failed P2P-sum self-test on ONE rank (PE_FAULT_INJECT=p2ptest@rank:1):
+    every rank keeps the base transport for the sums (so no in-sweep sum and
+    no halo push); the labels say why, and the job solves correctly."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60",
+               PE_FAULT_INJECT="p2ptest@rank:1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+           "--quiet", "--decomp", "rows", "400", "600"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["ranks"] == 3 and not d["xr"] and not d["halo_push"] and d["comm"] == "host-staged"
+    assert d["p2p_sum_setup"] == "fallback: self-test sum wrong on a peer"
+    assert d["push_status"].startswith("off: no P2P transport") and d["sums"].startswith("allreduce launch")
+    assert d["peer_access"] == [-1, -1, -1]  # one GPU shared by the ranks
+    assert d["iters"] == 546
 
 
 def test_halo_push_checkpoint_resume_bitwise(gpu, tmp_path):
@@ -465,6 +494,38 @@ def test_bench_halo_push_graphs(gpu, nproc):
     assert c["algo"].startswith("three-step")
     assert d["valid"] and d["converged"] and abs(d["iters_converged"] - one.iters) <= 1
     assert d["l2_err"] == pytest.approx(one.l2_err, rel=1e-6)
+
+
+@pytest.mark.parametrize("fault", ["pushtest@rank:1", "p2ptest@rank:1"])
+def test_bench_reports_transport_fallbacks(gpu, fault):
+    """A first cross-device run must say why it fell back:
+    with one rank's halo-push or P2P-sum self-test failing, bench still
+    succeeds (rc 0: a clean fallback) and every rank's entry in its JSON names
+    the set-up outcome and the transport the sweep finally uses."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_FAULT_INJECT=fault)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "3", "--steps", "12", "--warmup", "3", "--grid", "400", "600", "--decomp", "rows",
+           "--no-random-solve"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    ranks = d["config"]["ranks"]
+    assert len(ranks) == 3 and d["valid"] and d["converged"] and d["iters_converged"] == 546
+    for r in ranks:
+        assert set(r["neighbors"]) == ({"right"} if r["rank"] == 0 else {"left"} if r["rank"] == 2 else {"left", "right"})
+        assert all(v == -1 for v in r["peer_access"].values())  # the ranks share one GPU
+        if fault.startswith("pushtest"):
+            assert r["p2p_sum_setup"] == "ok" and r["sums"] == "in-sweep P2P over xGMI"
+            assert r["halo_push"] == ("fallback: self-test failed on this rank" if r["rank"] == 1
+                                      else "fallback: self-test failed on a peer")
+        else:
+            assert r["p2p_sum_setup"] == ("fallback: self-test sum wrong on this rank" if r["rank"] == 1
+                                          else "fallback: self-test sum wrong on a peer")
+            assert r["halo_push"].startswith("off: no P2P transport") and r["sums"].startswith("allreduce launch")
+    assert d["config"]["halo"].startswith("exchange")
 
 
 def test_bench_self_launch_and_random_init(gpu):
@@ -664,6 +725,24 @@ def test_resident_barrier_timeout_falls_back(gpu, monkeypatch):
     assert rep.resident_fallback and rep.algo == "fused (resident fallback)"
     assert rep.converged and rep.iters == 989
     assert rep.l2_err == pytest.approx(1.92e-4, rel=5e-3)
+
+
+def test_resident_late_workgroup_restarts(gpu, monkeypatch):
+    """A workgroup that arrives at the grid barrier AFTER the others timed out
+    (PE_FAULT_INJECT=reslate) passes it and writes its tile back while the
+    rest aborted: the launch's state is not resumable.  The sticky res_abort
+    makes the solver start over on the streaming sweep, and w equals a
+    streaming solve's (resident.hip:454)."""
+    prob = EllipseProblem(800, 1200)
+    monkeypatch.setenv("PE_RESIDENT", "0")
+    ref = solve(prob, backend="hip", return_w=True, algo="fused")
+    monkeypatch.delenv("PE_RESIDENT")
+    monkeypatch.setenv("PE_FAULT_INJECT", "reslate")
+    monkeypatch.setenv("PE_RES_TIMEOUT_S", "0.1")
+    rep = solve(prob, backend="hip", return_w=True)
+    assert rep.resident_fallback and rep.algo == "fused (resident fallback)"
+    assert rep.converged and rep.iters == ref.iters == 989
+    np.testing.assert_allclose(rep.w, ref.w, rtol=0, atol=1e-12)
 
 
 @pytest.mark.parametrize("M,N,chunk,max_iter", [(800, 1200, 988, 0), (300, 700, 512, 513)])

@@ -84,6 +84,14 @@ def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, ove
     assert d["comm"].endswith("rccl")
     assert d["comm"].startswith("p2p-allreduce") == (allreduce == "p2p")
     assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p" and halo == "push")
+    # first cross-device run labels (rank 0): distinct GPUs, peer access to each
+    # (xGMI), every self-tested set-up passed, and the transports they chose
+    assert len(d["peer_access"]) == nproc and d["peer_access"][0] == -1
+    assert all(v == 1 for v in d["peer_access"][1:]), d["peer_access"]
+    if allreduce == "p2p":
+        assert d["p2p_sum_setup"] == "ok" and d["sums"] == "in-sweep P2P over xGMI"
+    assert d["push_status"] == ("on" if d["halo_push"] else d["push_status"]) and (d["halo_push"] or
+                                                                                  d["push_status"].startswith("off"))
     # every block of 600×840 keeps >= 12 rows and columns: three-step everywhere
     # (row slabs push their halos, 2-D blocks exchange them through RCCL)
     assert d["algo"] == "three-step", d["algo"]
@@ -126,6 +134,10 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     # 2047 rows: slabs while every rank keeps >= 512 rows (2 and 4 GPUs) → the
     # halo is pushed by the sweep and the iterations run as captured graphs
     assert c["halo"].startswith("in-sweep xGMI push") == (c["decomposition"]["Py"] == 1)
+    for r in c["ranks"]:  # per-rank diagnostics of the first cross-device run
+        assert r["p2p_sum_setup"] == "ok" and r["sums"] == "in-sweep P2P over xGMI"
+        assert r["halo_push"] == ("on" if c["decomposition"]["Py"] == 1 else "off: 2-D blocks (RCCL exchange)")
+        assert all(v == 1 for k, v in r["peer_access"].items() if int(k) != r["rank"])
 
 
 @pytest.mark.parametrize("nproc", [2, 8])
