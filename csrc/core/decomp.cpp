@@ -54,12 +54,15 @@ ProcessGrid process_grid_from_spec(const std::string& spec, int P, int M, int N)
   if (spec == "rows") return choose_process_grid(P, M, N, DecompMode::Rows);
   if (spec == "cols") return choose_process_grid(P, M, N, DecompMode::Cols);
   // "device": the GPU solver's preference — P×1 row slabs while every rank
-  // keeps >= 32 rows, else the aspect rule.  Slabs run the two-step sweep (two
-  // iterations per pass, 4-row halo pushed by the sweep itself over xGMI, one
-  // contiguous message per side, no strided strips); 2D blocks run the single
-  // sweep.  Per rank block, zero-latency transport (profiles/r3_block_probe.txt):
-  // 4096² on 8 ranks 28.3 µs/iter as 8×1 vs 39.8 as 4×2, on 4 ranks 41.2 vs
-  // 59.7 (4×1 / 2×2); 2048² on 8: 23.4 vs 31.9; 16384² on 8: 168 vs 279.
+  // keeps >= 32 rows, else the aspect rule.  Both run the three-step sweep
+  // (three iterations per pass): slabs push their 6-row halo from the sweep
+  // itself over xGMI (one contiguous message per side, no strided strips), 2-D
+  // blocks exchange theirs through RCCL after (or, overlapped, during) each
+  // sweep; the single sweep remains only for blocks under 12 rows / columns.
+  // Per rank block, zero-latency transport, measured with the two-step sweep
+  // (profiles/r3_block_probe.txt): 4096² on 8 ranks 28.3 µs/iter as 8×1 vs
+  // 39.8 as 4×2, on 4 ranks 41.2 vs 59.7 (4×1 / 2×2); 2048² on 8: 23.4 vs
+  // 31.9; 16384² on 8: 168 vs 279.
   if (spec == "device") {
     if ((int64_t(M) - 1) / P >= 32) return choose_process_grid(P, M, N, DecompMode::Rows);
     return choose_process_grid(P, M, N, DecompMode::Aspect);

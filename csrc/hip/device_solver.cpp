@@ -1194,6 +1194,11 @@ void DeviceSolver::reset() {
 }
 
 void DeviceSolver::run_iterations(int64_t iters, bool use_graph) {
+  // (the three-step sweep ends an n-iteration run with a partial sweep when
+  // 3 ∤ n; the two-step sweep has none — its one-iteration sweep ends the
+  // solve — so an odd count would run one iteration too many)
+  if (steps_ == 2 && iters % 2 != 0)
+    throw std::invalid_argument("two-step sweep: run an even number of iterations (got " + std::to_string(iters) + ")");
   const bool saved = opt_.use_graph;
   opt_.use_graph = use_graph;
   int64_t done = 0;

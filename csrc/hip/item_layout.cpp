@@ -165,13 +165,20 @@ void DeviceSolver::setup_items() {
       if (row_gen(q, s) || row_mixed(q, s)) return false;
     return true;
   };
+  // Three-step, PE_ALTDIR=1: items of even row chunks march upward, odd
+  // ones downward, so two vertically adjacent items read the 2H pipeline-fill
+  // rows they share at the same time — both at their start or both at their
+  // end — instead of one at its end and the other one item later.
+  const bool altdir = steps_ == 3 && k.order == 0 && std::getenv("PE_ALTDIR") && std::atoi(std::getenv("PE_ALTDIR")) == 1;
+  k.altdir = altdir ? 1 : 0;
   auto entry = [&](int64_t ib, int64_t rows, int s) {
     int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
+    if (altdir && ((ib - 1) / k.ti) % 2 == 0) flag |= dev::kUpBit;
     // (not the last strip of a block with an UP neighbour: its output lanes
     // past ny hold that neighbour's columns, which only the lane-tested
     // march keeps out of the sums)
     const bool cut = (blk_.has(UP) && int64_t(s + 1) * fsw_ > blk_.ny);
-    if (flag == 0 && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
+    if (!(flag & dev::kBandBit) && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag |= dev::kUniBit;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
   // outputs a neighbour needs: first in the layout under the overlap (they

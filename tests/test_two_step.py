@@ -154,3 +154,22 @@ def test_two_step_random_init(gpu):
     d = solve(prob, backend="hip", init="random", seed=11, return_w=True, algo=TWO)
     assert abs(c.iters - d.iters) <= 1
     np.testing.assert_allclose(d.w, c.w, rtol=0, atol=1e-9)
+
+
+def test_two_step_rejects_odd_counts(gpu, nat):
+    """The two-step sweep has no partial sweep (its one-iteration sweep ends
+    the solve): an odd run_iterations count is refused instead of silently
+    running one iteration more; even counts run exactly."""
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+    prob = EllipseProblem(300, 420)
+    opt = nat.SolveOptions()
+    opt.algo = 3
+    opt.check_tol = False
+    s = nat.DeviceSolver(prob.to_native(), D.block(300, 420, 1, 0), None, opt)
+    s.reset()
+    with pytest.raises(ValueError, match="even number"):
+        s.run_iterations(7, False)
+    s.run_iterations(8, False)
+    s.synchronize()
+    assert s.state()["iter"] == 8 and s.state()["status"] == 0
