@@ -452,6 +452,17 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("layout_cuts", &DeviceSolver::layout_cuts)
+      .def_property_readonly(
+          "layout_entries",
+          [](const DeviceSolver& s) {
+            // (first row, rows, strip, flags) per list position; rows 0: an empty position
+            std::vector<std::tuple<int, int, int, int>> v;
+            for (const int2& e : s.layout_entries())
+              v.emplace_back(e.x & dev::kRowMask3, e.y >> 20, e.y & 0xFFFFF, e.x & ~dev::kRowMask3);
+            return v;
+          },
+          "the static item list: (first row, rows, strip, flags: kBandBit | kUniBit | kUpBit)")
+      .def_property_readonly("layout_waves", [](DeviceSolver& s) { return s.params().lwaves; })
       .def_property_readonly("peer_access", &DeviceSolver::peer_access,
                              "hipDeviceCanAccessPeer toward each rank's device (1/0; -1 same device)")
       .def_property_readonly("push_status", &DeviceSolver::push_status, "halo push: on / off: why / fallback: why")

@@ -1286,128 +1286,132 @@ SolveResult DeviceSolver::solve() {
   int restarts = 0;
   DevState hs;
   for (;;) {  // (a three-step restart runs the loop again from the restart's iteration)
-  for (;;) {
-    while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
-      const bool sample = sample_every > 0 && nchunk % sample_every == 0;
-      sample_iter_ = enq;
-      enqueue_chunk(chunk_, sample ? sample_iters : 0);
-      enq += chunk_;
-      if (!drift_done && enq >= fault_drift_) {  // PE_FAULT_INJECT=drift@iter:K
-        drift_done = true;
-        const int64_t li = prob_.M / 2 - kp_->gi0, lj = prob_.N / 2 - kp_->gj0;
-        if (fused_ && li >= 1 && li <= blk_.nx && lj >= 1 && lj <= blk_.ny)
-          dev::launch_poke_w(*kp_, li, lj, fault_drift_amp_, stream_);
+    for (;;) {
+      while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
+        const bool sample = sample_every > 0 && nchunk % sample_every == 0;
+        sample_iter_ = enq;
+        enqueue_chunk(chunk_, sample ? sample_iters : 0);
+        enq += chunk_;
+        if (!drift_done && enq >= fault_drift_) {  // PE_FAULT_INJECT=drift@iter:K
+          drift_done = true;
+          const int64_t li = prob_.M / 2 - kp_->gi0, lj = prob_.N / 2 - kp_->gj0;
+          if (fused_ && li >= 1 && li <= blk_.nx && lj >= 1 && lj <= blk_.ny)
+            dev::launch_poke_w(*kp_, li, lj, fault_drift_amp_, stream_);
+        }
+        sampling_ = sample;
+        sample_iter_ = enq - 1;
+        mark_begin(kPhCopy, stream_);
+        if (state_memcpy_)
+          PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
+        else
+          dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
+        mark_end(stream_);
+        sampling_ = false;
+        PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
+        inflight.push_back(Flight{slot, recs_.size()});
+        slot ^= 1;
+        ++nchunk;
       }
-      sampling_ = sample;
-      sample_iter_ = enq - 1;
-      mark_begin(kPhCopy, stream_);
-      if (state_memcpy_)
-        PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
-      else
-        dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
-      mark_end(stream_);
-      sampling_ = false;
-      PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));
-      inflight.push_back(Flight{slot, recs_.size()});
-      slot ^= 1;
-      ++nchunk;
-    }
-    if (inflight.empty()) {
-      if (!stop && enq < cap && enq >= next_ck) {  // drained at a checkpoint boundary
-        const auto tc = clk::now();
-        save_checkpoint(opt_.checkpoint_path + ".r" + std::to_string(blk_.rank));
-        copy_s += secs(tc, clk::now());
-        while (next_ck <= enq) next_ck += ck_every;
-        continue;
+      if (inflight.empty()) {
+        if (!stop && enq < cap && enq >= next_ck) {  // drained at a checkpoint boundary
+          const auto tc = clk::now();
+          save_checkpoint(opt_.checkpoint_path + ".r" + std::to_string(blk_.rank));
+          copy_s += secs(tc, clk::now());
+          while (next_ck <= enq) next_ck += ck_every;
+          continue;
+        }
+        if (res_abort) {
+          // Resident fallback: a workgroup of a resident launch timed out at a
+          // grid barrier.  The aborted launch may still have written back part
+          // of the grid (a late workgroup passes the barrier the others gave up
+          // on), so its state is not resumed: the solve starts over from its
+          // initial state (or its checkpoint) on the streaming sweep.
+          res_abort = false;
+          DevState s0;
+          read_state(&s0);
+          std::fprintf(stderr, "[pe] rank %d: resident kernel barrier timed out by iteration %lld; "
+                               "restarting the solve with the streaming sweep\n", blk_.rank, (long long)s0.iter);
+          resident_ = false;
+          resident_fallback_ = true;
+          chunk_ = stream_chunk_;
+          harvest(recs_.size());
+          samples_.clear();
+          if (!opt_.resume_path.empty()) load_checkpoint(opt_.resume_path + ".r" + std::to_string(blk_.rank));
+          else reset();
+          enq = start_iter;
+          sample_iter_ = start_iter;
+          stop = false;
+          continue;
+        }
+        break;
       }
-      if (res_abort) {
-        // Resident fallback: a workgroup of a resident launch timed out at a
-        // grid barrier.  The aborted launch may still have written back part
-        // of the grid (a late workgroup passes the barrier the others gave up
-        // on), so its state is not resumed: the solve starts over from its
-        // initial state (or its checkpoint) on the streaming sweep.
-        res_abort = false;
-        DevState s0;
-        read_state(&s0);
-        std::fprintf(stderr, "[pe] rank %d: resident kernel barrier timed out by iteration %lld; "
-                             "restarting the solve with the streaming sweep\n", blk_.rank, (long long)s0.iter);
-        resident_ = false;
-        resident_fallback_ = true;
-        chunk_ = stream_chunk_;
-        harvest(recs_.size());
-        samples_.clear();
-        if (!opt_.resume_path.empty()) load_checkpoint(opt_.resume_path + ".r" + std::to_string(blk_.rank));
-        else reset();
-        enq = start_iter;
-        sample_iter_ = start_iter;
-        stop = false;
-        continue;
+      const Flight f = inflight.front();
+      inflight.pop_front();
+      wait_event(ev_[f.slot]);
+      // this chunk's (and every earlier) phase events have completed
+      const size_t done_recs = std::min(f.nrec, recs_.size());
+      harvest(done_recs);
+      for (Flight& g : inflight) g.nrec -= std::min(g.nrec, done_recs);
+      if (hst_[f.slot].done) {
+        stop = true;
+        if ((hst_[f.slot].status == 5 || hst_[f.slot].res_abort) && resident_) res_abort = true;
       }
-      break;
+      if (opt_.log_every > 0 && blk_.rank == 0 && hst_[f.slot].iter >= next_log) {  // chunk-granular progress log
+        std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[f.slot].iter,
+                     hst_[f.slot].last_diff, hst_[f.slot].rz_cur);
+        while (next_log <= hst_[f.slot].iter) next_log += opt_.log_every;
+      }
     }
-    const Flight f = inflight.front();
-    inflight.pop_front();
-    wait_event(ev_[f.slot]);
-    // this chunk's (and every earlier) phase events have completed
-    const size_t done_recs = std::min(f.nrec, recs_.size());
-    harvest(done_recs);
-    for (Flight& g : inflight) g.nrec -= std::min(g.nrec, done_recs);
-    if (hst_[f.slot].done) {
-      stop = true;
-      if ((hst_[f.slot].status == 5 || hst_[f.slot].res_abort) && resident_) res_abort = true;
+    // True-residual check of the returned w: ρ = B − A w.  Three-step: the
+    // s-step moment recurrence (fused3.hip) is checked against it — after a
+    // fix-up (the solve stopped inside the last sweep), the replay launch
+    // first recomputes that iterate's r into x[wpar], so w and r belong to the
+    // same iterate.
+    const bool three = fused_ && steps_ == 3;
+    enqueue_wflush();
+    if (three) {  // (after a fix-up: x[wpar] ← the r of the returned w)
+      KParams kk = *kp_;
+      kk.mlimit = dev::kReplay3;
+      dev::launch_S(kk, par_, stream_);
     }
-    if (opt_.log_every > 0 && blk_.rank == 0 && hst_[f.slot].iter >= next_log) {  // chunk-granular progress log
-      std::fprintf(stderr, "[pe] iter %lld  |dw| = %.6e  (z,r) = %.6e\n", (long long)hst_[f.slot].iter,
-                   hst_[f.slot].last_diff, hst_[f.slot].rz_cur);
-      while (next_log <= hst_[f.slot].iter) next_log += opt_.log_every;
+    if (fused_) residual_pass(three, three);
+    read_state(&hs);
+    const double hh = prob_.h1() * prob_.h2();
+    if (three) {
+      res.res_rec = std::sqrt(hs.res[1] * hh);
+      // relative to the recurrence's own ‖r‖: the fp64 gap of any CG recurrence
+    // scales with the residuals it has summed, not with ‖B‖ (8192² random
+    // init: 8e-3 absolute = 5e-7 of ‖r‖ = 1.5e4; zero init 2e-10 of ‖r‖ —
+    // profiles/r4_resid.txt)
+    res.res_gap = std::sqrt(hs.res[2] / std::max(hs.res[1], 1e-300));
     }
-  }
-  // True-residual check of the returned w: ρ = B − A w.  Three-step: the
-  // s-step moment recurrence (fused3.hip) is checked against it — after a
-  // fix-up (the solve stopped inside the last sweep), the replay launch
-  // first recomputes that iterate's r into x[wpar], so w and r belong to the
-  // same iterate.
-  const bool three = fused_ && steps_ == 3;
-  enqueue_wflush();
-  if (three) {  // (after a fix-up: x[wpar] ← the r of the returned w)
-    KParams kk = *kp_;
-    kk.mlimit = dev::kReplay3;
-    dev::launch_S(kk, par_, stream_);
-  }
-  if (fused_) residual_pass(three, three);
-  read_state(&hs);
-  const double hh = prob_.h1() * prob_.h2();
-  if (three) {
-    res.res_rec = std::sqrt(hs.res[1] * hh);
-    res.res_gap = std::sqrt(hs.res[2] / std::max(hs.res[3], 1e-300));
-  }
-  if (fused_) {
-    res.res_true = std::sqrt(hs.res[0] * hh);
-    res.b_norm = std::sqrt(hs.res[3] * hh);
-  }
-  // Residual replacement: a converged three-step solve whose recurrence has
-  // drifted from B − A w (gap above PE_RESID_GAP, default 1e-6 of ‖B‖) goes on
-  // from the returned w with r = B − A w (stored by the pass above), p = 0 and
-  // a fresh recurrence (β = 0 after the restart), at most twice.  Every rank
-  // reads the same reduced sums: every rank decides the same.
-  if (three && hs.status == 1 && res.res_gap > gap_bound_ && restarts < 2 && hs.iter < cap) {
-    ++restarts;
-    std::fprintf(stderr, "[pe] rank %d: residual gap %.3e > %.1e at iteration %lld; restarting the recurrence from w\n",
-                 blk_.rank, res.res_gap, gap_bound_, (long long)hs.iter);
-    dev::launch_zero_p(*kp_, 0, stream_);
-    dev::launch_restart3(*kp_, stream_);
-    ov_epoch_ = 0;
-    dev::launch_pack(*kp_, 0, stream_);
-    enqueue_exchange(0, false);
-    dev::launch_S(*kp_, 1, stream_);
-    enqueue_exchange(1);
-    enqueue_fs_reduce(1);
-    par_ = 0;
-    enq = hs.iter;
-    stop = false;
-    continue;
-  }
-  break;
+    if (fused_) {
+      res.res_true = std::sqrt(hs.res[0] * hh);
+      res.b_norm = std::sqrt(hs.res[3] * hh);
+    }
+    // Residual replacement: a converged three-step solve whose recurrence has
+    // drifted from B − A w (gap above PE_RESID_GAP, default 1e-4 of ‖r‖) goes on
+    // from the returned w with r = B − A w (stored by the pass above), p = 0 and
+    // a fresh recurrence (β = 0 after the restart), at most twice.  Every rank
+    // reads the same reduced sums: every rank decides the same.
+    if (three && hs.status == 1 && res.res_gap > gap_bound_ && restarts < 2 && hs.iter < cap) {
+      ++restarts;
+      std::fprintf(stderr, "[pe] rank %d: residual gap %.3e > %.1e at iteration %lld; restarting the recurrence from w\n",
+                   blk_.rank, res.res_gap, gap_bound_, (long long)hs.iter);
+      dev::launch_zero_p(*kp_, 0, stream_);
+      dev::launch_restart3(*kp_, stream_);
+      ov_epoch_ = 0;
+      dev::launch_pack(*kp_, 0, stream_);
+      enqueue_exchange(0, false);
+      dev::launch_S(*kp_, 1, stream_);
+      enqueue_exchange(1);
+      enqueue_fs_reduce(1);
+      par_ = 0;
+      enq = hs.iter;
+      stop = false;
+      continue;
+    }
+    break;
   }
   res.restarts = restarts;
   PE_HIP_CHECK(hipEventRecord(t1_, stream_));

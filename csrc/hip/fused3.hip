@@ -679,7 +679,7 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
 #pragma unroll
   for (int q = 0; q < 2; ++q) x.RI[q] = x.R1[q] = x.R2[q] = x.S[q] = 0.0;
 
-  const int nsteps = ie + H3 - c.t0 + 1;
+  const int nsteps = c.tmax - c.tmin + 1;  // (either direction)
   const int rows = ie - ib + 1;
   int bs = 0;  // band ring slot of row t: (t - t0) mod 7
   // steady groups (uniform items): stage rows t-6 .. t and the prefetched

@@ -313,16 +313,154 @@ void DeviceSolver::setup_items() {
     // re-reads 2H fill rows, which T accounts for).  Largest first, ties in
     // chunk-major order, so each round of positions still covers a compact
     // window of rows.  PE_LAYOUT=lpt keeps the LPT layout.
-    const bool fill = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1) &&
-                      !(std::getenv("PE_LAYOUT") && std::string(std::getenv("PE_LAYOUT")) == "lpt");
+    const std::string lay_env = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : "";
+    const bool s3lay = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1) && lay_env != "lpt";
+    const bool equal = s3lay && lay_env != "fill";
+    const bool fill = s3lay && !equal;
     int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
     std::vector<std::vector<int>> per;
     std::vector<double> load;
     int nbnd = 0;
-    if (fill) {
-      double fband = 2.2, fmixed = 1.3;
-      if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
-      if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
+    double fband = 2.45, fmixed = 1.3;  // row-step cost of a band / mixed item, uniform = 1 (profiles/r4_stamps*.txt)
+    if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
+    if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
+    if (equal) {
+      // Three-step sweep: EQUAL-COST PIECES, EXACTLY k PER WAVE.  Whole items
+      // cannot balance ~8 items per wave: the waves hold 8 or 9 uniform items,
+      // or a band item of 2.3 uniform ones (8192²: wave busy time max/mean
+      // 1.06-1.08; the 8-rank slab block's waves with one 41-row band item ran
+      // 1.30× the mean — tools/stamp_probe.py, profiles/r4_stamps*.txt).  So
+      // every strip is cut into runs of one march kind (a row is "band" when a
+      // boundary-band row lies within H rows of it — the kernel marches an
+      // item whose window holds one on the band path — else "mixed" likewise,
+      // else uniform), every run into n_g pieces of equal rows, with the n_g
+      // chosen so that a piece costs X ≈ (its rows + 2H fill rows) × its
+      // kind's factor + overhead everywhere and there are exactly k·W pieces;
+      // the pieces, sorted by cost (ties in row order), are dealt in rounds of
+      // W, snaking, so each wave gets k pieces and each round a compact window
+      // of rows.  k follows the rows-per-item knob: uniform pieces of ≈ ti rows.
+      // PE_LAYOUT=fill / lpt select the earlier layouts.
+      const int64_t nx = blk_.nx;
+      const int ns = k.nstrips;
+      struct Seg {
+        int64_t a, rows;
+        int s;
+        double f;
+        bool bnd;
+        int n;
+      };
+      std::vector<Seg> segs;
+      std::vector<int> cg, cm;  // prefix counts of band / mixed rows (rows 1-H .. nx+H)
+      for (int sx = 0; sx < ns; ++sx) {
+        cg.assign(size_t(nx + 2 * H + 2), 0);
+        cm.assign(size_t(nx + 2 * H + 2), 0);
+        for (int64_t q = 1 - H; q <= nx + H; ++q) {
+          const size_t i = size_t(q + H);
+          cg[i + 1] = cg[i] + (row_gen(q, sx) ? 1 : 0);
+          cm[i + 1] = cm[i] + (row_mixed(q, sx) ? 1 : 0);
+        }
+        auto kind = [&](int64_t q) {  // 2 band, 1 mixed, 0 uniform (window q-H .. q+H)
+          const size_t lo = size_t(q), hi = size_t(q + 2 * H + 1);
+          return cg[hi] - cg[lo] > 0 ? 2 : cm[hi] - cm[lo] > 0 ? 1 : 0;
+        };
+        int64_t a = 1;
+        int ka = kind(1);
+        for (int64_t q = 2; q <= nx + 1; ++q) {
+          const int kq = q <= nx ? kind(q) : -1;
+          // (pieces: also split where a neighbour's halo rows begin, so the push /
+          // overlap boundary pieces stay small)
+          const bool cut_b = (push_ || overlap_) && ((blk_.has(LEFT) && q == H + 1) || (blk_.has(RIGHT) && q == nx - H + 1));
+          if (kq != ka || cut_b) {
+            segs.push_back(Seg{a, q - a, sx, ka == 2 ? fband : ka == 1 ? fmixed : 1.0, false, 1});
+            a = q;
+            ka = kq;
+          }
+        }
+      }
+      for (Seg& g : segs) g.bnd = is_boundary(g.a, g.a + g.rows - 1, g.s);
+      const int64_t minr = 8, maxr = dev::kTImax3;
+      auto Fk = [&](double f) { return double(2 * H) * f + overhead; };  // a piece's fill rows + overhead
+      // pieces of a run for a piece cost X: rows·f / (X − F) rounded, within [rows/maxr, rows/minr]
+      auto nfor = [&](const Seg& g, double X) {
+        const double want = double(g.rows) * g.f / std::max(1e-9, X - Fk(g.f));
+        const int64_t lo = std::max<int64_t>(1, (g.rows + maxr - 1) / maxr), hi = std::max<int64_t>(lo, g.rows / minr);
+        return int(std::min<int64_t>(hi, std::max<int64_t>(lo, std::llround(want))));
+      };
+      auto count = [&](double X) {
+        int64_t P = 0;
+        for (const Seg& g : segs) P += nfor(g, X);
+        return P;
+      };
+      int64_t Pmax = 0, Pmin = 0;
+      for (const Seg& g : segs) {
+        Pmax += std::max<int64_t>(1, g.rows / minr);
+        Pmin += std::max<int64_t>(1, (g.rows + maxr - 1) / maxr);
+      }
+      W = std::max<int>(dev::kWPB, int(std::min<int64_t>(waves_avail, Pmax) / dev::kWPB) * dev::kWPB);
+      const double X0 = double(k.ti + 2 * H) + overhead;  // a uniform piece of ti rows
+      int kr = int(std::max<int64_t>(1, std::llround(double(count(X0)) / W)));
+      while (int64_t(kr) * W < Pmin) ++kr;
+      while (kr > 1 && int64_t(kr) * W > Pmax) --kr;
+      const int64_t P = std::min<int64_t>(Pmax, int64_t(kr) * W);
+      // the piece cost X that gives P pieces (count(X) falls as X grows)
+      double lo = Fk(fband) + 1e-3, hi = 1e9;
+      for (int it = 0; it < 200 && hi - lo > 1e-9 * hi; ++it) {
+        const double mid = 0.5 * (lo + hi);
+        (count(mid) > P ? lo : hi) = mid;
+      }
+      for (Seg& g : segs) g.n = nfor(g, hi);
+      // exactly P: add pieces where they are largest, remove where the merge is cheapest
+      int64_t have = count(hi);
+      auto pc = [&](const Seg& g, int n) { return double(g.rows) * g.f / n + Fk(g.f); };
+      while (have != P) {
+        int best = -1;
+        double bv = 0.0;
+        for (int i = 0; i < int(segs.size()); ++i) {
+          const Seg& g = segs[size_t(i)];
+          if (have < P && g.rows / (g.n + 1) >= minr) {
+            const double v = pc(g, g.n);
+            if (best < 0 || v > bv) best = i, bv = v;
+          } else if (have > P && g.n > 1 && (g.rows + g.n - 2) / (g.n - 1) <= maxr) {
+            const double v = pc(g, g.n - 1);
+            if (best < 0 || v < bv) best = i, bv = v;
+          }
+        }
+        if (best < 0) break;
+        segs[size_t(best)].n += have < P ? 1 : -1;
+        have += have < P ? 1 : -1;
+      }
+      pcs.clear();
+      for (const Seg& g : segs)
+        for (int j = 0; j < g.n; ++j) {
+          const int64_t a0 = g.a + g.rows * j / g.n, a1 = g.a + g.rows * (j + 1) / g.n;
+          pcs.push_back(Piece{a0, a1 - a0, g.s, double(a1 - a0) * g.f + Fk(g.f), is_boundary(a0, a1 - 1, g.s)});
+        }
+      // boundary pieces first (push / overlap), then in row order (chunk-major:
+      // a round of W positions covers a compact window of rows, and the
+      // neighbouring strips of the same rows run on one workgroup's waves —
+      // sorting by cost first scattered the rounds: 8192² 287 vs 254 µs per
+      // iteration, profiles/r4_layout2.txt)
+      std::vector<int> ord(pcs.size());
+      for (size_t i = 0; i < ord.size(); ++i) ord[i] = int(i);
+      // (row bands of ~ti rows by the pieces' centres, then strips: the
+      // neighbouring strips of the same rows run on one workgroup's waves —
+      // sorting by first row alone interleaved strips whose pieces start a
+      // row apart: 8192² 279 vs 254 µs, profiles/r4_layout2.txt)
+      auto band_of = [&](const Piece& p) { return (2 * p.ib + p.rows - 1) / (2 * int64_t(k.ti)); };
+      std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
+        const Piece &a = pcs[size_t(x)], &b = pcs[size_t(y)];
+        if (a.bnd != b.bnd) return a.bnd;
+        const int64_t ra = band_of(a), rb = band_of(b);
+        if (ra != rb) return ra < rb;
+        return a.s != b.s ? a.s < b.s : a.ib < b.ib;
+      });
+      per.assign(size_t(W), {});
+      for (size_t i = 0; i < ord.size(); ++i) {
+        per[i % size_t(W)].push_back(ord[i]);
+        if (pcs[size_t(ord[i])].bnd) ++nbnd;
+      }
+      lay_cuts_ = int(pcs.size());
+    } else if (fill) {
       auto pcost = [&](int64_t ib, int64_t rows, int sx) {
         const int2 e = entry(ib, rows, sx);
         const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
@@ -479,6 +617,7 @@ void DeviceSolver::setup_items() {
     PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
     const auto tc = clk::now();
     upload(ilist_, all.data(), sizeof(int2) * all.size());
+    ilist_host_.assign(all.begin(), all.end());
     copy_setup_s_ += secs(tc, clk::now());
     k.ilist = ilist_;
     k.lnsh = 1;
@@ -558,6 +697,7 @@ void DeviceSolver::setup_items() {
   PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
   const auto tc = clk::now();
   upload(ilist_, all.data(), sizeof(int2) * all.size());
+  ilist_host_.assign(all.begin(), all.end());
   copy_setup_s_ += secs(tc, clk::now());
   // Every dynamic sweep walks the list (the plain one counts no boundary
   // items: lnb = 0; the overlapped iteration's launch carries ov_lnb_).

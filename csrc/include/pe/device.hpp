@@ -194,6 +194,9 @@ class DeviceSolver {
   // in row-step cost units (0s for a dynamic layout)
   std::vector<double> layout_load() const { return {lay_max_, lay_mean_, double(lay_items_)}; }
   int layout_cuts() const { return lay_cuts_; }
+  // the item list as laid out (host copy of KParams::ilist; empty for walks
+  // without a list): {first row | flags, strip | rows << 20} per position
+  const std::vector<int2>& layout_entries() const { return ilist_host_; }
   // First cross-device run diagnostics: hipDeviceCanAccessPeer of this
   // rank's device toward each rank's (1 / 0; -1 the same device; empty on
   // one rank), why the halo push is on / off / fell back, and the transport
@@ -322,8 +325,8 @@ class DeviceSolver {
   // enqueued iteration K (the residual check's test hook)
   long long fault_drift_ = 0;
   double fault_drift_amp_ = 1e-6;
-  // three-step restart threshold on ‖B − A w − r‖_E / ‖B‖_E (PE_RESID_GAP)
-  double gap_bound_ = 1e-6;
+  // three-step restart threshold on ‖B − A w − r‖_E / ‖r‖_E (PE_RESID_GAP)
+  double gap_bound_ = 1e-4;
   hipEvent_t ev_[2] = {nullptr, nullptr};
   hipEvent_t ev_sync_ = nullptr;  // synchronize() under the watchdog
   hipEvent_t t0_ = nullptr, t1_ = nullptr;
@@ -343,6 +346,7 @@ class DeviceSolver {
   int lay_items_ = 0;                  // static layout: most items on one wave
   int lay_cuts_ = 0;                   // three-step filling layout: items cut to fill the waves
   std::vector<int> peer_access_;
+  std::vector<int2> ilist_host_;
   std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   bool resident_ = false;

@@ -106,7 +106,7 @@ struct SolveResult {
   // End-of-solve true-residual check (device single-sweep-layout paths; -1:
   // not computed): E-norms ‖B − A w‖ of the returned w, ‖B‖ and (three-step)
   // the recurrence's ‖r‖ of the same iterate and the relative gap
-  // ‖B − A w − r‖ / ‖B‖; how many times the gap restarted the three-step
+  // ‖B − A w − r‖ / ‖r‖; how many times the gap restarted the three-step
   // recurrence from w (residual replacement).
   double res_true = -1, res_rec = -1, res_gap = -1, b_norm = -1;
   int restarts = 0;

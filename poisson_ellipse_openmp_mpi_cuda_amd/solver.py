@@ -69,7 +69,7 @@ class SolveReport:
     resident_fallback: bool = False  # a resident launch aborted (barrier timeout); the solve finished streaming
     # end-of-solve true-residual check (device single-sweep-layout paths, -1: not computed): E-norm of
     # B - A w for the returned w, ||B||, and (three-step) the recurrence's ||r|| of the same iterate, the
-    # gap ||B - A w - r|| / ||B||, and the restarts (residual replacement) the gap triggered
+    # gap ||B - A w - r|| / ||r||, and the restarts (residual replacement) the gap triggered
     res_true: float = -1.0
     res_rec: float = -1.0
     res_gap: float = -1.0

@@ -1,0 +1,55 @@
+"""MI355X tests of the static item layouts (csrc/hip/item_layout.cpp): every
+owned row of every strip is marched exactly once, whatever the layout — the
+three-step filling layout (kind-aware costs, items cut to fill each wave),
+the LPT layout (PE_LAYOUT=lpt), alternating march directions
+(PE_ALTDIR=1) and the overlap's boundary-first order — and the filling
+layout evens the waves' estimated loads.  Construction only (no solve)."""
+
+import numpy as np
+import pytest
+
+from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem
+from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+pytestmark = pytest.mark.gpu
+BAND, UNI, UP = 1 << 30, 1 << 29, 1 << 28
+
+
+def _coverage(s, nx, ny):
+    ent = [e for e in s.layout_entries if e[1] > 0]
+    nstrips = (ny + 51) // 52
+    cov = np.zeros((nstrips, nx + 1), dtype=np.int32)
+    for ib, rows, strip, _flags in ent:
+        assert 0 <= strip < nstrips and ib >= 1 and ib + rows - 1 <= nx
+        cov[strip, ib:ib + rows] += 1
+    assert (cov[:, 1:] == 1).all(), "a row of a strip is marched twice or never"
+    return ent
+
+
+@pytest.mark.parametrize("P,spec,env", [(1, "device", {}), (1, "device", {"PE_LAYOUT": "lpt"}),
+                                        (1, "device", {"PE_ALTDIR": "1"}), (8, "device", {}),
+                                        (2, "device", {"PE_ALTDIR": "1"}), (8, "4x2", {"PE_OVERLAP": "1"})])
+def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
+    for k, v in env.items():
+        monkeypatch.setenv(k, v)
+    M = N = 8192
+    g = D.grid(P, M, N, spec)
+    blk = nat.decompose(M, N, g, P // 2)
+    opt = nat.SolveOptions()
+    opt.check_tol = False
+    comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
+    s = nat.DeviceSolver(EllipseProblem(M, N).to_native(), blk, comm, opt)
+    assert s.sweep_steps == 3
+    ent = _coverage(s, blk.nx, blk.ny)
+    ups = [e for e in ent if e[3] & UP]
+    if env.get("PE_ALTDIR") == "1":
+        # even row chunks march up, odd ones down
+        assert ups and len(ups) < len(ent)
+        assert all(((ib - 1) // s.ti) % 2 == 0 for ib, _r, _s, fl in ent if fl & UP)
+    else:
+        assert not ups
+    mx, mean, _ = s.layout_load
+    if env.get("PE_LAYOUT") == "lpt" or env.get("PE_OVERLAP") == "1":
+        return
+    # the filling layout: every wave within a few percent of the mean estimated load
+    assert s.layout_cuts >= 0 and mx <= 1.06 * mean, (mx, mean, s.layout_cuts)

@@ -5,7 +5,7 @@ Every device solve on a single-sweep layout reports ‖B − A w‖_E of the
 returned w (kResid, csrc/hip/kernels.hip); the three-step solve also reports
 the recurrence's ‖r‖_E of the same iterate (after a fix-up, the replay launch
 recomputes it: fused3.hip, kReplay3) and the relative gap
-‖B − A w − r‖_E / ‖B‖_E.  A gap above PE_RESID_GAP restarts the recurrence
+‖B − A w − r‖_E / ‖r‖_E.  A gap above PE_RESID_GAP restarts the recurrence
 from w (residual replacement); the drift fault hook makes one.
 
 The reference iterates (stage2-mpi/poisson_mpi_decomp.cpp:400-457) are
@@ -21,7 +21,7 @@ from poisson_ellipse_openmp_mpi_cuda_amd.models.ellipse import GOLDEN_ITERS
 
 pytestmark = pytest.mark.gpu
 THREE = "three-step"
-GAP = 1e-6  # the default PE_RESID_GAP
+GAP = 1e-4  # the default PE_RESID_GAP (relative to the recurrence's ||r||)
 
 
 @pytest.mark.parametrize("M,N,init", [(2048, 2048, "zero"), (2048, 2048, "random"), (1600, 2400, "zero"),
@@ -53,19 +53,22 @@ def test_single_sweep_reports_true_residual(gpu):
 
 
 def test_drift_fault_restarts(gpu, monkeypatch):
-    """PE_FAULT_INJECT=drift@iter:900 adds 1e-3 to w(M/2, N/2) behind the
+    """PE_FAULT_INJECT=drift@iter:900 adds 1e-2 to w(M/2, N/2) behind the
     recurrence's back: the solve still "converges" on ‖Δw‖, the check sees
     the gap, restarts from w with r = B − A w, and the restarted solve
-    removes the perturbation: w matches the clean solve."""
+    removes the perturbation to the tolerance: ‖w − w_clean‖_E is of the
+    order of δ = 1e-6 (the stop rule's own scale; pointwise, the 1e-2 spike
+    shrinks below 1e-3)."""
     prob = EllipseProblem(2048, 2048)
     clean = solve(prob, backend="hip", algo=THREE, return_w=True)
-    monkeypatch.setenv("PE_FAULT_INJECT", "drift@iter:900,amp:1e-3")
+    monkeypatch.setenv("PE_FAULT_INJECT", "drift@iter:900,amp:1e-2")
     hit = solve(prob, backend="hip", algo=THREE, return_w=True)
     assert hit.restarts >= 1 and hit.converged
     assert hit.res_gap < GAP
     assert hit.iters > clean.iters
-    scale = np.abs(clean.w).max()
-    assert np.abs(hit.w - clean.w).max() < 1e-4 * scale
+    d = hit.w - clean.w
+    assert np.sqrt((d * d).sum() * prob.h1 * prob.h2) < 1e-5
+    assert np.abs(d).max() < 1e-3
     assert hit.l2_err == pytest.approx(clean.l2_err, rel=1e-2)
 
 
