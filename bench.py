@@ -322,8 +322,9 @@ def main(argv=None) -> int:
                      ("exchange: " + comm.name)) if world > 1 else "none",
             "overlap": bool(solver.overlap),
             "exchange_us_measured": round(solver.exchange_us, 2),
-            "item_order": "dynamic per-XCD queue" if solver.order == 3 else "static LPT layout",
+            "item_order": "dynamic per-XCD queue" if solver.order == 3 else f"static {solver.layout_name} layout",
             "rows_per_item": "segments (one per wave)" if solver.segment_layout else solver.ti,
+            # (a negative entry: another static layout tried at that height)
             "rows_per_item_candidates": list(solver.ti_tuning_rows),
             "rows_per_item_tuning_ms": [round(x, 4) for x in solver.ti_tuning_ms],
             "resident": bool(solver.resident),

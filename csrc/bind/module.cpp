@@ -452,6 +452,7 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("layout_cuts", &DeviceSolver::layout_cuts)
+      .def_property_readonly("layout_name", &DeviceSolver::layout_name, "static item layout: lpt / fill / equal")
       .def_property_readonly(
           "layout_entries",
           [](const DeviceSolver& s) {
@@ -461,7 +462,7 @@ PYBIND11_MODULE(_native, m) {
               v.emplace_back(e.x & dev::kRowMask3, e.y >> 20, e.y & 0xFFFFF, e.x & ~dev::kRowMask3);
             return v;
           },
-          "the static item list: (first row, rows, strip, flags: kBandBit | kUniBit | kUpBit)")
+          "the static item list: (first row, rows, strip, flags: kBandBit | kUniBit)")
       .def_property_readonly("layout_waves", [](DeviceSolver& s) { return s.params().lwaves; })
       .def_property_readonly("peer_access", &DeviceSolver::peer_access,
                              "hipDeviceCanAccessPeer toward each rank's device (1/0; -1 same device)")

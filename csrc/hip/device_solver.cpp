@@ -379,6 +379,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
   if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
+  // Three-step static layout by block size, one placement per block
+  // (tools/layout_probe.py, profiles/r4_layout2.txt, µs per iteration): the
+  // LPT layout of whole items for ≥ 5·10⁷ nodes (8192²: 253 vs 260 filling,
+  // 275 equal-cost), the filling layout from 2.5·10⁷ (the 2-rank 8192² block:
+  // 137 vs 145-147), the equal-cost one below (4-rank block 83.4-84.2 vs
+  // 87.4-87.9 LPT, 8-rank block 45.1 vs 47.6-49.6); tuned blocks also try the
+  // other two at their best rows per item.
+  if (steps_ == 3) lay_name_ = npts >= 5e7 ? "lpt" : npts >= 2.5e7 ? "fill" : "equal";
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
   const int ti_min = tune_ti_ ? (sstep_ ? tic[0] : kTiCands[0]) : ti;
   set_items(ti);
@@ -471,6 +479,33 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       }
     }
     seg_layout_ = best == 0;
+    // three-step: the other static layouts at the best height
+    if (steps_ == 3 && best != 0 && !std::getenv("PE_LAYOUT")) {
+      const std::string base = lay_name_;
+      std::string keep = base;
+      for (const char* alt : {"equal", "fill", "lpt"}) {
+        if (base == alt) continue;
+        lay_name_ = alt;
+        set_items(best);
+        setup_items();
+        enqueue_init();
+        dev::launch_S(*kp_, 1, stream_);
+        for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
+        PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+        for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
+        PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+        PE_HIP_CHECK(hipEventSynchronize(t1_));
+        float ms = 0.f;
+        PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+        ti_ms_.push_back(ms / 6.0f);
+        ti_rows_.push_back(-best);  // (negative: a layout candidate at that height)
+        if (ms < best_ms) {
+          best_ms = ms;
+          keep = alt;
+        }
+      }
+      lay_name_ = keep;
+    }
     set_items(best == 0 ? ti : best);
     setup_items();
   }

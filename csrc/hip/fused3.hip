@@ -58,7 +58,6 @@
 // 6-deep halo: local rows −5..nx+6 and columns −5..ny+6 hold data; buffer
 // element 0 of a row is column −5.
 #include <cstdlib>
-#include <type_traits>
 
 #include "peer_sum.hpp"
 #include "sstep.hpp"
@@ -308,7 +307,7 @@ struct M3Ctx {
   double* Wm;         // w rows
   const double* hrd;  // PUSH: receive buffer of the parity this sweep reads
   int64_t pitch, poff, wp;
-  int J, c0, ib, ie, t0, tmin, tmax, nx, par;
+  int J, c0, ib, ie, t0, tmax, nx, par;
   unsigned off;
   bool lv0, o0, fix;
   bool scol;          // the lane's column is not past ny (2-D blocks: past ny are the UP neighbour's)
@@ -382,11 +381,10 @@ __device__ __forceinline__ void push_row3(const KParams& k, const M3Ctx& c, M3Ri
 }
 
 // One row step of the march: stage A at row t = t0 + n, B..G at rows
-// t-1..t-6 (UP: t = t0 - n, stages at t+1..t+6).  JJ = n mod 6 fixes the
-// register ring slots at compile time; bs is the band face-ring slot of row
-// t.  STEADY (uniform items): every stage row lies inside the item — no row
-// tests, no clamped loads.
-template <int KIND, bool PUSH, bool EDGE, bool STEADY, int JJ, bool UP>
+// t-1..t-6.  JJ = n mod 6 fixes the register ring slots at compile time; bs
+// is the band face-ring slot of row t.  STEADY (uniform items): every stage
+// row lies inside the item — no row tests, no clamped loads.
+template <int KIND, bool PUSH, bool EDGE, bool STEADY, int JJ>
 __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings& x, const RowCtx& rx, WaveTV3& tvw,
                                       double (&sv)[NS], int n, int bs) {
   constexpr bool BAND = KIND == kBand, UNI = KIND == kUniform;
@@ -396,8 +394,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   constexpr int m0 = JJ % 3, m1 = (JJ + 2) % 3, m2 = (JJ + 1) % 3;  // rows t, t-1, t-2 (t-3 ≡ t)
   constexpr int e0 = JJ & 1, e1 = (JJ + 1) & 1;                      // rows t, t-1 (t-2 ≡ t)
   constexpr int xs = JJ % XD, ws = JJ % WD;
-  constexpr int sd = UP ? -1 : 1;  // march direction: stage d works on row t - sd·d
-  const int t = c.t0 + sd * n;
+  const int t = c.t0 + n;
   const int c0 = c.c0;
   // row inside the item (steady: always — tested as "not a fix-up launch",
   // which skips the sums there: the uniform branch keeps the compiler from
@@ -416,7 +413,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   // pipeline fill: stage d (B = 1 … F = 5) first feeds a needed row at step
   // 2d (G's rows are tested by inr): skip it before — its rows are never used
   auto live = [&](int d) { return STEADY || n >= 2 * d; };
-  // band ring slots (runtime, mod 7) of rows t .. t-6 (UP: t .. t+6)
+  // band ring slots (runtime, mod 7) of rows t .. t-6
   int bsl[7];
 #pragma unroll
   for (int d = 0; d < 7; ++d) bsl[d] = bs >= d ? bs - d : bs - d + kRing3;
@@ -428,26 +425,23 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
       return (interior(q) && c.lv0) ? v * d : 0.0;
     }
   };
-  // the operator at row q (band ring slots sl, sln) and 1/D of the node;
-  // callers pass the ring rows oldest first (rows q-1, q, q+1 marching down;
-  // q+1, q, q-1 marching up)
-  auto op = [&](int q, int sl, int sln, double uo, double u0, double uy, double& d) {
-    const double um = UP ? uy : uo, un = UP ? uo : uy;
+  // the operator at row q (band ring slots sl, sln) and 1/D of the node
+  auto op = [&](int q, int sl, int sln, double um, double u0, double un, double& d) {
     if constexpr (UNI) {
       const URow r = urow<STEADY>(c, rx, q);
       d = r.d;
       return lapu(r, um, u0, un);
     } else {
-      return apply_row1<BAND, WaveTV3, UP>(k, rx, tvw, q, c0, sl, sln, um, u0, un, d);
+      return apply_row1<BAND>(k, rx, tvw, q, c0, sl, sln, um, u0, un, d);
     }
   };
   // ---- A: row t ----
   const double rin = x.RQ[xs], pin = x.PQ[xs], wrow = x.WQ[ws];
   {
-    const int tn = STEADY ? t + sd * XD : UP ? max(t - XD, c.tmin) : min(t + XD, c.tmax);
+    const int tn = STEADY ? t + XD : min(t + XD, c.tmax);
     x.RQ[xs] = ldx3<PUSH>(k, c, tn, c.off);
     x.PQ[xs] = ldx3<PUSH>(k, c, tn, unsigned(c.poff) + c.off);
-    const int wr = STEADY ? t + sd * (WD - 2) : min(max(t + sd * (WD - 2), c.ib), c.ie);
+    const int wr = STEADY ? t - 2 + WD : min(max(t - 2 + WD, c.ib), c.ie);
     // (only the lanes that store w load it: the 12 halo lanes' columns are a
     // neighbouring strip's, and their lines would be fetched for nothing)
     x.WQ[ws] = c.o0 ? ldnt1(c.Wm + int64_t(wr) * c.wp + c.off) : 0.0;
@@ -455,7 +449,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   {
     double d;
     if constexpr (UNI) d = urow<STEADY>(c, rx, t).d;
-    else d = BAND ? enter_band1<WaveTV3, UP>(k, rx, tvw, t, c0, bsl[0]) : dinv_plain1(k, rx, t, c0);
+    else d = BAND ? enter_band1(k, rx, tvw, t, c0, bsl[0]) : dinv_plain1(k, rx, t, c0);
     const double z = zmask(t, rin, d);
     x.P1[m0] = zc1 * z + c.b1 * pin;
     x.RI[e0] = rin;
@@ -463,7 +457,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);  // (stage by stage, as the row tests of the generic steps)
   // ---- B: row t-1 ----
   if (live(1)) {
-    const int q = t - sd * 1;
+    const int q = t - 1;
     double d;
     const double s1 = op(q, bsl[1], bsl[0], x.P1[m2], x.P1[m1], x.P1[m0], d);
     const double r1 = x.RI[e1] - c.a1 * s1;
@@ -476,7 +470,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- C: row t-2 (w) ----
   if (live(2)) {
-    const int q = t - sd * 2;
+    const int q = t - 2;
     double d;
     const double s2 = op(q, bsl[2], bsl[1], x.P2[m0], x.P2[m2], x.P2[m1], d);
     const double r2 = x.R1[e0] - c.a2 * s2;
@@ -491,7 +485,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- D: row t-3 (r, p outputs) ----
   if (live(3)) {
-    const int q = t - sd * 3;
+    const int q = t - 3;
     double d;
     const double s3 = op(q, bsl[3], bsl[2], x.P3[m1], x.P3[m0], x.P3[m2], d);
     const double r3 = x.R2[e1] - c.a3 * s3;
@@ -517,7 +511,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- E: row t-4 ----
   if (live(4)) {
-    const int q = t - sd * 4;
+    const int q = t - 4;
     double d;
     const double qv = op(q, bsl[4], bsl[3], x.Z[m2], x.Z[m1], x.Z[m0], d);
     const double sr = x.S[e0];
@@ -535,7 +529,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- F: row t-5 ----
   if (live(5)) {
-    const int q = t - sd * 5;
+    const int q = t - 5;
     double d, d2;
     const double au = op(q, bsl[5], bsl[4], x.U[m0], x.U[m2], x.U[m1], d);
     const double av = op(q, bsl[5], bsl[4], x.V[m0], x.V[m2], x.V[m1], d2);
@@ -556,7 +550,7 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
   if (STEADY) __builtin_amdgcn_sched_barrier(0);
   // ---- G: row t-6 ----
   {
-    const int q = t - sd * 6;
+    const int q = t - 6;
     if (inr(q)) {
       double d;
       const double auu = op(q, bsl[6], bsl[5], x.UU[m1], x.UU[m0], x.UU[m2], d);
@@ -573,13 +567,13 @@ __device__ __forceinline__ void step3(const KParams& k, const M3Ctx& c, M3Rings&
 // the item's last step.  Steady groups are straight-line code: a scheduling
 // barrier after each step keeps the scheduler from hoisting later steps'
 // work into this one.
-template <int KIND, bool PUSH, bool EDGE, bool STEADY, bool UP>
+template <int KIND, bool PUSH, bool EDGE, bool STEADY>
 __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings& x, const RowCtx& rx, WaveTV3& tvw,
                                        double (&sv)[NS], int n0, int nsteps, int& bs) {
   auto adv = [&]() { bs = bs == kRing3 - 1 ? 0 : bs + 1; };
 #define PE_STEP3(JJ)                                                              \
   if (STEADY || n0 + JJ < nsteps) {                                               \
-    step3<KIND, PUSH, EDGE, STEADY, JJ, UP>(k, c, x, rx, tvw, sv, n0 + JJ, bs);   \
+    step3<KIND, PUSH, EDGE, STEADY, JJ>(k, c, x, rx, tvw, sv, n0 + JJ, bs);       \
     adv();                                                                        \
     if (STEADY) __builtin_amdgcn_sched_barrier(0);                                \
   }
@@ -603,7 +597,7 @@ __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings
 // sum has a factor among z, p, u, v, ũ, ṽ, which are exactly 0 at the
 // global-boundary and padding columns, and the lanes that do not own their
 // columns (0..5, 58..63) are dropped once, at the end of the sweep.
-template <int KIND, bool PUSH, bool EDGE, bool UP>
+template <int KIND, bool PUSH, bool EDGE>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
                                        WaveTV3& tvw, double (&sv)[NS]) {
   const int lane = threadIdx.x & 63;
@@ -626,9 +620,8 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   c.fix = fix;
   c.ib = ib;
   c.ie = ie;
-  c.tmin = ib - H3;
+  c.t0 = ib - H3;
   c.tmax = ie + H3;
-  c.t0 = UP ? c.tmax : c.tmin;
   c.nx = int(k.nx);
   c.par = par;
   c.hrd = PUSH ? k.hrecv + int64_t(par ^ 1) * 2 * H3 * k.pitch : nullptr;
@@ -658,56 +651,49 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   RowCtx rx;
   auto load_seg = [&](int base) { load_rows<KIND == kBand, WaveTV3, 64>(k, rx, tvw, base, ie + H3 + 1, c.J); };
   if (KIND == kBand) load_strip_tables1(k, tvw, c.c0);
-  // (UP: a window ending at the group's highest row t + 6 — never below the
-  // item's first pipeline row, where the row-class table begins)
-  load_seg(UP ? max(c.t0 + 6 - 63, c.tmin) : c.t0);
+  load_seg(c.t0);
 
   M3Rings x;
   x.pushed = false;
   constexpr int XD = kS3XD, WD = kS3WD;
 #pragma unroll
   for (int q = 0; q < XD; ++q) {
-    const int t = UP ? max(c.t0 - q, c.tmin) : min(c.t0 + q, c.tmax);
+    const int t = min(c.t0 + q, c.tmax);
     x.RQ[q] = ldx3<PUSH>(k, c, t, c.off);
     x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off);
   }
 #pragma unroll
   for (int q = 0; q < WD; ++q)
-    x.WQ[q] = c.o0 ? ldnt1(c.Wm + int64_t(min(max(UP ? c.t0 + 2 - q : c.t0 - 2 + q, ib), ie)) * c.wp + c.off) : 0.0;
+    x.WQ[q] = c.o0 ? ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off) : 0.0;
 #pragma unroll
   for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = 0.0;
 #pragma unroll
   for (int q = 0; q < 2; ++q) x.RI[q] = x.R1[q] = x.R2[q] = x.S[q] = 0.0;
 
-  const int nsteps = c.tmax - c.tmin + 1;  // (either direction)
+  const int nsteps = ie + H3 - c.t0 + 1;
   const int rows = ie - ib + 1;
   int bs = 0;  // band ring slot of row t: (t - t0) mod 7
   // steady groups (uniform items): stage rows t-6 .. t and the prefetched
   // rows inside the item for all six steps (n ≥ 12, n ≤ rows + 4); the fill
   // and drain groups around them test rows.  Three loops, not one with a
   // branch: the merged ring state would cost a copy of every ring.
-  auto reload = [&](int n0) {  // tall items: next row window
-    if constexpr (UP) {
-      const int tg = c.t0 - n0;  // the group's rows tg-5 .. tg+6
-      if (tg - 5 < rx.segbase) load_seg(max(tg + 6 - 63, c.tmin));
-    } else {
-      if (c.t0 + n0 + 6 - rx.segbase > 63) load_seg(c.t0 + n0 - H3);
-    }
+  auto reload = [&](int n0) {
+    if (c.t0 + n0 + 6 - rx.segbase > 63) load_seg(c.t0 + n0 - H3);  // tall items: next row window
   };
   int n0 = 0;
   const int nsteady_end = KIND == kUniform ? rows + 4 - 5 : -1;  // last steady group start
   for (; n0 < nsteps && !(n0 >= 12 && n0 <= nsteady_end); n0 += 6) {
     reload(n0);
-    group3<KIND, PUSH, EDGE, false, UP>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+    group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
   }
   if constexpr (KIND == kUniform) {
     for (; n0 <= nsteady_end; n0 += 6) {
       reload(n0);
-      group3<KIND, PUSH, EDGE, true, UP>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+      group3<KIND, PUSH, EDGE, true>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
     }
     for (; n0 < nsteps; n0 += 6) {
       reload(n0);
-      group3<KIND, PUSH, EDGE, false, UP>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+      group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
     }
   }
   if constexpr (PUSH) {
@@ -751,7 +737,7 @@ __device__ __forceinline__ unsigned long long rtc3() {
 // writes the L2s back and the exchange starts while interior items run).
 enum { kPlain = 0, kStamp = 1, kReplay = 2, kSignal = 3 };
 
-template <bool PUSH, int MODE, bool ALT>
+template <bool PUSH, int MODE>
 __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fix, int par, WaveTV3& tv, int wid,
                                       double (&acc)[NS]) {
   constexpr bool STAMP = MODE == kStamp;
@@ -768,26 +754,18 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     const int s = e.y & 0xFFFFF, ib = e.x & kRowMask3;
     const int ie = min(ib + rows - 1, int(k.nx));
     const unsigned long long t_item = STAMP ? rtc3() : 0ull;
-    auto go = [&](auto up) {
-      constexpr bool UP = decltype(up)::value;
-      if (e.x & kBandBit) {
-        march3<kBand, PUSH, true, UP>(k, cf, fix, par, s, ib, ie, tv, acc);
-      } else if (e.x & kUniBit) {
-        // edge strips (a global-boundary or padding column in the window) mask z
-        const int c0 = -(H3 - 1) + s * FSW3 + int(threadIdx.x & 63);
-        const int64_t g0 = k.gj0 + c0;
-        const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
-        if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false, UP>(k, cf, fix, par, s, ib, ie, tv, acc);
-        else march3<kUniform, PUSH, true, UP>(k, cf, fix, par, s, ib, ie, tv, acc);
-      } else {
-        march3<kMixed, PUSH, true, UP>(k, cf, fix, par, s, ib, ie, tv, acc);
-      }
-    };
-    // (ALT kernels only: the upward march's code costs the plain kernel ~50
-    // SGPR spills; the replay marches every item down — it keeps only r and
-    // p, whose per-node arithmetic does not depend on the direction)
-    if (ALT && (e.x & kUpBit)) go(std::bool_constant<ALT>{});
-    else go(std::false_type{});
+    if (e.x & kBandBit) {
+      march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    } else if (e.x & kUniBit) {
+      // edge strips (a global-boundary or padding column in the window) mask z
+      const int c0 = -(H3 - 1) + s * FSW3 + int(threadIdx.x & 63);
+      const int64_t g0 = k.gj0 + c0;
+      const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
+      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false>(k, cf, fix, par, s, ib, ie, tv, acc);
+      else march3<kUniform, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    } else {
+      march3<kMixed, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+    }
     if constexpr (MODE == kSignal) {
       if (pos < k.lnb[0]) {  // a boundary item: count it once its stores have left (no L2 writeback here)
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -810,7 +788,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   }
 }
 
-template <bool PUSH, int MODE = kPlain, bool ALT = false>
+template <bool PUSH, int MODE = kPlain>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
   const int done = st->done;
@@ -907,7 +885,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     cf = sc.c;
   }
   zero_ring();
-  walk3<PUSH, MODE, ALT>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
   if (replay) return;
   if (fix) {
     finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);
@@ -948,20 +926,17 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
 
 void launch_S3(const KParams& k, int par, hipStream_t s) {
   const dim3 g(unsigned(k.nblocks)), b(TJ);
-  auto go = [&](auto alt) {
-    constexpr bool A = decltype(alt)::value;
-    if (k.stamps && !k.push) hipLaunchKernelGGL((kS3<false, kStamp, A>), g, b, 0, s, k, par);
-    else if (k.lnb[0] > 0 && !k.push) hipLaunchKernelGGL((kS3<false, kSignal, A>), g, b, 0, s, k, par);
-    else if (k.push) hipLaunchKernelGGL((kS3<true, kPlain, A>), g, b, 0, s, k, par);
-    else hipLaunchKernelGGL((kS3<false, kPlain, A>), g, b, 0, s, k, par);
-  };
   if (k.mlimit == kReplay3) {
     if (k.push) hipLaunchKernelGGL((kS3<true, kReplay>), g, b, 0, s, k, par);
     else hipLaunchKernelGGL((kS3<false, kReplay>), g, b, 0, s, k, par);
-  } else if (k.altdir) {
-    go(std::true_type{});
+  } else if (k.stamps && !k.push) {
+    hipLaunchKernelGGL((kS3<false, kStamp>), g, b, 0, s, k, par);
+  } else if (k.lnb[0] > 0 && !k.push) {
+    hipLaunchKernelGGL((kS3<false, kSignal>), g, b, 0, s, k, par);
+  } else if (k.push) {
+    hipLaunchKernelGGL((kS3<true, kPlain>), g, b, 0, s, k, par);
   } else {
-    go(std::false_type{});
+    hipLaunchKernelGGL((kS3<false, kPlain>), g, b, 0, s, k, par);
   }
 }
 

@@ -165,20 +165,13 @@ void DeviceSolver::setup_items() {
       if (row_gen(q, s) || row_mixed(q, s)) return false;
     return true;
   };
-  // Three-step, PE_ALTDIR=1: items of even row chunks march upward, odd
-  // ones downward, so two vertically adjacent items read the 2H pipeline-fill
-  // rows they share at the same time — both at their start or both at their
-  // end — instead of one at its end and the other one item later.
-  const bool altdir = steps_ == 3 && k.order == 0 && std::getenv("PE_ALTDIR") && std::atoi(std::getenv("PE_ALTDIR")) == 1;
-  k.altdir = altdir ? 1 : 0;
   auto entry = [&](int64_t ib, int64_t rows, int s) {
     int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
-    if (altdir && ((ib - 1) / k.ti) % 2 == 0) flag |= dev::kUpBit;
     // (not the last strip of a block with an UP neighbour: its output lanes
     // past ny hold that neighbour's columns, which only the lane-tested
     // march keeps out of the sums)
     const bool cut = (blk_.has(UP) && int64_t(s + 1) * fsw_ > blk_.ny);
-    if (!(flag & dev::kBandBit) && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag |= dev::kUniBit;
+    if (flag == 0 && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
   // outputs a neighbour needs: first in the layout under the overlap (they
@@ -313,10 +306,14 @@ void DeviceSolver::setup_items() {
     // re-reads 2H fill rows, which T accounts for).  Largest first, ties in
     // chunk-major order, so each round of positions still covers a compact
     // window of rows.  PE_LAYOUT=lpt keeps the LPT layout.
-    const std::string lay_env = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : "";
-    const bool s3lay = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1) && lay_env != "lpt";
-    const bool equal = s3lay && lay_env != "fill";
-    const bool fill = s3lay && !equal;
+    // three-step layouts: PE_LAYOUT forces one; else the construction's
+    // choice (lay_name_: by block size, or by the rows-per-item tuning)
+    std::string lay = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : lay_name_;
+    const bool s3lay = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
+    if (!s3lay) lay = "lpt";
+    const bool equal = s3lay && lay == "equal";
+    const bool fill = s3lay && lay == "fill";
+    lay_used_ = equal ? "equal" : fill ? "fill" : "lpt";
     int W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(pcs.size())) / dev::kWPB) * dev::kWPB);
     std::vector<std::vector<int>> per;
     std::vector<double> load;

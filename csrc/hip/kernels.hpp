@@ -203,9 +203,6 @@ struct KParams {
   // three-step sweep: > 0 → this launch applies at most mlimit iterations (a
   // run of n iterations ends with a partial sweep when 3 ∤ n)
   int mlimit;
-  // three-step sweep: the item list has upward items (kUpBit) — the kernel
-  // variant that marches both ways
-  int altdir;
 };
 constexpr int kFoldGroup = 64;
 // KParams::mlimit of the three-step replay launch (DevState::fixj)
@@ -224,11 +221,7 @@ constexpr int kRowMask = kBandBit - 1;
 // lies wholly inside or wholly outside the interior in its strip's window
 // (the kernel's uniform-row march: three scalars per row, no lane tests).
 constexpr int kUniBit = 1 << 29;
-// Three-step sweep only: kUpBit — march the item's rows upward (ie → ib).
-// Items of neighbouring row chunks marching in opposite directions read the
-// pipeline-fill rows they share at the same time (start / end of both).
-constexpr int kUpBit = 1 << 28;
-constexpr int kRowMask3 = kUpBit - 1;
+constexpr int kRowMask3 = kUniBit - 1;
 constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (128 loaded, 2-column halo per side)
 constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
 constexpr int kNS2 = 20;         // two-step sweep: sums per sweep

@@ -234,9 +234,7 @@ __device__ __forceinline__ void row_in1(const RowCtx& rx, int q, int c0, bool& i
 }
 
 // First stage of a band item: row q's faces into ring slot `sl`; returns 1/D.
-// UP (upward march): the ring keeps the face BELOW each row (a1) — the row
-// after q in march order is q-1, whose a1 is q's a0.
-template <class WT, bool UP = false>
+template <class WT>
 __device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx, WT& tv, int q, int c0, int sl) {
   const int lane = threadIdx.x & 63;
   bool in0, gen;
@@ -249,7 +247,7 @@ __device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx
     const CT ct{tv.half[l], tv.half[l + 1], tv.sB[l], tv.eB[l]};
     const CS x0 = cset_rc(k, rc, ct, c0, TV{tv.sA[lane], tv.eA[lane], tv.hB[lane], tv.hB[lane + 1]});
     d = x0.d;
-    a0 = UP ? x0.a1 : x0.a0;
+    a0 = x0.a0;
     b0 = x0.b0;
   } else {
     d = in0 ? k.dinv_in : k.dinv_out;
@@ -263,10 +261,9 @@ __device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx
   return d;
 }
 
-// The 5-point operator at row q (ring slot sl, the row entered after it in
-// slot sln: q+1 marching down, q-1 marching up) for the lane's column; d =
-// 1/D of the node.
-template <bool BAND, class WT, bool UP = false>
+// The 5-point operator at row q (ring slot sl, the row above it in slot sln)
+// for the lane's column; d = 1/D of the node.
+template <bool BAND, class WT>
 __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx, const WT& tv, int q, int c0, int sl,
                                              int sln, double um, double u0, double un, double& d) {
   const int lane = threadIdx.x & 63;
@@ -274,7 +271,7 @@ __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx,
   bool in0, gen;
   row_in1(rx, q, c0, in0, gen);
   if (BAND && gen) {
-    const double a0 = tv.a0r[UP ? sln : sl][lane], a1 = tv.a0r[UP ? sl : sln][lane];
+    const double a0 = tv.a0r[sl][lane], a1 = tv.a0r[sln][lane];
     const double b0 = tv.b0r[sl][lane], b1 = tv.b0r[sl][lane + 1];
     const CS x0{a0, a1, b0, b1, dinv_faces(k, a0, a1, b0, b1)};
     d = x0.d;

@@ -194,6 +194,8 @@ class DeviceSolver {
   // in row-step cost units (0s for a dynamic layout)
   std::vector<double> layout_load() const { return {lay_max_, lay_mean_, double(lay_items_)}; }
   int layout_cuts() const { return lay_cuts_; }
+  // the static layout in use: "lpt", "fill" or "equal" (three-step sweep)
+  const std::string& layout_name() const { return lay_used_; }
   // the item list as laid out (host copy of KParams::ilist; empty for walks
   // without a list): {first row | flags, strip | rows << 20} per position
   const std::vector<int2>& layout_entries() const { return ilist_host_; }
@@ -345,6 +347,9 @@ class DeviceSolver {
   double lay_max_ = 0, lay_mean_ = 0;  // static layout: heaviest / mean wave load (row steps)
   int lay_items_ = 0;                  // static layout: most items on one wave
   int lay_cuts_ = 0;                   // three-step filling layout: items cut to fill the waves
+  // three-step static layout: lay_name_ the construction's choice (by block
+  // size / rows-per-item tuning; PE_LAYOUT overrides), lay_used_ the last laid out
+  std::string lay_name_ = "lpt", lay_used_ = "lpt";
   std::vector<int> peer_access_;
   std::vector<int2> ilist_host_;
   std::string push_status_ = "off", xr_status_ = "none";

@@ -1,9 +1,9 @@
 """MI355X tests of the static item layouts (csrc/hip/item_layout.cpp): every
 owned row of every strip is marched exactly once, whatever the layout — the
 three-step filling layout (kind-aware costs, items cut to fill each wave),
-the LPT layout (PE_LAYOUT=lpt), alternating march directions
-(PE_ALTDIR=1) and the overlap's boundary-first order — and the filling
-layout evens the waves' estimated loads.  Construction only (no solve)."""
+the equal-cost layout (PE_LAYOUT=equal), the LPT layout (PE_LAYOUT=lpt) and
+the overlap's boundary-first order — and the equal-cost layout evens the
+waves' estimated loads.  Construction only (no solve)."""
 
 import numpy as np
 import pytest
@@ -12,7 +12,7 @@ from poisson_ellipse_openmp_mpi_cuda_amd import EllipseProblem
 from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
 
 pytestmark = pytest.mark.gpu
-BAND, UNI, UP = 1 << 30, 1 << 29, 1 << 28
+BAND, UNI = 1 << 30, 1 << 29
 
 
 def _coverage(s, nx, ny):
@@ -26,9 +26,10 @@ def _coverage(s, nx, ny):
     return ent
 
 
-@pytest.mark.parametrize("P,spec,env", [(1, "device", {}), (1, "device", {"PE_LAYOUT": "lpt"}),
-                                        (1, "device", {"PE_ALTDIR": "1"}), (8, "device", {}),
-                                        (2, "device", {"PE_ALTDIR": "1"}), (8, "4x2", {"PE_OVERLAP": "1"})])
+@pytest.mark.parametrize("P,spec,env", [(1, "device", {}), (1, "device", {"PE_LAYOUT": "equal"}),
+                                        (1, "device", {"PE_LAYOUT": "fill"}), (8, "device", {}),
+                                        (2, "device", {}), (4, "device", {"PE_LAYOUT": "equal"}),
+                                        (8, "4x2", {"PE_OVERLAP": "1"})])
 def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -40,16 +41,10 @@ def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
     s = nat.DeviceSolver(EllipseProblem(M, N).to_native(), blk, comm, opt)
     assert s.sweep_steps == 3
-    ent = _coverage(s, blk.nx, blk.ny)
-    ups = [e for e in ent if e[3] & UP]
-    if env.get("PE_ALTDIR") == "1":
-        # even row chunks march up, odd ones down
-        assert ups and len(ups) < len(ent)
-        assert all(((ib - 1) // s.ti) % 2 == 0 for ib, _r, _s, fl in ent if fl & UP)
-    else:
-        assert not ups
-    mx, mean, _ = s.layout_load
-    if env.get("PE_LAYOUT") == "lpt" or env.get("PE_OVERLAP") == "1":
-        return
-    # the filling layout: every wave within a few percent of the mean estimated load
-    assert s.layout_cuts >= 0 and mx <= 1.06 * mean, (mx, mean, s.layout_cuts)
+    _coverage(s, blk.nx, blk.ny)
+    mx, mean, per = s.layout_load
+    if s.layout_name == "equal":
+        # exactly k pieces per wave, estimated loads within a few percent
+        assert mx <= 1.08 * mean, (mx, mean)
+        ent = [e for e in s.layout_entries if e[1] > 0]
+        assert (per - 1) * s.layout_waves < len(ent) <= per * s.layout_waves

@@ -221,17 +221,3 @@ def test_three_step_virtual_ranks_cap(gpu, cap):
     assert grp.algo == "three-step" and grp.iters == one.iters == cap and not grp.converged
     np.testing.assert_allclose(grp.w, one.w, rtol=0, atol=1e-12 * np.abs(one.w).max())
 
-
-@pytest.mark.parametrize("M,N", [(1600, 2400), (2048, 2048), (2400, 3200)])
-def test_three_step_alternating_directions(gpu, monkeypatch, M, N):
-    """PE_ALTDIR=1: items of even row chunks march upward (kUpBit; the kernel
-    variant with both marches).  Per-node arithmetic does not depend on the
-    direction, only the order of the sums: golden iteration counts, and the
-    same w as the downward-only layout to rounding."""
-    prob = EllipseProblem(M, N)
-    down = solve(prob, backend="hip", algo=THREE, return_w=True)
-    monkeypatch.setenv("PE_ALTDIR", "1")
-    alt = solve(prob, backend="hip", algo=THREE, return_w=True)
-    assert alt.iters == down.iters == GOLDEN_ITERS[(M, N, "weighted")]
-    np.testing.assert_allclose(alt.w, down.w, rtol=0, atol=1e-11)
-    assert alt.res_gap < 1e-6
