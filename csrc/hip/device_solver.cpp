@@ -174,8 +174,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // 120·nstrips+4, rows -3 .. nx+6.
     fsw_ = steps_ == 3 ? dev::kFSW3 : steps_ == 2 ? dev::kFSW2 : dev::kFSW;
     hdep_ = 2 * steps_;
+    xorg_ = steps_ == 3 ? dev::kHL3 - 1 : hdep_ - 1;
     strips = (ny + fsw_ - 1) / fsw_;
     plane_ = ((fsw_ * strips + 2 * hdep_ + 7) / 8) * 8;
+    // Three-step: strip s loads columns 48s-7 .. 48s+56 (one per lane) and
+    // outputs 48s+1 .. 48s+48.  Element 0 of a row is column -7 and the
+    // plane a whole number of 128-B lines, so every strip's loads are 4 whole
+    // lines and its stores 6 whole 64-B segments of r, p and w (52 outputs of
+    // 64 loaded straddled 64-B segments: partial writes from two strips, and
+    // 5 lines touched for 4 lines of data).
+    if (steps_ == 3) plane_ = ((xorg_ + fsw_ * (strips - 1) + 64 - dev::kHL3 + 1 + 15) / 16) * 16;
     if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
     const int64_t rows = nx + 2 * hdep_ + 2;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
@@ -198,6 +206,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     rows_hi = sstep_ ? nx + hdep_ + 2 : nx + 3;
     cols_hi = sstep_ ? fsw_ * strips + hdep_ + 3 : dev::kFSW * strips + 3;
     tab_lo_ = sstep_ ? -hdep_ : -1;
+    if (steps_ == 3) {  // the last strip's last lane + 3; the first strip's lane 0 is column -xorg
+      cols_hi = fsw_ * (strips - 1) + 64 - dev::kHL3 + 3;
+      tab_lo_ = -(xorg_ + 1);
+    }
   } else {
     strips = (ny + dev::kSW - 1) / dev::kSW;
     const int64_t A = blk_.alloc;
@@ -228,6 +240,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.fused = fused_ ? 1 : 0;
   k.steps = steps_;
   k.hdep = hdep_;
+  k.xorg = xorg_;
   k.nx = nx;
   k.ny = ny;
   k.M = prob_.M;
@@ -726,11 +739,11 @@ void DeviceSolver::set_fused_fields(double* x0, double* x1, double* w) {
   fields_ = x0;
   xalt_ = x1;
   walt_ = w;
-  // local (0, 0): row -(hdep-1), column -(hdep-1) at element 0
-  const int64_t h = hdep_ - 1;
-  k.x[0] = x0 + h * k.pitch + h;
-  k.x[1] = x1 + h * k.pitch + h;
-  k.w = w + h * plane_ + h;
+  // local (0, 0): row -(hdep-1), column -xorg at element 0
+  const int64_t h = hdep_ - 1, hc = xorg_;
+  k.x[0] = x0 + h * k.pitch + hc;
+  k.x[1] = x1 + h * k.pitch + hc;
+  k.w = w + h * plane_ + hc;
   k.r = k.x[0];
   k.p[0] = k.x[0] + plane_;
   k.p[1] = k.x[1] + plane_;
@@ -878,12 +891,12 @@ std::vector<DeviceSolver::HaloPhase> DeviceSolver::halo_phases(int buf) const {
   // neighbour): rows 1..h → the LEFT neighbour's rows nx'+1..nx'+h, rows
   // nx-h+1..nx → the RIGHT neighbour's rows 1-h..0.
   double* x = k.x[buf];
-  const int64_t h = hdep_, n = h * k.pitch;
+  const int64_t h = hdep_, n = h * k.pitch, hc = xorg_;  // (whole rows: from column -xorg)
   if (blk_.has(LEFT))
-    ph[1].ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], x + 1 * k.pitch - (h - 1), x + (1 - h) * k.pitch - (h - 1), n});
+    ph[1].ex.push_back(Exchange{LEFT, blk_.nbr[LEFT], x + 1 * k.pitch - hc, x + (1 - h) * k.pitch - hc, n});
   if (blk_.has(RIGHT))
-    ph[1].ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], x + (blk_.nx - h + 1) * k.pitch - (h - 1),
-                                x + (blk_.nx + 1) * k.pitch - (h - 1), n});
+    ph[1].ex.push_back(Exchange{RIGHT, blk_.nbr[RIGHT], x + (blk_.nx - h + 1) * k.pitch - hc,
+                                x + (blk_.nx + 1) * k.pitch - hc, n});
   return ph;
 }
 

@@ -1183,7 +1183,7 @@ __global__ void kUnpack(KParams k, int b) {
 __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
   const int h = k.hdep;
   const int64_t n = int64_t(h) * k.pitch;
-  double* x = k.x[b] - (h - 1);  // row 0, column -(h-1)
+  double* x = k.x[b] - k.xorg;  // row 0, column -xorg
   for (int side = 0; side < 2; ++side) {
     if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
     const double* src = k.hrecv + (int64_t(b) * 2 + side) * n;
@@ -1200,7 +1200,7 @@ __global__ __launch_bounds__(256) void kHaloImport(KParams k, int b) {
 __global__ __launch_bounds__(256) void kHaloSeed(KParams k, int b) {
   const int h = k.hdep;
   const int64_t n = int64_t(h) * k.pitch;
-  const double* x = k.x[b] - (h - 1);  // row 0, column -(h-1)
+  const double* x = k.x[b] - k.xorg;  // row 0, column -xorg
   for (int side = 0; side < 2; ++side) {
     if (!k.has[side == 0 ? LEFT : RIGHT]) continue;
     double* dst = const_cast<double*>(k.hrecv) + (int64_t(b) * 2 + side) * n;  // this rank's own buffer

@@ -38,8 +38,11 @@
 // one 19-sum reduction per three iterations.
 //
 // Machine mapping (gfx950): fused2.hip's march with a 6-deep pipeline, ONE
-// column per lane: each wave64 strip loads 64 columns and outputs the middle
-// 52 (lanes 6..57: radius-6 dependence).  Two columns per lane (116 of 128)
+// column per lane: each wave64 strip loads 64 columns and outputs 48 (lanes
+// 8..55; the dependence radius is 6, two more halo lanes per side make the
+// strip's loads whole 128-B lines and its stores whole 64-B segments — 52
+// outputs straddled segments: 5 lines touched per 4 lines loaded and partial
+// writes from two strips).  Two columns per lane (116 of 128)
 // needed ~380 VGPRs — one wave per SIMD, issue-bound at 53 % VALU and 3.3 TB/s
 // (8192²: 0.94 ms per sweep); one column halves the rings, so two waves share
 // a SIMD and hide each other's latencies.  Rows march with seven stages in
@@ -56,7 +59,8 @@
 //
 // Layout: fused.hip's (x[b] interleaves the r and p planes by row) with a
 // 6-deep halo: local rows −5..nx+6 and columns −5..ny+6 hold data; buffer
-// element 0 of a row is column −5.
+// element 0 of a row is column −7 (KParams::xorg; rows and planes are whole
+// 128-B lines, so strip s's first column 48s−7 starts a line).
 #include <cstdlib>
 
 #include "peer_sum.hpp"
@@ -69,9 +73,10 @@ namespace dev {
 
 namespace {
 
-constexpr int H3 = 6;
+constexpr int H3 = 6;  // dependence radius of a sweep (rows and columns)
 constexpr int FSW3 = kFSW3;
-static_assert(FSW3 == 64 - 2 * H3, "three-step strip: 64 loaded columns (one per lane), H3 halo columns per side");
+constexpr int HL3 = kHL3, HR3 = 64 - kFSW3 - kHL3;  // a strip's left / right halo lanes
+static_assert(HL3 >= H3 && HR3 >= H3, "three-step strip: 64 loaded columns (one per lane), >= H3 halo lanes per side");
 #ifndef PE_S3_XD
 #define PE_S3_XD 3
 #endif
@@ -596,7 +601,7 @@ __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings
 // Sums are taken over the item's rows without per-term column masks: every
 // sum has a factor among z, p, u, v, ũ, ṽ, which are exactly 0 at the
 // global-boundary and padding columns, and the lanes that do not own their
-// columns (0..5, 58..63) are dropped once, at the end of the sweep.
+// columns (0..7, 56..63) are dropped once, at the end of the sweep.
 template <int KIND, bool PUSH, bool EDGE>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
                                        WaveTV3& tvw, double (&sv)[NS]) {
@@ -606,16 +611,16 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   c.pitch = k.pitch;
   c.poff = k.poff;
   c.wp = k.wpitch;
-  c.Xm = k.x[par ^ 1] - (H3 - 1);  // row pointers at column -5
-  c.Ym = k.x[par] - (H3 - 1);
-  c.Wm = k.w - (H3 - 1);
-  c.J = -(H3 - 1) + s * FSW3;
+  c.Xm = k.x[par ^ 1] - (HL3 - 1);  // row pointers at column -(HL3-1) = element 0 (k.xorg)
+  c.Ym = k.x[par] - (HL3 - 1);
+  c.Wm = k.w - (HL3 - 1);
+  c.J = -(HL3 - 1) + s * FSW3;
   c.c0 = c.J + lane;
-  c.off = unsigned(c.c0 + H3 - 1);
+  c.off = unsigned(c.c0 + HL3 - 1);
   const int64_t g0 = k.gj0 + c.c0;
   c.lv0 = c.c0 <= ny + H3 && g0 >= 1 && g0 <= k.N - 1;
   c.lf0 = c.lv0 ? 1.0 : 0.0;
-  c.o0 = lane >= H3 && lane < 64 - H3 && c.c0 >= 1 && c.c0 <= ny;
+  c.o0 = lane >= HL3 && lane < 64 - HR3 && c.c0 >= 1 && c.c0 <= ny;
   c.scol = c.c0 <= ny;
   c.fix = fix;
   c.ib = ib;
@@ -758,7 +763,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
       march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
     } else if (e.x & kUniBit) {
       // edge strips (a global-boundary or padding column in the window) mask z
-      const int c0 = -(H3 - 1) + s * FSW3 + int(threadIdx.x & 63);
+      const int c0 = -(HL3 - 1) + s * FSW3 + int(threadIdx.x & 63);
       const int64_t g0 = k.gj0 + c0;
       const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
       if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false>(k, cf, fix, par, s, ib, ie, tv, acc);
@@ -891,7 +896,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);
     return;
   }
-  if (lane < H3 || lane >= 64 - H3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
+  if (lane < HL3 || lane >= 64 - HR3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
 #pragma unroll
     for (int n = 0; n < NS; ++n) acc[n] = 0.0;
   block_reduce<NS, false>(acc, sm);

@@ -122,9 +122,10 @@ void DeviceSolver::setup_items() {
   // Does local row q have a boundary-band node in strip s's loaded
   // columns?  (The kernel's has_gen on the same row-class table.)
   const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step, 6 three-step)
+  const int HL = xorg_ + 1;  // a strip's left halo columns (three-step: 8, for aligned loads and stores)
   const int64_t Wc = steps_ == 3 ? 64 : 128;  // columns a wave strip loads (three-step: one per lane)
   auto row_gen = [&](int64_t q, int s) {
-    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
+    const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;  // table index of local row q
     if (t < 0 || t >= rows_tab) return false;
     const int* r = &rowcls_host_[size_t(t) * 4];
@@ -152,7 +153,7 @@ void DeviceSolver::setup_items() {
   // uniform-row march)?  Rows with a band node are never uniform here: the
   // band flag wins.
   auto row_mixed = [&](int64_t q, int s) {
-    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
+    const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;
     if (t < 0 || t >= rows_tab) return true;
     const int* r = &rowcls_host_[size_t(t) * 4];
@@ -178,8 +179,8 @@ void DeviceSolver::setup_items() {
   // feed the exchange) and under the halo push (their xGMI stores then
   // overlap the rest of the sweep instead of ending it)
   auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
-    const int64_t J = -(H - 1) + int64_t(s) * fsw_;
-    const int64_t jlo = std::max<int64_t>(1, J + H), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + H - 1);
+    const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
+    const int64_t jlo = std::max<int64_t>(1, J + HL), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + HL - 1);
     // (the H owned rows / columns next to a neighbour: what the exchange sends)
     return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
            ((blk_.has(LEFT) && ib <= H) || (blk_.has(RIGHT) && ie >= blk_.nx - H + 1) || (blk_.has(DOWN) && jlo <= H) ||
@@ -451,10 +452,41 @@ void DeviceSolver::setup_items() {
         if (ra != rb) return ra < rb;
         return a.s != b.s ? a.s < b.s : a.ib < b.ib;
       });
+      // Dealt round by round, one piece per wave: a round's pieces of the
+      // target cost (±15 %) go to the waves in order, so neighbouring strips
+      // stay on neighbouring waves; its odd pieces (short runs, rounding:
+      // up to ±50 %) go first, heaviest to the least-loaded wave so far.
       per.assign(size_t(W), {});
-      for (size_t i = 0; i < ord.size(); ++i) {
-        per[i % size_t(W)].push_back(ord[i]);
-        if (pcs[size_t(ord[i])].bnd) ++nbnd;
+      std::vector<double> wl(size_t(W), 0.0);
+      std::vector<char> taken(size_t(W), 0);
+      std::vector<int> byload(static_cast<size_t>(W), 0);
+      for (size_t r0 = 0; r0 < ord.size(); r0 += size_t(W)) {
+        const size_t r1 = std::min(ord.size(), r0 + size_t(W));
+        std::vector<int> odd, norm;
+        for (size_t i = r0; i < r1; ++i) {
+          const Piece& p = pcs[size_t(ord[i])];
+          (std::fabs(p.cost - hi) > 0.15 * hi && !p.bnd ? odd : norm).push_back(ord[i]);
+        }
+        std::fill(taken.begin(), taken.end(), 0);
+        if (!odd.empty()) {
+          std::stable_sort(odd.begin(), odd.end(), [&](int x, int y) { return pcs[size_t(x)].cost > pcs[size_t(y)].cost; });
+          for (int w = 0; w < W; ++w) byload[size_t(w)] = w;
+          std::stable_sort(byload.begin(), byload.end(), [&](int x, int y) { return wl[size_t(x)] < wl[size_t(y)]; });
+          for (size_t j = 0; j < odd.size(); ++j) {
+            const int w = byload[j];
+            per[size_t(w)].push_back(odd[j]);
+            wl[size_t(w)] += pcs[size_t(odd[j])].cost;
+            taken[size_t(w)] = 1;
+          }
+        }
+        size_t w = 0;
+        for (int id : norm) {
+          while (taken[w]) ++w;
+          per[w].push_back(id);
+          wl[w] += pcs[size_t(id)].cost;
+          taken[w] = 1;
+          if (pcs[size_t(id)].bnd) ++nbnd;
+        }
       }
       lay_cuts_ = int(pcs.size());
     } else if (fill) {

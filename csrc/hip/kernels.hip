@@ -544,10 +544,10 @@ __global__ __launch_bounds__(TJ) void kWtoP(KParams k, int b) {
 }
 
 // p-plane of x[b] ← 0 over every allocated row and column (halos included):
-// rows 1-hdep .. nx+hdep+2, columns 1-hdep .. poff-hdep.
+// rows 1-hdep .. nx+hdep+2, columns -xorg .. poff-xorg-1.
 __global__ __launch_bounds__(TJ) void kZeroP(KParams k, int b) {
   const int64_t h = k.hdep, rows = k.nx + 2 * h + 2, cols = k.poff;
-  double* base = k.x[b] + k.poff - (h - 1) * k.pitch - (h - 1);
+  double* base = k.x[b] + k.poff - (h - 1) * k.pitch - k.xorg;
   for (int64_t idx = int64_t(blockIdx.x) * TJ + threadIdx.x; idx < rows * cols; idx += int64_t(gridDim.x) * TJ)
     base[(idx / cols) * k.pitch + idx % cols] = 0.0;
 }

@@ -200,6 +200,7 @@ struct KParams {
   // sweep (fused3.hip kS3: 6-deep halo, 116-column strips, 19 sums)
   int steps;
   int hdep;  // halo depth of the single-sweep layouts: 2 (kS), 4 (kS2), 6 (kS3); rows per side of a push message
+  int xorg;  // columns stored left of column 0: element 0 of an x / w row is column -xorg (hdep - 1; kS3: kHL3 - 1)
   // three-step sweep: > 0 → this launch applies at most mlimit iterations (a
   // run of n iterations ends with a partial sweep when 3 ∤ n)
   int mlimit;
@@ -226,7 +227,10 @@ constexpr int kFSW = 124;        // fused sweep: output columns per wave strip (
 constexpr int kFSW2 = 120;       // two-step sweep: output columns per strip (4-column halo per side)
 constexpr int kNS2 = 20;         // two-step sweep: sums per sweep
 constexpr int kTImax2 = 48;      // two-step sweep: max rows per item (rows ib-4 .. ie+5 live one per lane)
-constexpr int kFSW3 = 52;        // three-step sweep: output columns per 64-column strip (one per lane, 6-column halo per side)
+constexpr int kFSW3 = 48;        // three-step sweep: output columns per 64-column strip (one per lane; 6-column halo needed per side)
+constexpr int kHL3 = 8;          // three-step sweep: left halo lanes of a strip (right: 64 - kFSW3 - kHL3); with the
+                                 // rows' element 0 at column -(kHL3 - 1), every strip's loads are whole 128-B lines
+                                 // and its outputs whole 64-B segments
 constexpr int kNS3 = 19;         // three-step sweep: sums per sweep
 constexpr int kTImax3 = 128;     // three-step sweep: max rows per item (row windows reload every ~58 rows)
 

@@ -288,6 +288,7 @@ class DeviceSolver {
   int steps_ = 1;         // iterations per sweep launch (1, 2, 3)
   int fsw_ = 124;         // output columns per strip (kFSW / kFSW2 / kFSW3)
   int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4 / 6)
+  int xorg_ = 1;          // columns stored left of column 0 (KParams::xorg)
   int64_t tab_lo_ = -1;   // first local index of the chord tables / row classes
   bool seg_layout_ = false;  // static layout of tall equal-cost segments, one per wave (setup_items)
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w

@@ -17,7 +17,8 @@ BAND, UNI = 1 << 30, 1 << 29
 
 def _coverage(s, nx, ny):
     ent = [e for e in s.layout_entries if e[1] > 0]
-    nstrips = (ny + 51) // 52
+    nstrips = s.strips
+    assert nstrips == (ny + 47) // 48  # 48 output columns per three-step strip (fused3.hip)
     cov = np.zeros((nstrips, nx + 1), dtype=np.int32)
     for ib, rows, strip, _flags in ent:
         assert 0 <= strip < nstrips and ib >= 1 and ib + rows - 1 <= nx
@@ -43,8 +44,10 @@ def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     assert s.sweep_steps == 3
     _coverage(s, blk.nx, blk.ny)
     mx, mean, per = s.layout_load
-    if s.layout_name == "equal":
-        # exactly k pieces per wave, estimated loads within a few percent
+    if s.layout_name == "equal" and env.get("PE_OVERLAP") != "1":
+        # exactly k pieces per wave, estimated loads within a few percent (with
+        # the overlap, the 6-row boundary pieces cut off for the exchange are
+        # a wave's whole share on small blocks: no balance bound there)
         assert mx <= 1.08 * mean, (mx, mean)
         ent = [e for e in s.layout_entries if e[1] > 0]
         assert (per - 1) * s.layout_waves < len(ent) <= per * s.layout_waves

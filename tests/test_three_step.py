@@ -156,7 +156,7 @@ def test_three_step_checkpoint_resume_bitwise(gpu, tmp_path):
     res = solve(prob, backend="hip", return_w=True, algo=THREE, resume=ck, chunk=12)
     assert res.converged and res.iters == full.iters
     assert np.array_equal(res.w, full.w)
-    with pytest.raises(RuntimeError, match="does not match"):  # a two-step layout is not resumable here
+    with pytest.raises(RuntimeError, match="has the three-step layout.*pass --algo three-step"):  # not resumable here
         solve(prob, backend="hip", algo="two-step", resume=ck)
 
 

@@ -126,7 +126,7 @@ def test_two_step_checkpoint_resume_bitwise(gpu, tmp_path):
     res = solve(prob, backend="hip", return_w=True, algo=TWO, resume=ck, chunk=8)
     assert res.converged and res.iters == full.iters
     assert np.array_equal(res.w, full.w)
-    with pytest.raises(RuntimeError, match="does not match"):  # a single-sweep layout is not resumable here
+    with pytest.raises(RuntimeError, match="has the two-step layout.*pass --algo two-step"):  # not resumable here
         solve(prob, backend="hip", algo="fused", resume=ck)
 
 

@@ -1,13 +1,13 @@
 # DRAM-side request counters (TCC_EA0_RDREQ x 128 B, TCC_EA0_WRREQ x 64 B) of the
 # three-step sweep kS3 at 8192^2 (pe_hip, 300 iterations, tol off) under the
-# round-4 layouts: round-3 LPT 80 rows, filling 80 / 128 rows, alternating
-# directions -> profiles/r4_dram.txt
+# round-4 layouts (LPT, filling, equal-cost) on 8192^2 and the 8-rank
+# slab block (GRID=1024 8191) -> profiles/r4_dram.txt
 set -o pipefail
 R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r4dram; mkdir -p $O
 BIN=$R/bin/pe_hip
 cd /tmp && export TMPDIR=/tmp
 i=0
-for cfg in "PE_LAYOUT=lpt" "PE_TI=80" "PE_TI=128" "PE_ALTDIR=1" "PE_ALTDIR=1 PE_TI=128" ${EXTRA_CFGS}; do
+for cfg in ${CFGS:-"PE_LAYOUT=lpt" "PE_LAYOUT=fill" "PE_LAYOUT=equal"}; do
   i=$((i+1))
   echo "$cfg" > $O/c$i.cfg
   env $cfg timeout -s KILL 120 rocprofv3 --kernel-trace --pmc TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum -d $O/p$i -o run -- $BIN --quiet --max-iter 300 --no-tol ${GRID:-8192 8192} > $O/p$i.log 2>&1 || { tail -5 $O/p$i.log; exit 1; }

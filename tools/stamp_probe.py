@@ -119,11 +119,41 @@ def summarise(st: np.ndarray, nitems: int, nw: int) -> str:
             coef = np.linalg.lstsq(A, dur[m], rcond=None)[0] if m.sum() > 2 else (float("nan"), float("nan"))
             out.append(f"  kind {name:7s}: {m.sum():6d} items  us per row step median {np.median(per):6.3f} p90 {pct(per, 90):6.3f}"
                        f"  fit {coef[0]:6.3f} us/step + {coef[1]:6.2f} us")
-    wl = np.zeros(int(it[:, 2].max()) + 1)
-    np.add.at(wl, it[:, 2], dur)
-    wl = wl[wl > 0]
+    wl_all = np.zeros(int(it[:, 2].max()) + 1)
+    np.add.at(wl_all, it[:, 2], dur)
+    wl = wl_all[wl_all > 0]
     out.append(f"  wave item time: max {wl.max():7.1f}  mean {wl.mean():7.1f}  = {wl.max() / wl.mean():5.3f};"
                f" p10 {pct(wl, 10):7.1f} p90 {pct(wl, 90):7.1f} us")
+    # per XCD (workgroup b runs on XCD b mod 8) and per wave slot in the workgroup:
+    # item time per row step of the uniform items (the same work everywhere)
+    gw = it[:, 2]
+    uni = kind == 2
+    if uni.any():
+        steps_u = (rows + 2 * halo).astype(float)
+        per_step = dur / steps_u
+        xcd = (gw // 4) % 8
+        slot = gw % 4
+        out.append("  uniform us/step by XCD: " + " ".join(f"{np.median(per_step[uni & (xcd == x)]):.3f}" for x in range(8)))
+        out.append("  uniform us/step by wave slot: " + " ".join(f"{np.median(per_step[uni & (slot == x)]):.3f}" for x in range(4)))
+        # position in the wave's list (round): early rounds run with the whole chip busy
+        rnd = np.zeros(len(it), dtype=int)
+        order = np.lexsort((it[:, 0], gw))
+        prev = -1
+        r = 0
+        for i in order:
+            r = r + 1 if gw[i] == prev else 0
+            prev = gw[i]
+            rnd[i] = r
+        out.append("  uniform us/step by round: " + " ".join(f"{np.median(per_step[uni & (rnd == x)]):.3f}"
+                                                          for x in range(int(rnd.max()) + 1) if (uni & (rnd == x)).any()))
+        # a wave's total time against its static cost (row steps, band x2.45): the unexplained spread
+        cost = np.where(kind == 1, 2.45, np.where(kind == 0, 1.3, 1.0)) * steps_u
+        wc = np.zeros_like(wl_all)
+        np.add.at(wc, gw, cost)
+        m = wl_all > 0
+        ratio = wl_all[m] / wc[m]
+        out.append(f"  wave time / static cost: p10 {pct(ratio, 10):.3f} median {np.median(ratio):.3f} p90 {pct(ratio, 90):.3f}"
+                   f"  (corr of wave time with cost {np.corrcoef(wl_all[m], wc[m])[0, 1]:.2f})")
     out.append(step_timeline(steps))
     return "\n".join(out)
 
