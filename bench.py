@@ -67,6 +67,8 @@ def parse_args(argv):
     ap.add_argument("--gpus", type=int, default=int(os.environ.get("WORLD_SIZE", "1")))
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--warmup", type=int, default=100)
+    ap.add_argument("--warmup-s", type=float, default=0.25,
+                    help="the warm-up lasts at least this long (GPU clocks ramp up under load; 0: exactly --warmup steps)")
     ap.add_argument("--grid", type=int, nargs="+", default=[8192, 8192])
     ap.add_argument("--decomp", default="device", help="device | aspect | reference | rows | cols | <Px>x<Py>")
     ap.add_argument("--no-solve", action="store_true", help="skip the (untimed) full solves")
@@ -236,9 +238,23 @@ def main(argv=None) -> int:
     # inside the timed region)
     use_graph = a.launch == "graph"
     solver.reset()
+    t_w = time.perf_counter()
     if a.warmup > 0:
         solver.run_iterations(a.warmup, use_graph)
     solver.synchronize()
+    # GPU clocks ramp up under load: a 20-step window that follows a short
+    # warm-up or an idle gap ran 255-290 us per step, the same window after
+    # 600 warm-up iterations 249 (tools/settle_probe.py, profiles/r4_settle.txt).
+    # So the warm-up lasts at least --warmup-s seconds of sweeps (the same
+    # extra count on every rank: the slowest rank's rate decides).
+    clock_iters = 0
+    dt_w = maxval(time.perf_counter() - t_w)
+    if a.warmup_s > 0 and dt_w < a.warmup_s:
+        per = dt_w / max(1, a.warmup)
+        clock_iters = min(20000, int((a.warmup_s - dt_w) / max(per, 1e-6)) + 1)
+        clock_iters = int(maxval(float(clock_iters)))
+        solver.run_iterations(clock_iters, use_graph)
+        solver.synchronize()
     if use_graph:
         solver.prepare_graphs(a.steps)
     solver.reset()  # the timed steps start a fresh solve (w⁰ = 0)
@@ -291,6 +307,7 @@ def main(argv=None) -> int:
         "n_gpus": world,
         "steps": a.steps,
         "warmup": a.warmup,
+        "clock_warmup_steps": clock_iters,
         "ms_per_step": 1000.0 * dt / a.steps,
         "higher_is_better": True,
         "scaling": "strong",

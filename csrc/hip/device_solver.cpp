@@ -346,7 +346,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
     // (three-step beyond 2²⁶ nodes: 128 rows — 16384² 978 vs 999 µs/iteration
     // at 80, one placement, profiles/r3_ti_final.txt)
-    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 128 : big ? 80 : 48) : (big ? 40 : 24);
+    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 256 : npts >= double(1 << 25) ? 112 : big ? 80 : 48) : (big ? 40 : 24);
     ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
@@ -386,8 +386,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // within ±2 % over 24-48 rows: fixed 40 — one placement per grid,
   // tools/ti_probe.py, profiles/r3_ti_probe.txt).  Three-step sweep (12
   // pipeline-fill rows per item): among {32 .. 96} (2400×3200 32 rows 45.7
-  // µs/iter vs 57.1 at 64, 1600×2400 and 2048² 48, 4096² 64); fixed 80 above
-  // (8192² 247.9 vs 253.2 at 64 and 268.6 at 48 — profiles/r3_three_ti.txt).
+  // µs/iter vs 57.1 at 64, 1600×2400 and 2048² 48, 4096² 64); fixed above,
+  // with the aligned 48-column strips: 8192² 112 rows (240-247 µs/iter vs
+  // 253-256 at 80, 266-271 at 104, 249 at 120, 255 at 128 — the same on two
+  // boxes and with padded rows), 16384² 256 (939 vs 959 at 128, 968 at 112)
+  // — tools/layout_probe.py, tools/block_probe.py, profiles/r4_ti48.txt.
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
@@ -454,7 +457,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     if (npts >= 12e6 && !sstep_) cands.insert(cands.end(), {24, 30});
     {
       const int64_t W = std::max(dev::kWPB, wave_cap_);
-      const int tlo = sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? dev::kTImax3 : sstep_ ? dev::kTImax2 : 40;
+      const int tlo = sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
       for (int q = 2; q <= 5; ++q)
         for (int t = tlo; t <= thi; ++t)
           if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {

@@ -376,7 +376,7 @@ void DeviceSolver::setup_items() {
         }
       }
       for (Seg& g : segs) g.bnd = is_boundary(g.a, g.a + g.rows - 1, g.s);
-      const int64_t minr = 8, maxr = dev::kTImax3;
+      const int64_t minr = 8, maxr = 128;  // (pieces of the tuned heights' range)
       auto Fk = [&](double f) { return double(2 * H) * f + overhead; };  // a piece's fill rows + overhead
       // pieces of a run for a piece cost X: rows·f / (X − F) rounded, within [rows/maxr, rows/minr]
       auto nfor = [&](const Seg& g, double X) {

@@ -197,10 +197,11 @@ bool DeviceSolver::placement_search(bool retry) {
   // best-class threshold: the single sweep's 40 B/node at ≥ 4.9 TB/s (8192²:
   // ≤ 0.548 ms); the two-step sweep's 48 B/node per sweep at ≥ 4.7 TB/s
   // (8192²: its classes are 0.676-0.69 and 0.83-0.85 ms per sweep); the
-  // three-step sweep's 48 B/node per sweep at ≥ 4.2 TB/s (8192²: ≤ 0.767 ms;
-  // its classes are 0.751-0.757, 0.83 and 0.95 ms — profiles/r3_quad.txt,
-  // r4_bench600 in profiles/r4_resid.txt; 4.7 was never reached: every try ran)
-  double fast_tbs = steps_ == 3 ? 4.2 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
+  // three-step sweep's 48 B/node per sweep at ≥ 4.4 TB/s (8192²: ≤ 0.732 ms;
+  // with the aligned strips and 112-row items its classes are 0.709-0.722,
+  // 0.74, 0.78-0.79 and 0.83-0.85 ms, the first fast one usually the 5th try —
+  // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates)
+  double fast_tbs = steps_ == 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return true;
