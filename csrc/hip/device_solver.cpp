@@ -134,7 +134,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
 
   mark("start");
-  PE_HIP_CHECK(hipStreamCreateWithFlags(&stream_, hipStreamNonBlocking));
+  stream_ = acquire_stream();  // (pooled: set_device created one — runtime.cpp)
   mark("stream");
   // Peer access of this rank's device toward every rank's (first cross-device
   // run diagnostics: the halo push and the in-sweep sums map peers' memory):
@@ -817,7 +817,8 @@ DeviceSolver::~DeviceSolver() {
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   (void)hipFree(st_);
   (void)hipHostFree(hst_);
-  (void)hipStreamDestroy(stream_);
+  (void)hipStreamSynchronize(stream_);
+  release_stream(stream_);
 }
 
 KParams& DeviceSolver::params() { return *kp_; }

@@ -7,6 +7,9 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "pe/device.hpp"
 
@@ -26,7 +29,51 @@ int device_count() {
   return n;
 }
 
-void set_device(int dev) { PE_HIP_CHECK(hipSetDevice(dev)); }
+// Per-device pool of idle solver streams.  A new stream costs the runtime a
+// hardware queue: 20-41 ms in a fresh process, the largest part of a small
+// grid's construction (400×600: T_solver 0.035-0.054 s of which the stream
+// 21-41 ms — PE_CTOR_TRACE=1, profiles/r4_cold.txt).  set_device() creates
+// one while binding the process to its GPU (like the RCCL / P2P set-up, before
+// any solver), and a solver returns its stream here when it is destroyed.
+namespace {
+std::mutex g_stream_mu;
+std::vector<std::pair<int, hipStream_t>> g_idle_streams;  // (device, stream)
+}  // namespace
+
+hipStream_t acquire_stream() {
+  int dev = 0;
+  PE_HIP_CHECK(hipGetDevice(&dev));
+  {
+    std::lock_guard<std::mutex> g(g_stream_mu);
+    for (size_t i = 0; i < g_idle_streams.size(); ++i)
+      if (g_idle_streams[i].first == dev) {
+        const hipStream_t s = g_idle_streams[i].second;
+        g_idle_streams.erase(g_idle_streams.begin() + long(i));
+        return s;
+      }
+  }
+  hipStream_t s = nullptr;
+  PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  return s;
+}
+
+void release_stream(hipStream_t s) {
+  if (!s) return;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return;
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  g_idle_streams.emplace_back(dev, s);
+}
+
+void set_device(int dev) {
+  PE_HIP_CHECK(hipSetDevice(dev));
+  bool have = false;
+  {
+    std::lock_guard<std::mutex> g(g_stream_mu);
+    for (const auto& e : g_idle_streams) have = have || e.first == dev;
+  }
+  if (!have) release_stream(acquire_stream());
+}
 
 int current_device() {
   int d = -1;

@@ -28,7 +28,10 @@ struct PeerSum;
 
 [[noreturn]] void hip_fail(hipError_t e, const char* expr, const char* file, int line);
 int device_count();
-void set_device(int dev);
+void set_device(int dev);  // hipSetDevice + one pooled solver stream for that device
+// Solver streams (non-blocking) from / back to the per-device idle pool.
+hipStream_t acquire_stream();
+void release_stream(hipStream_t s);
 std::string device_name(int dev);
 int current_device();
 std::string device_pci_bus_id(int dev);
