@@ -83,6 +83,9 @@ static_assert(HL3 >= H3 && HR3 >= H3, "three-step strip: 64 loaded columns (one 
 #ifndef PE_S3_WD
 #define PE_S3_WD 3
 #endif
+#ifndef PE_S3_NTX
+#define PE_S3_NTX 0  // 1: non-temporal loads of r and p (experiment)
+#endif
 constexpr int kS3XD = PE_S3_XD, kS3WD = PE_S3_WD;
 constexpr int NS = kNS3;
 constexpr int kRing3 = 7;  // band face ring: rows t-6 .. t
@@ -365,7 +368,11 @@ __device__ __forceinline__ double ldx3(const KParams& k, const M3Ctx& c, int t, 
       return __hip_atomic_load(h, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
     }
   }
+#if PE_S3_NTX
+  return __builtin_nontemporal_load(c.Xm + int64_t(t) * c.pitch + o);
+#else
   return c.Xm[int64_t(t) * c.pitch + o];
+#endif
 }
 
 __device__ __forceinline__ double ldnt1(const double* p) { return __builtin_nontemporal_load(p); }
