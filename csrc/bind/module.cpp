@@ -465,6 +465,8 @@ PYBIND11_MODULE(_native, m) {
           "the static item list: (first row, rows, strip, flags: kBandBit | kUniBit)")
       .def_property_readonly("layout_waves", [](DeviceSolver& s) { return s.params().lwaves; })
       .def_property_readonly("strips", [](DeviceSolver& s) { return s.params().nstrips; }, "wave strips across the block")
+      .def_property_readonly("layout_boundary", &DeviceSolver::layout_boundary,
+                             "overlap: list positions 0 .. n-1 hold the boundary items (0: no overlap)")
       .def_property_readonly("peer_access", &DeviceSolver::peer_access,
                              "hipDeviceCanAccessPeer toward each rank's device (1/0; -1 same device)")
       .def_property_readonly("push_status", &DeviceSolver::push_status, "halo push: on / off: why / fallback: why")

@@ -452,10 +452,13 @@ void DeviceSolver::setup_items() {
         if (ra != rb) return ra < rb;
         return a.s != b.s ? a.s < b.s : a.ib < b.ib;
       });
-      // Dealt round by round, one piece per wave: a round's pieces of the
-      // target cost (±15 %) go to the waves in order, so neighbouring strips
-      // stay on neighbouring waves; its odd pieces (short runs, rounding:
-      // up to ±50 %) go first, heaviest to the least-loaded wave so far.
+      // Dealt round by round, one piece per wave: a round's boundary pieces
+      // take its first waves (the kernel's kSignal variant counts list
+      // positions 0 .. nbnd-1 as the boundary items), its odd pieces (short
+      // runs, rounding: up to ±50 % off the target cost) the least-loaded
+      // waves so far, heaviest first, and the rest (within ±15 %) the
+      // remaining waves in order, so neighbouring strips stay on
+      // neighbouring waves.
       per.assign(size_t(W), {});
       std::vector<double> wl(size_t(W), 0.0);
       std::vector<char> taken(size_t(W), 0);
@@ -463,17 +466,27 @@ void DeviceSolver::setup_items() {
       for (size_t r0 = 0; r0 < ord.size(); r0 += size_t(W)) {
         const size_t r1 = std::min(ord.size(), r0 + size_t(W));
         std::vector<int> odd, norm;
+        std::fill(taken.begin(), taken.end(), 0);
+        int wb = 0;
         for (size_t i = r0; i < r1; ++i) {
           const Piece& p = pcs[size_t(ord[i])];
-          (std::fabs(p.cost - hi) > 0.15 * hi && !p.bnd ? odd : norm).push_back(ord[i]);
+          if (p.bnd) {  // (ord: boundary pieces first, so these are waves 0, 1, … of the round)
+            per[size_t(wb)].push_back(ord[i]);
+            wl[size_t(wb)] += p.cost;
+            taken[size_t(wb++)] = 1;
+            ++nbnd;
+            continue;
+          }
+          (std::fabs(p.cost - hi) > 0.15 * hi ? odd : norm).push_back(ord[i]);
         }
-        std::fill(taken.begin(), taken.end(), 0);
         if (!odd.empty()) {
           std::stable_sort(odd.begin(), odd.end(), [&](int x, int y) { return pcs[size_t(x)].cost > pcs[size_t(y)].cost; });
           for (int w = 0; w < W; ++w) byload[size_t(w)] = w;
           std::stable_sort(byload.begin(), byload.end(), [&](int x, int y) { return wl[size_t(x)] < wl[size_t(y)]; });
+          size_t q = 0;
           for (size_t j = 0; j < odd.size(); ++j) {
-            const int w = byload[j];
+            while (taken[size_t(byload[q])]) ++q;
+            const int w = byload[q];
             per[size_t(w)].push_back(odd[j]);
             wl[size_t(w)] += pcs[size_t(odd[j])].cost;
             taken[size_t(w)] = 1;
@@ -485,7 +498,6 @@ void DeviceSolver::setup_items() {
           per[w].push_back(id);
           wl[w] += pcs[size_t(id)].cost;
           taken[w] = 1;
-          if (pcs[size_t(id)].bnd) ++nbnd;
         }
       }
       lay_cuts_ = int(pcs.size());

