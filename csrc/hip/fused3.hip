@@ -78,7 +78,7 @@ constexpr int FSW3 = kFSW3;
 constexpr int HL3 = kHL3, HR3 = 64 - kFSW3 - kHL3;  // a strip's left / right halo lanes
 static_assert(HL3 >= H3 && HR3 >= H3, "three-step strip: 64 loaded columns (one per lane), >= H3 halo lanes per side");
 #ifndef PE_S3_XD
-#define PE_S3_XD 3
+#define PE_S3_XD 4
 #endif
 #ifndef PE_S3_WD
 #define PE_S3_WD 3
