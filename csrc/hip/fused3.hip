@@ -78,7 +78,7 @@ constexpr int FSW3 = kFSW3;
 constexpr int HL3 = kHL3, HR3 = 64 - kFSW3 - kHL3;  // a strip's left / right halo lanes
 static_assert(HL3 >= H3 && HR3 >= H3, "three-step strip: 64 loaded columns (one per lane), >= H3 halo lanes per side");
 #ifndef PE_S3_XD
-#define PE_S3_XD 4
+#define PE_S3_XD 3  // rows of r / p loads in flight: a divisor of the 6-step unroll (the ring slot is JJ mod XD)
 #endif
 #ifndef PE_S3_WD
 #define PE_S3_WD 3
@@ -87,6 +87,7 @@ static_assert(HL3 >= H3 && HR3 >= H3, "three-step strip: 64 loaded columns (one 
 #define PE_S3_NTX 0  // 1: non-temporal loads of r and p (experiment)
 #endif
 constexpr int kS3XD = PE_S3_XD, kS3WD = PE_S3_WD;
+static_assert(6 % kS3XD == 0 && 6 % kS3WD == 0, "register ring periods must divide the 6-step group");
 constexpr int NS = kNS3;
 constexpr int kRing3 = 7;  // band face ring: rows t-6 .. t
 using WaveTV3 = WaveTV1<kRing3>;
