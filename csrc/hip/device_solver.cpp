@@ -346,7 +346,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
     // (three-step beyond 2²⁶ nodes: 128 rows — 16384² 978 vs 999 µs/iteration
     // at 80, one placement, profiles/r3_ti_final.txt)
-    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 256 : npts >= double(1 << 25) ? 112 : big ? 80 : 48) : (big ? 40 : 24);
+    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 448 : npts >= double(1 << 25) ? 112 : big ? 80 : 48) : (big ? 40 : 24);
     ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
@@ -389,8 +389,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // µs/iter vs 57.1 at 64, 1600×2400 and 2048² 48, 4096² 64); fixed above,
   // with the aligned 48-column strips: 8192² 112 rows (240-247 µs/iter vs
   // 253-256 at 80, 266-271 at 104, 249 at 120, 255 at 128 — the same on two
-  // boxes and with padded rows), 16384² 256 (939 vs 959 at 128, 968 at 112)
-  // — tools/layout_probe.py, tools/block_probe.py, profiles/r4_ti48.txt.
+  // boxes and with padded rows; a scan of 64-224 found only 132 as good),
+  // 16384² 448 (867 vs 880 at 272, 891-899 at 256, 975 at 288, 934-940 at
+  // 512; 256 was 939 vs 959 at 128 on another box) — tools/layout_probe.py,
+  // tools/block_probe.py, profiles/r4_ti48.txt.
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;

@@ -232,7 +232,7 @@ constexpr int kHL3 = 8;          // three-step sweep: left halo lanes of a strip
                                  // rows' element 0 at column -(kHL3 - 1), every strip's loads are whole 128-B lines
                                  // and its outputs whole 64-B segments
 constexpr int kNS3 = 19;         // three-step sweep: sums per sweep
-constexpr int kTImax3 = 256;     // three-step sweep: max rows per item (row windows reload every ~58 rows)
+constexpr int kTImax3 = 512;     // three-step sweep: max rows per item (row windows reload every ~58 rows)
 
 // LDS-resident single sweep (resident.hip): small single-rank blocks run many
 // iterations in ONE launch.  The block is cut into tiles of one 124-column
