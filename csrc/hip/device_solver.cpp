@@ -443,7 +443,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   setup_resident();
   mark("resident");
   if (tune_ti_ && !resident_) {
-    // time S_0 + 2 + 6 local sweeps per candidate on real data (no
+    // time S_0 + 1 + 4 local sweeps per candidate on real data (no
     // communication: the in-sweep cross-rank sum is not set up yet) and keep
     // the fastest; every rank tunes its own block
     Range range("pe.tune_rows_per_item");
@@ -476,20 +476,32 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     }
     float best_ms = 0.f;
     int best = ti;
-    for (int cand : cands) {
-      seg_layout_ = cand == 0;
-      set_items(cand == 0 ? ti : cand);
-      setup_items();
+    // one candidate: S_0 + 1 + kTimed local sweeps on real data, the last
+    // kTimed timed (round 3: S_0 + 2 + 6 — construction is inside T_solver)
+    constexpr int kTimed = 4;
+    auto time_layout = [&]() {
       enqueue_init();
       dev::launch_S(*kp_, 1, stream_);
-      for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
+      dev::launch_S(*kp_, 0, stream_);
       PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-      for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
+      for (int i = 0; i < kTimed; ++i) dev::launch_S(*kp_, (i + 1) & 1, stream_);
       PE_HIP_CHECK(hipEventRecord(t1_, stream_));
       PE_HIP_CHECK(hipEventSynchronize(t1_));
       float ms = 0.f;
       PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-      ti_ms_.push_back(ms / 6.0f);
+      return ms;
+    };
+    for (int cand : cands) {
+      seg_layout_ = cand == 0;
+      const auto tl = clk::now();
+      set_items(cand == 0 ? ti : cand);
+      setup_items();
+      const auto tg = clk::now();
+      const float ms = time_layout();
+      if (ctor_trace)
+        std::fprintf(stderr, "[pe] ctor   tune %3d rows: layout %7.3f ms, timing %7.3f ms\n", cand,
+                     1e3 * secs(tl, tg), 1e3 * secs(tg, clk::now()));
+      ti_ms_.push_back(ms / float(kTimed));
       ti_rows_.push_back(cand);
       if (best_ms == 0.f || ms < best_ms) {
         best_ms = ms;
@@ -506,16 +518,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
         lay_name_ = alt;
         set_items(best);
         setup_items();
-        enqueue_init();
-        dev::launch_S(*kp_, 1, stream_);
-        for (int i = 0; i < 2; ++i) dev::launch_S(*kp_, i & 1, stream_);
-        PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-        for (int i = 0; i < 6; ++i) dev::launch_S(*kp_, i & 1, stream_);
-        PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-        PE_HIP_CHECK(hipEventSynchronize(t1_));
-        float ms = 0.f;
-        PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-        ti_ms_.push_back(ms / 6.0f);
+        const float ms = time_layout();
+        ti_ms_.push_back(ms / float(kTimed));
         ti_rows_.push_back(-best);  // (negative: a layout candidate at that height)
         if (ms < best_ms) {
           best_ms = ms;

@@ -92,10 +92,14 @@ void DeviceSolver::setup_items() {
   // heavy items split, below) and the overlap; orders 1 / 2 are plain
   // tuning walks.
   if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
-  if (ilist_) {  // re-laid out (rows-per-item tuning)
-    PE_HIP_CHECK(hipFree(ilist_));
-    ilist_ = nullptr;
-  }
+  // (re-laid out by the rows-per-item tuning: the list buffer is reused while
+  // it is large enough — a free per candidate synchronised the device)
+  auto list_alloc = [&](size_t n) {
+    if (n <= ilist_cap_) return;
+    if (ilist_) PE_HIP_CHECK(hipFree(ilist_));
+    ilist_cap_ = std::max(n, ilist_cap_ + ilist_cap_ / 2);
+    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * ilist_cap_));
+  };
   if (overlap_) {
     ov_reserve_ = 8;
     // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
@@ -124,7 +128,7 @@ void DeviceSolver::setup_items() {
   const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step, 6 three-step)
   const int HL = xorg_ + 1;  // a strip's left halo columns (three-step: 8, for aligned loads and stores)
   const int64_t Wc = steps_ == 3 ? 64 : 128;  // columns a wave strip loads (three-step: one per lane)
-  auto row_gen = [&](int64_t q, int s) {
+  auto row_gen_x = [&](int64_t q, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;  // table index of local row q
     if (t < 0 || t >= rows_tab) return false;
@@ -132,27 +136,13 @@ void DeviceSolver::setup_items() {
     const int64_t lo = std::max<int64_t>(J, r[2]), hi = std::min<int64_t>(J + Wc - 1, r[3]);
     return lo <= hi && (r[0] > r[1] || lo < r[0] || hi > r[1]);
   };
-  auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
-    double c = 0.0;
-    for (int64_t q = ib - H; q <= ie + H; ++q) c += row_gen(q, s) ? gen_cost : 1.0;
-    return c;
-  };
-  auto rows_band = [&](int64_t ib, int64_t ie, int s) {
-    for (int64_t q = ib - H; q <= ie + H; ++q)
-      if (row_gen(q, s)) return true;
-    return false;
-  };
-  auto item_cost = [&](int ch, int s) {
-    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
-    return rows_cost(ib, ie, s);
-  };
   // {first row | band flag, strip | rows << 20}; the band flag selects the
   // kernel's coefficient path (rows ib-H .. ie+H include a boundary-band row)
   // Three-step sweep: is every row of the item's window wholly interior or
   // wholly non-interior in the strip's 64 columns (kUniBit: the kernel's
   // uniform-row march)?  Rows with a band node are never uniform here: the
   // band flag wins.
-  auto row_mixed = [&](int64_t q, int s) {
+  auto row_mixed_x = [&](int64_t q, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;
     if (t < 0 || t >= rows_tab) return true;
@@ -161,10 +151,44 @@ void DeviceSolver::setup_items() {
     if (lo > hi) return false;                 // no interior column
     return !(r[0] <= J && r[1] >= J + Wc - 1);  // some interior, some not
   };
+  // Per strip, prefix counts of the band / mixed rows q = 1-H .. nx+H (the
+  // windows of every item; built once per solver: the rows-per-item tuning
+  // re-lays out up to 11 times, and evaluating the rows one by one per item
+  // took 4.5-5.7 ms per layout at 4096², inside T_solver).
+  const int64_t q0 = 1 - H, R = blk_.nx + 2 * H;
+  if (pgen_.empty()) {
+    pgen_.assign(size_t(k.nstrips) * size_t(R + 1), 0);
+    pmix_.assign(size_t(k.nstrips) * size_t(R + 1), 0);
+    for (int s = 0; s < k.nstrips; ++s) {
+      int* g = &pgen_[size_t(s) * size_t(R + 1)];
+      int* m = &pmix_[size_t(s) * size_t(R + 1)];
+      for (int64_t i = 0; i < R; ++i) {
+        g[i + 1] = g[i] + (row_gen_x(q0 + i, s) ? 1 : 0);
+        m[i + 1] = m[i] + (row_mixed_x(q0 + i, s) ? 1 : 0);
+      }
+    }
+  }
+  // band / mixed rows among q = a .. b of strip s (inside 1-H .. nx+H)
+  auto ngen = [&](int64_t a, int64_t b, int s) {
+    const int* g = &pgen_[size_t(s) * size_t(R + 1)];
+    return g[b - q0 + 1] - g[a - q0];
+  };
+  auto nmix = [&](int64_t a, int64_t b, int s) {
+    const int* m = &pmix_[size_t(s) * size_t(R + 1)];
+    return m[b - q0 + 1] - m[a - q0];
+  };
+  auto row_gen = [&](int64_t q, int s) { return q >= q0 && q < q0 + R ? ngen(q, q, s) > 0 : row_gen_x(q, s); };
+  auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
+    const int64_t n = ie - ib + 1 + 2 * H, ng = ngen(ib - H, ie + H, s);
+    return double(n - ng) + double(ng) * gen_cost;
+  };
+  auto rows_band = [&](int64_t ib, int64_t ie, int s) { return ngen(ib - H, ie + H, s) > 0; };
   auto rows_uniform = [&](int64_t ib, int64_t ie, int s) {
-    for (int64_t q = ib - H; q <= ie + H; ++q)
-      if (row_gen(q, s) || row_mixed(q, s)) return false;
-    return true;
+    return ngen(ib - H, ie + H, s) == 0 && nmix(ib - H, ie + H, s) == 0;
+  };
+  auto item_cost = [&](int ch, int s) {
+    const int64_t ib = 1 + int64_t(ch) * k.ti, ie = std::min<int64_t>(ib + k.ti - 1, blk_.nx);
+    return rows_cost(ib, ie, s);
   };
   auto entry = [&](int64_t ib, int64_t rows, int s) {
     int flag = rows_band(ib, ib + rows - 1, s) ? dev::kBandBit : 0;
@@ -348,18 +372,9 @@ void DeviceSolver::setup_items() {
         int n;
       };
       std::vector<Seg> segs;
-      std::vector<int> cg, cm;  // prefix counts of band / mixed rows (rows 1-H .. nx+H)
       for (int sx = 0; sx < ns; ++sx) {
-        cg.assign(size_t(nx + 2 * H + 2), 0);
-        cm.assign(size_t(nx + 2 * H + 2), 0);
-        for (int64_t q = 1 - H; q <= nx + H; ++q) {
-          const size_t i = size_t(q + H);
-          cg[i + 1] = cg[i] + (row_gen(q, sx) ? 1 : 0);
-          cm[i + 1] = cm[i] + (row_mixed(q, sx) ? 1 : 0);
-        }
         auto kind = [&](int64_t q) {  // 2 band, 1 mixed, 0 uniform (window q-H .. q+H)
-          const size_t lo = size_t(q), hi = size_t(q + 2 * H + 1);
-          return cg[hi] - cg[lo] > 0 ? 2 : cm[hi] - cm[lo] > 0 ? 1 : 0;
+          return ngen(q - H, q + H, sx) > 0 ? 2 : nmix(q - H, q + H, sx) > 0 ? 1 : 0;
         };
         int64_t a = 1;
         int ka = kind(1);
@@ -655,7 +670,7 @@ void DeviceSolver::setup_items() {
     for (int x = 1; x <= 8; ++x) ov_lbase_[x] = int(all.size());
     ov_lnb_[0] = nbnd;
     for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
-    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+    list_alloc(all.size());
     const auto tc = clk::now();
     upload(ilist_, all.data(), sizeof(int2) * all.size());
     ilist_host_.assign(all.begin(), all.end());
@@ -735,7 +750,7 @@ void DeviceSolver::setup_items() {
   }
   ov_lbase_[nsh] = int(all.size());
   if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
-  PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * all.size()));
+  list_alloc(all.size());
   const auto tc = clk::now();
   upload(ilist_, all.data(), sizeof(int2) * all.size());
   ilist_host_.assign(all.begin(), all.end());

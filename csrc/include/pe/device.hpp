@@ -313,6 +313,8 @@ class DeviceSolver {
   // halo/interior overlap (multi-rank single-sweep)
   bool overlap_ = false;
   int2* ilist_ = nullptr;  // per shard: boundary items, heavy items, the rest (dev::KParams::ilist)
+  size_t ilist_cap_ = 0;   // entries allocated at ilist_
+  std::vector<int> pgen_, pmix_;  // item layout: per strip, prefix counts of band / mixed rows (item_layout.cpp)
   int nslot_cap_ = 0;      // item-sum slots allocated
   int ov_lnsh_ = 1, ov_nb_ = 0, ov_reserve_ = 8, ov_debug_ = 0;
   int wave_cap_ = 0;     // resident waves of the sweep grid (occupancy)
