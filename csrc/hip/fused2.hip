@@ -475,7 +475,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     for (int i = lane; i < 6 * 130; i += 64) (&tv.b0r[0][0])[i] = 0.0;
   }
   const int W = k.lwaves;
-  for (int pos = int(blockIdx.x) * kWPB + wid; pos < k.nslots; pos += W) {
+  // (waves past the layout's W — a grid with reserved blocks — have no positions)
+  for (int pos = int(blockIdx.x) * kWPB + wid < W ? int(blockIdx.x) * kWPB + wid : k.nslots; pos < k.nslots; pos += W) {
     const int2 e = cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
     if (rows == 0) continue;  // empty position of the static layout

@@ -760,7 +760,11 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   if constexpr (STAMP) {
     if (l0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave] = rtc3();
   }
-  for (int pos = gwave; pos < k.nslots; pos += W) {
+  // (waves past the layout's W — the overlap's reserved blocks when a launch
+  // uses the whole grid: the construction's timing sweeps, S_0, the replay —
+  // have no list positions; they used to march round r+1's first items twice)
+  const int pend = gwave < W ? k.nslots : 0;
+  for (int pos = gwave; pos < pend; pos += W) {
     const int2 e = cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
     if (rows == 0) continue;  // empty position of the static layout

@@ -77,3 +77,33 @@ def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
         assert mx <= 1.10 * mean, (mx, mean)  # (8192² at 112 rows: 7 pieces per wave, 1.09)
         ent = [e for e in s.layout_entries if e[1] > 0]
         assert (per - 1) * s.layout_waves < len(ent) <= per * s.layout_waves
+
+
+def test_overlap_full_grid_launches(gpu, nat, monkeypatch):
+    """Launches that use the whole grid (S_0, the construction's timing
+    sweeps, the replay) include the overlap's reserved blocks: their waves
+    have no list positions (they used to march round r+1's first items a
+    second time, so S_0 counted those items' sums twice).  One rank's 4x2
+    block of 8192² (two rounds of items): 30 iterations with the overlap
+    give the w of 30 without it, to rounding (the boundary-first order sums
+    in another order)."""
+    g = D.grid(8, 8192, 8192, "4x2")
+    blk = nat.decompose(8192, 8192, g, 4)
+    monkeypatch.setenv("PE_TI", "48")  # (fixed rows per item: two rounds of LPT items)
+    monkeypatch.setenv("PE_LAYOUT", "lpt")
+    ws = []
+    for ov in ("0", "1"):
+        monkeypatch.setenv("PE_OVERLAP", ov)
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        comm = nat.make_delay_comm(8, 0.0, 0.0)
+        s = nat.DeviceSolver(EllipseProblem(8192, 8192).to_native(), blk, comm, opt)
+        if ov == "1":
+            assert s.layout_boundary > 0 and len([e for e in s.layout_entries if e[1] > 0]) > s.layout_waves
+        s.reset()
+        s.run_iterations(30, False)
+        s.synchronize()
+        ws.append(np.array(s.w()))
+        del s, comm
+    scale = np.abs(ws[0]).max()
+    assert scale > 0 and np.abs(ws[0] - ws[1]).max() <= 1e-9 * scale
