@@ -248,9 +248,14 @@ def main(argv=None) -> int:
     # So the warm-up lasts at least --warmup-s seconds of sweeps (the same
     # extra count on every rank: the slowest rank's rate decides).
     clock_iters = 0
+    n_w = a.warmup
+    if a.warmup_s > 0 and n_w == 0:  # (no warm-up steps asked for: time 3 to size the clock warm-up)
+        solver.run_iterations(3, use_graph)
+        solver.synchronize()
+        n_w = 3
     dt_w = maxval(time.perf_counter() - t_w)
     if a.warmup_s > 0 and dt_w < a.warmup_s:
-        per = dt_w / max(1, a.warmup)
+        per = dt_w / n_w
         clock_iters = min(20000, int((a.warmup_s - dt_w) / max(per, 1e-6)) + 1)
         clock_iters = int(maxval(float(clock_iters)))
         solver.run_iterations(clock_iters, use_graph)
