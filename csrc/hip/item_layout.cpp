@@ -118,6 +118,11 @@ void DeviceSolver::setup_items() {
   // worse everywhere); larger blocks see no difference above the placement
   // noise and keep 3 (profiles/r2_gencost.txt).  PE_GEN_COST overrides.
   double gen_cost = double(blk_.nx) * double(blk_.ny) >= double(1 << 24) ? 3.0 : 2.0;
+  // three-step LPT at 2²⁵-2²⁶ nodes (8192², 112-row items): 3.25-4 run ≈1 %
+  // faster than 3 on three boxes, 5-8 ≈8 % slower (profiles/r4_ti48.txt)
+  if (steps_ == 3 && double(blk_.nx) * double(blk_.ny) >= double(1 << 25) &&
+      double(blk_.nx) * double(blk_.ny) <= double(1 << 26))
+    gen_cost = 3.5;
   if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
   const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
   const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
