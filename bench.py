@@ -237,27 +237,35 @@ def main(argv=None) -> int:
     # instantiate every chunk graph the timed run will launch (no capture
     # inside the timed region)
     use_graph = a.launch == "graph"
+    sweep = int(solver.sweep_steps) if int(solver.sweep_steps) == 2 else 1
+
+    def whole_sweeps(n):
+        return -(-n // sweep) * sweep
+
     solver.reset()
     t_w = time.perf_counter()
+    if sweep > 1 and a.steps % sweep:
+        raise SystemExit(f"bench: the two-step sweep times whole sweeps: --steps must be even (got {a.steps})")
     if a.warmup > 0:
-        solver.run_iterations(a.warmup, use_graph)
+        solver.run_iterations(whole_sweeps(a.warmup), use_graph)
     solver.synchronize()
     # GPU clocks ramp up under load: a 20-step window that follows a short
     # warm-up or an idle gap ran 255-290 us per step, the same window after
     # 600 warm-up iterations 249 (tools/settle_probe.py, profiles/r4_settle.txt).
     # So the warm-up lasts at least --warmup-s seconds of sweeps (the same
     # extra count on every rank: the slowest rank's rate decides).
+    # (counts are whole sweeps: the two-step sweep runs only even counts)
     clock_iters = 0
-    n_w = a.warmup
-    if a.warmup_s > 0 and n_w == 0:  # (no warm-up steps asked for: time 3 to size the clock warm-up)
-        solver.run_iterations(3, use_graph)
+    n_w = whole_sweeps(a.warmup)
+    if a.warmup_s > 0 and n_w == 0:  # (no warm-up steps asked for: time one sweep's worth to size the clock warm-up)
+        n_w = whole_sweeps(2)
+        solver.run_iterations(n_w, use_graph)
         solver.synchronize()
-        n_w = 3
     dt_w = maxval(time.perf_counter() - t_w)
     if a.warmup_s > 0 and dt_w < a.warmup_s:
         per = dt_w / n_w
         clock_iters = min(20000, int((a.warmup_s - dt_w) / max(per, 1e-6)) + 1)
-        clock_iters = int(maxval(float(clock_iters)))
+        clock_iters = whole_sweeps(int(maxval(float(clock_iters))))
         solver.run_iterations(clock_iters, use_graph)
         solver.synchronize()
     if use_graph:
@@ -286,6 +294,7 @@ def main(argv=None) -> int:
         res = solver.solve()
         tm = res.timers
         extra = dict(t_solver_s=maxval(tm["solver"]), t_setup_s=maxval(tm["setup"]), t_iterate_s=maxval(tm["iterate"]),
+                     t_check_s=maxval(tm.get("check", 0.0)),
                      t_breakdown_s={k: maxval(tm[k]) for k in ("gpu", "dot", "halo", "reduce", "wait", "copy")},
                      iters_converged=int(res.iters), converged=bool(res.converged),
                      l2_err=float(res.l2_err), max_err=float(res.max_err),

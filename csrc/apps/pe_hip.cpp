@@ -141,12 +141,12 @@ int main(int argc, char** argv) {
                   "\"t_reduce\": %.6f, \"timer_samples\": %.0f, "
                   "\"iters_per_s\": %.3f, \"l2_err\": %.6e, \"max_err\": %.6e, \"max_outside\": %.6e, \"total\": %.6f, "
                   "\"algo\": \"%s\", \"res_true\": %.6e, \"res_rec\": %.6e, \"res_gap\": %.6e, "
-                  "\"b_norm\": %.6e, \"restarts\": %d, %s}\n",
+                  "\"b_norm\": %.6e, \"restarts\": %d, \"t_check\": %.6f, %s}\n",
                   P.M, P.N, size * vranks, r.Px, r.Py, (long long)r.iters, r.converged ? "true" : "false", r.t.solver,
                   r.t.setup, r.t.construct, r.t.iterate, r.t.gpu, r.t.dot, r.t.dot_fused ? "true" : "false", r.t.copy,
                   r.t.halo, r.t.reduce, r.t.sampled, r.iters / std::max(1e-12, r.t.iterate), r.l2_err, r.max_err,
                   r.max_outside, total, r.algo.c_str(), r.res_true, r.res_rec, r.res_gap, r.b_norm,
-                  r.restarts, diag.c_str());
+                  r.restarts, r.t.check, diag.c_str());
     } else {
       std::cout << format_result_legacy(P, r, size, "stage4");
       std::printf("   Process grid %dx%d | iters/s ~ %.1f | L2 error in D ~ %.6e | max error in D ~ %.6e\n", r.Px, r.Py,

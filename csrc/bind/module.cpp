@@ -28,6 +28,7 @@ py::dict timers_dict(const Timers& t) {
   d["setup"] = t.setup;
   d["solver"] = t.solver;
   d["iterate"] = t.iterate;
+  d["check"] = t.check;
   d["construct"] = t.construct;
   d["sampled"] = t.sampled;
   d["wait"] = t.wait;

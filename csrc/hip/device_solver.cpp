@@ -138,24 +138,57 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   mark("stream");
   // Peer access of this rank's device toward every rank's (first cross-device
   // run diagnostics: the halo push and the in-sweep sums map peers' memory):
-  // 1 / 0 hipDeviceCanAccessPeer, -1 the same device.
+  // 1 / 0 hipDeviceCanAccessPeer, -1 the same physical device, -2 a device this
+  // process cannot see (another node, or masked by HIP_VISIBLE_DEVICES).
+  // Devices are compared by PCI location, not by process-local ordinals, and
+  // gathered 64 ranks per collective (the comms' host scratch size); a failure
+  // leaves the diagnostics empty and never aborts construction.
   if (comm_->size() > 1) {
-    const int P = comm_->size();
-    int mydev = 0;
-    PE_HIP_CHECK(hipGetDevice(&mydev));
-    std::vector<double> ids(size_t(P), -1.0);
-    ids[size_t(comm_->rank())] = double(mydev);
-    comm_->host_max(ids.data(), P, stream_);
-    peer_access_.assign(size_t(P), -1);
-    for (int r = 0; r < P; ++r) {
-      const int d = int(ids[size_t(r)]);
-      if (d == mydev || d < 0) continue;
-      int can = 0;
-      if (hipDeviceCanAccessPeer(&can, mydev, d) != hipSuccess) {
-        (void)hipGetLastError();
-        can = 0;
+    try {
+      const int P = comm_->size();
+      auto pci_key = [](int dv) -> double {
+        int dom = 0, bus = -1, dev = 0;
+        if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dv) != hipSuccess ||
+            hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dv) != hipSuccess ||
+            hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, dv) != hipSuccess) {
+          (void)hipGetLastError();
+          return -1.0;
+        }
+        return double((int64_t(dom) << 16) | (int64_t(bus) << 8) | int64_t(dev));
+      };
+      int mydev = 0, ndev = 0;
+      PE_HIP_CHECK(hipGetDevice(&mydev));
+      PE_HIP_CHECK(hipGetDeviceCount(&ndev));
+      const double mykey = pci_key(mydev);
+      std::vector<double> keys(size_t(P), -1.0);
+      for (int c0 = 0; c0 < P; c0 += 64) {
+        const int n = std::min(64, P - c0);
+        double chunk[64];
+        for (int i = 0; i < n; ++i) chunk[i] = c0 + i == comm_->rank() ? mykey : -1.0;
+        comm_->host_max(chunk, n, stream_);
+        for (int i = 0; i < n; ++i) keys[size_t(c0 + i)] = chunk[i];
       }
-      peer_access_[size_t(r)] = can;
+      std::vector<int> pa(size_t(P), -1);
+      for (int r = 0; r < P; ++r) {
+        const double key = keys[size_t(r)];
+        if (key < 0 || key == mykey) continue;
+        int d = -1;
+        for (int i = 0; i < ndev && d < 0; ++i)
+          if (pci_key(i) == key) d = i;
+        if (d < 0) {
+          pa[size_t(r)] = -2;
+          continue;
+        }
+        int can = 0;
+        if (hipDeviceCanAccessPeer(&can, mydev, d) != hipSuccess) {
+          (void)hipGetLastError();
+          can = 0;
+        }
+        pa[size_t(r)] = can;
+      }
+      peer_access_ = std::move(pa);
+    } catch (const std::exception&) {
+      peer_access_.clear();
     }
   }
   KParams& k = *kp_;
@@ -1343,6 +1376,7 @@ SolveResult DeviceSolver::solve() {
   bool drift_done = fault_drift_ <= 0;
   int restarts = 0;
   DevState hs;
+  double check_s = 0.0;
   for (;;) {  // (a three-step restart runs the loop again from the restart's iteration)
     for (;;) {
       while (!stop && enq < cap && inflight.size() < 2 && enq < next_ck) {
@@ -1427,6 +1461,9 @@ SolveResult DeviceSolver::solve() {
     // same iterate.
     const bool three = fused_ && steps_ == 3;
     enqueue_wflush();
+    // (the check below is timed on its own: res.t.check, outside T_iterate / T_solver)
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    const auto t_chk = clk::now();
     if (three) {  // (after a fix-up: x[wpar] ← the r of the returned w)
       KParams kk = *kp_;
       kk.mlimit = dev::kReplay3;
@@ -1434,6 +1471,7 @@ SolveResult DeviceSolver::solve() {
     }
     if (fused_) residual_pass(three, three);
     read_state(&hs);
+    check_s += secs(t_chk, clk::now());
     const double hh = prob_.h1() * prob_.h2();
     if (three) {
       res.res_rec = std::sqrt(hs.res[1] * hh);
@@ -1477,7 +1515,8 @@ SolveResult DeviceSolver::solve() {
   harvest(recs_.size());
   float ms = 0;
   PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-  res.t.iterate = secs(t_loop, clk::now());
+  res.t.iterate = secs(t_loop, clk::now()) - check_s;
+  res.t.check = check_s;
   roctxRangePop();
 
   if (opt_.compute_error) {
@@ -1540,11 +1579,12 @@ SolveResult DeviceSolver::solve() {
     res.t.dot_fused = !(fused_ && kp_->order == 3 && !kp_->fold);
     if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
   }
-  res.t.solver = construct + secs(t_start, clk::now());
+  res.t.solver = construct + secs(t_start, clk::now()) - check_s;
   // Timers: max over ranks (reference MPI_Reduce(MAX), :962-966).
-  double tv[10] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate,
-                   res.t.dot, res.t.construct, res.t.wait};
-  comm_->host_max(tv, 10, stream_);
+  double tv[11] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate,
+                   res.t.dot, res.t.construct, res.t.wait, res.t.check};
+  comm_->host_max(tv, 11, stream_);
+  res.t.check = tv[10];
   res.t.wait = tv[9];
   res.t.gpu = tv[0];
   res.t.copy = tv[1];

@@ -59,8 +59,13 @@ hipStream_t acquire_stream() {
 
 void release_stream(hipStream_t s) {
   if (!s) return;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return;
+  // filed under the device the stream was created on, not the current one (a
+  // solver may be destroyed after the process moved to another device)
+  hipDevice_t dev = 0;
+  if (hipStreamGetDevice(s, &dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return;
+  }
   std::lock_guard<std::mutex> g(g_stream_mu);
   g_idle_streams.emplace_back(dev, s);
 }

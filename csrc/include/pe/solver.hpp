@@ -51,6 +51,7 @@ namespace pe {
 struct Timers {
   double gpu = 0, copy = 0, halo = 0, reduce = 0, prec = 0, dot = 0, setup = 0, solver = 0;
   double iterate = 0;  // wall time of the iteration loop only
+  double check = 0;    // the end-of-solve true-residual check (not in iterate / solver)
   double construct = 0, sampled = 0;
   double wait = 0;  // in-sweep cross-rank wait (see above)
   bool dot_fused = false;

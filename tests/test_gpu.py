@@ -281,6 +281,18 @@ def test_bench_contract(gpu):
     assert d["converged"] and d["l2_err"] < 1e-3
 
 
+@pytest.mark.parametrize("warmup", ["0", "5"])
+def test_bench_two_step_warmup_counts(gpu, warmup):
+    """The clock warm-up and an odd --warmup run whole two-step sweeps (an odd
+    count used to make run_iterations throw)."""
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--algo", "two-step", "--steps", "10",
+                          "--warmup", warmup, "--warmup-s", "0.05", "--no-solve", "--grid", "512", "512"],
+                         capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["valid"] and d["steps"] == 10 and d["clock_warmup_steps"] % 2 == 0
+
+
 def test_graft_smoke(gpu):
     sys.path.insert(0, ROOT)
     import __graft_entry__ as g

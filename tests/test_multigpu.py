@@ -131,7 +131,7 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     c = d["config"]
     assert c["decomposition"]["Px"] * c["decomposition"]["Py"] == nproc
     assert "rccl" in c["transport"]
-    # 2047 rows: slabs while every rank keeps >= 512 rows (2 and 4 GPUs) → the
+    # 2047 rows: slabs while every rank keeps >= 32 rows (decomp.cpp: every N here) → the
     # halo is pushed by the sweep and the iterations run as captured graphs
     assert c["halo"].startswith("in-sweep xGMI push") == (c["decomposition"]["Py"] == 1)
     for r in c["ranks"]:  # per-rank diagnostics of the first cross-device run

@@ -103,3 +103,41 @@ def test_16384_residual_gap(gpu):
     rep = solve(EllipseProblem(16384, 16384), backend="hip")
     assert rep.algo == THREE and rep.converged and rep.iters == GOLDEN_ITERS[(16384, 16384, "weighted")]
     assert rep.restarts == 0 and 0 <= rep.res_gap < GAP
+
+
+@pytest.mark.parametrize("nproc,decomp,extra", [(3, "rows", {}), (4, "2x2", {"PE_OVERLAP": "1"})])
+def test_drift_fault_restarts_multi_rank(gpu, tmp_path, nproc, decomp, extra):
+    """the residual replacement across ranks.  Row slabs restart
+    with the in-sweep halo push and P2P sums (the replay launch pushes rows
+    into the neighbours' receive buffers); the 2x2 split restarts with the
+    halo/interior overlap forced on (kSignal).  Processes share the one GPU
+    (host-staged base transport); w matches the single-rank clean solve."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    from conftest import free_port
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prob = EllipseProblem(1024, 1024)
+    clean = solve(prob, backend="hip", algo=THREE, return_w=True)
+    outp = str(tmp_path / "w.npy")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60",
+               PE_FAULT_INJECT="drift@iter:500,amp:1e-2", **extra)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd",
+           "--json", "--quiet", "--algo", THREE, "--decomp", decomp, "--dump", outp, "1024", "1024"]
+    out = subprocess.run(cmd, cwd=root, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([ln for ln in out.stdout.splitlines() if ln.startswith("{")][0])
+    assert d["ranks"] == nproc and d["converged"] and d["restarts"] >= 1, d
+    assert d["res_gap"] < GAP
+    if decomp == "rows":
+        assert d["halo_push"]
+    else:
+        assert d["overlap"]
+    w = np.load(outp)
+    dw = w - clean.w
+    assert np.sqrt((dw * dw).sum() * prob.h1 * prob.h2) < 1e-5
+    assert np.abs(dw).max() < 1e-3
