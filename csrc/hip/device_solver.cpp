@@ -429,7 +429,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
-  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
+  // (three-step: from 2¹⁷ nodes — the multi-rank blocks of the published
+  // grids, e.g. 399×1199 of 800×1200 on 2 ranks, run the streaming sweep)
+  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(steps_ == 3 ? 1 << 17 : 1 << 20) && npts < double(1 << 25);
   // Three-step static layout by block size, one placement per block
   // (tools/layout_probe.py, profiles/r4_layout2.txt, µs per iteration): the
   // LPT layout of whole items for ≥ 5·10⁷ nodes (8192²: 253 vs 260 filling,
@@ -439,7 +441,35 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // other two at their best rows per item.
   if (steps_ == 3) lay_name_ = npts >= 5e7 ? "lpt" : npts >= 2.5e7 ? "fill" : "equal";
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
-  const int ti_min = tune_ti_ ? (sstep_ ? tic[0] : kTiCands[0]) : ti;
+  // Tuning candidates: the fixed set plus, for q = 1..5 items per wave, the
+  // smallest item height that gives every wave at most q items — a static
+  // layout's sweep lasts as long as its most loaded wave, and 3.4 items per
+  // wave means a quarter of the waves runs a 4th item while the rest idle
+  // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78,
+  // tools/stamp_probe.py).  Three-step: down to 4 rows (q = 1) — a block with
+  // fewer strip-rows than ~32 per wave is latency-bound, and one short item
+  // per wave beats 32+-row items on a fraction of the waves despite its 12
+  // pipeline-fill rows (2-rank 1600×2400 block at 80 rows: 21 µs per
+  // iteration, profiles/r5_block_probe_base.txt).
+  std::vector<int> ti_cands;
+  if (tune_ti_) {
+    ti_cands.assign(kTiCands, kTiCands + 4);
+    if (sstep_) ti_cands.assign(tic, tic + 5);
+    // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
+    // at 18, one placement, profiles/r2_ti_big.txt)
+    if (npts >= 12e6 && !sstep_) ti_cands.insert(ti_cands.end(), {24, 30});
+    const int64_t W = std::max(dev::kWPB, wave_cap_);
+    const int tlo = steps_ == 3 ? 4 : sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
+    for (int q = steps_ == 3 ? 1 : 2; q <= 5; ++q)
+      for (int t = tlo; t <= thi; ++t)
+        if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
+          ti_cands.push_back(t);
+          break;
+        }
+    std::sort(ti_cands.begin(), ti_cands.end());
+    ti_cands.erase(std::unique(ti_cands.begin(), ti_cands.end()), ti_cands.end());
+  }
+  const int ti_min = tune_ti_ ? ti_cands.front() : ti;
   set_items(ti);
   // block partials: interior grid, then (overlap) the boundary grid after it
   const int64_t npart = 8 * std::max<int64_t>(2 * int64_t(std::max(wave_cap, wave_cap0) / dev::kWPB + 1), 4096);
@@ -485,28 +515,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // layout's sweep lasts as long as its most loaded wave, and 3.4 items per
     // wave means a quarter of the waves runs a 4th item while the rest idle
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
-    std::vector<int> cands(kTiCands, kTiCands + 4);
-    if (sstep_) cands.assign(tic, tic + 5);  // (+ 0: the segment layout, added below)
-    // taller items for the largest tuned blocks (4096²: 30 rows 158 µs vs 165
-    // at 18, one placement, profiles/r2_ti_big.txt)
-    if (npts >= 12e6 && !sstep_) cands.insert(cands.end(), {24, 30});
-    {
-      const int64_t W = std::max(dev::kWPB, wave_cap_);
-      const int tlo = sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
-      for (int q = 2; q <= 5; ++q)
-        for (int t = tlo; t <= thi; ++t)
-          if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
-            cands.push_back(t);
-            break;
-          }
-      std::sort(cands.begin(), cands.end());
-      cands.erase(std::unique(cands.begin(), cands.end()), cands.end());
-      // (two-step sweep, PE_TI_SEGMENTS=1: also one tall segment per wave — its
-      // 8 pipeline-fill rows re-read once per segment; it lost to the LPT items
-      // on the 2/4/8-rank 8192² slabs, 128 vs 110 µs per sweep at 8 ranks:
-      // profiles/r3_block_probe.txt)
-      if (sstep_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
-    }
+    // (candidates: ti_cands above)
+    std::vector<int> cands = ti_cands;
+    // (two-step sweep, PE_TI_SEGMENTS=1: also one tall segment per wave — its
+    // 8 pipeline-fill rows re-read once per segment; it lost to the LPT items
+    // on the 2/4/8-rank 8192² slabs, 128 vs 110 µs per sweep at 8 ranks:
+    // profiles/r3_block_probe.txt)
+    if (sstep_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
     float best_ms = 0.f;
     int best = ti;
     // one candidate: S_0 + 1 + kTimed local sweeps on real data, the last
@@ -566,11 +581,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
     const size_t nw = size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
-    nstamps_ = 4 * size_t(nslot_cap_) + 2 * nw + 32 * nw;
+    nstamps_ = 4 * size_t(nslot_cap_) + 2 * nw + 32 * nw + 8;  // (+8 whole-grid stamps: three-step sweep)
     PE_HIP_CHECK(hipMalloc(&stamps_, sizeof(unsigned long long) * nstamps_));
     PE_HIP_CHECK(hipMemsetAsync(stamps_, 0, sizeof(unsigned long long) * nstamps_, stream_));
     k.stamps = stamps_;
-    k.stamps2 = stamps_ + nstamps_ - 32 * nw;  // the last 32 × waves entries
+    k.stamps2 = stamps_ + nstamps_ - 32 * nw;  // the last 32 × waves entries (the 8 grid stamps before them)
   }
   // In-sweep cross-rank reduction (after the placement search, whose sweeps
   // are local and differ in number between ranks).  PE_XR=0 keeps the

@@ -610,9 +610,17 @@ __device__ __forceinline__ void group3(const KParams& k, const M3Ctx& c, M3Rings
 // sum has a factor among z, p, u, v, ũ, ṽ, which are exactly 0 at the
 // global-boundary and padding columns, and the lanes that do not own their
 // columns (0..7, 56..63) are dropped once, at the end of the sweep.
-template <int KIND, bool PUSH, bool EDGE>
+__device__ __forceinline__ unsigned long long rtc3() {
+  unsigned long long t;  // one asm statement: never merged or moved by the compiler
+  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+  return t;
+}
+
+// (SST, the diagnostic build only: sst != nullptr stamps this item's
+// prologue and every 6-step group into the wave's step stamps)
+template <int KIND, bool PUSH, bool EDGE, bool SST = false>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
-                                       WaveTV3& tvw, double (&sv)[NS]) {
+                                       WaveTV3& tvw, double (&sv)[NS], unsigned long long* sst = nullptr) {
   const int lane = threadIdx.x & 63;
   const int ny = int(k.ny);
   M3Ctx c;
@@ -686,6 +694,16 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   const int nsteps = ie + H3 - c.t0 + 1;
   const int rows = ie - ib + 1;
   int bs = 0;  // band ring slot of row t: (t - t0) mod 7
+  int sg = 3;  // (SST: next step-stamp slot)
+  if constexpr (SST) {
+    if (sst && lane == 0) sst[2] = rtc3();
+  }
+  auto sstamp = [&]() {
+    if constexpr (SST) {
+      if (sst && lane == 0 && sg < 31) sst[sg] = rtc3();
+      ++sg;
+    }
+  };
   // steady groups (uniform items): stage rows t-6 .. t and the prefetched
   // rows inside the item for all six steps (n ≥ 12, n ≤ rows + 4); the fill
   // and drain groups around them test rows.  Three loops, not one with a
@@ -698,15 +716,18 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   for (; n0 < nsteps && !(n0 >= 12 && n0 <= nsteady_end); n0 += 6) {
     reload(n0);
     group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+    sstamp();
   }
   if constexpr (KIND == kUniform) {
     for (; n0 <= nsteady_end; n0 += 6) {
       reload(n0);
       group3<KIND, PUSH, EDGE, true>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+      sstamp();
     }
     for (; n0 < nsteps; n0 += 6) {
       reload(n0);
       group3<KIND, PUSH, EDGE, false>(k, c, x, rx, tvw, sv, n0, nsteps, bs);
+      sstamp();
     }
   }
   if constexpr (PUSH) {
@@ -728,12 +749,6 @@ __device__ __forceinline__ Coef3 uni3(const Coef3& c) {
     u.cw[i] = uni(c.cw[i]);
   }
   return u;
-}
-
-__device__ __forceinline__ unsigned long long rtc3() {
-  unsigned long long t;  // one asm statement: never merged or moved by the compiler
-  asm volatile("s_memrealtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
-  return t;
 }
 
 // Walk this wave's positions of the static item list.
@@ -764,6 +779,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   // uses the whole grid: the construction's timing sweeps, S_0, the replay —
   // have no list positions; they used to march round r+1's first items twice)
   const int pend = gwave < W ? k.nslots : 0;
+  unsigned long long* sst = STAMP ? k.stamps2 + 32 * int64_t(gwave) : nullptr;  // (the first item only)
   for (int pos = gwave; pos < pend; pos += W) {
     const int2 e = cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
@@ -771,17 +787,24 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     const int s = e.y & 0xFFFFF, ib = e.x & kRowMask3;
     const int ie = min(ib + rows - 1, int(k.nx));
     const unsigned long long t_item = STAMP ? rtc3() : 0ull;
+    if constexpr (STAMP) {
+      if (sst && l0) sst[0] = t_item;
+    }
     if (e.x & kBandBit) {
-      march3<kBand, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+      march3<kBand, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
     } else if (e.x & kUniBit) {
       // edge strips (a global-boundary or padding column in the window) mask z
       const int c0 = -(HL3 - 1) + s * FSW3 + int(threadIdx.x & 63);
       const int64_t g0 = k.gj0 + c0;
       const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
-      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false>(k, cf, fix, par, s, ib, ie, tv, acc);
-      else march3<kUniform, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
+      else march3<kUniform, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
     } else {
-      march3<kMixed, PUSH, true>(k, cf, fix, par, s, ib, ie, tv, acc);
+      march3<kMixed, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
+    }
+    if constexpr (STAMP) {
+      if (sst && l0) sst[31] = rtc3();
+      sst = nullptr;
     }
     if constexpr (MODE == kSignal) {
       if (pos < k.lnb[0]) {  // a boundary item: count it once its stores have left (no L2 writeback here)
@@ -815,12 +838,20 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   constexpr bool replay = MODE == kReplay;
+  if constexpr (MODE == kStamp) {  // wave entry; the previous launch's finalize time (grid stamp 2 → 0)
+    const unsigned long long t_in = rtc3();
+    if (lane == 0) {
+      k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + 1] = t_in;
+      if (blockIdx.x == 0 && wid == 0) k.stamps2[-8] = k.stamps2[-6];
+    }
+  }
   if (done && !replay) return;
   auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
                             // the slots garbage pipeline-fill rows read stay finite)
     WaveTV3& tv = tvs[wid];
     for (int i = lane; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
     for (int i = lane; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
+    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.d0r[0][0])[i] = 0.0;
   };
   // terminal paths: every wave has read the state before the last one to
   // arrive writes it
@@ -913,6 +944,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     for (int n = 0; n < NS; ++n) acc[n] = 0.0;
   block_reduce<NS, false>(acc, sm);
   if (publish_last<NS>(k.partial + NS * size_t(blockIdx.x), acc, &st->ticket[0], gridDim.x, &sflag)) {
+    if constexpr (MODE == kStamp) {
+      if (threadIdx.x == 0) k.stamps2[-7] = rtc3();  // the last block starts the grid's reduction
+    }
     double t[NS];
     reduce_partials<NS>(k.partial, gridDim.x, t, sm);
     __shared__ double xv[NS + 1];
@@ -935,6 +969,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     if (threadIdx.x == 0) {
       sweep3_finalize(k, st, par, sc, t);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if constexpr (MODE == kStamp) k.stamps2[-6] = rtc3();  // finalized
     }
   }
 }

@@ -213,6 +213,7 @@ struct WaveTV1 {
   double half[65], sB[64], eB[64];
   double a0r[RING][64];
   double b0r[RING][66];  // (column 64: read by lane 63 for its b1, never written)
+  double d0r[RING][64];  // 1/D of the ring's rows, evaluated once at entry
 };
 
 // The strip's row-table entries (per column), once per band item.
@@ -255,6 +256,7 @@ __device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx
   }
   tv.a0r[sl][lane] = a0;
   tv.b0r[sl][lane] = b0;
+  tv.d0r[sl][lane] = d;
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
@@ -262,7 +264,10 @@ __device__ __forceinline__ double enter_band1(const KParams& k, const RowCtx& rx
 }
 
 // The 5-point operator at row q (ring slot sl, the row above it in slot sln)
-// for the lane's column; d = 1/D of the node.
+// for the lane's column; d = 1/D of the node — read from the ring: the row's
+// entry evaluated it once (cset_rc), where every stage used to form it again
+// from the four faces (an fp64 reciprocal per operator application, eight
+// per band row step).
 template <bool BAND, class WT>
 __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx, const WT& tv, int q, int c0, int sl,
                                              int sln, double um, double u0, double un, double& d) {
@@ -273,7 +278,7 @@ __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx,
   if (BAND && gen) {
     const double a0 = tv.a0r[sl][lane], a1 = tv.a0r[sln][lane];
     const double b0 = tv.b0r[sl][lane], b1 = tv.b0r[sl][lane + 1];
-    const CS x0{a0, a1, b0, b1, dinv_faces(k, a0, a1, b0, b1)};
+    const CS x0{a0, a1, b0, b1, tv.d0r[sl][lane]};
     d = x0.d;
     return stencil<false>(k, x0, um, u0, un, ul, ur);
   }

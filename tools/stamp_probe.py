@@ -29,26 +29,59 @@ def pct(a, q):
     return float(np.percentile(a, q)) if len(a) else float("nan")
 
 
-def step_timeline(steps: np.ndarray) -> str:
+def step_timeline(steps: np.ndarray, three: bool = False) -> str:
     """Median time (µs) from a wave's first item start to each stamped point of that item."""
     s = steps.reshape(-1, 32).astype(np.int64)
     s = s[s[:, 0] > 0]
     if not len(s):
         return "  (no step stamps)"
-    names = {1: "prologue issued", 2: "row classes in", 3: "prologue rows in", 31: "item end"}
-    out = ["  first-item timeline (median us after item start, n waves):"]
+    if three:  # fused3.hip kStamp: [1] kernel entry, [2] prologue issued, [3..30] after each 6-step group, [31] end
+        names = {1: "kernel entry (wave)", 2: "prologue issued", 31: "item end"}
+        names.update({c: f"after row step {6 * (c - 2):d}" for c in range(3, 31)})
+    else:
+        names = {1: "prologue issued", 2: "row classes in", 3: "prologue rows in", 31: "item end"}
+    out = ["  first-item timeline (median us after item start, n waves; per-group increment):"]
+    prev = None
     for c in range(1, 32):
         v = s[:, c]
         ok = v > 0
         if ok.sum() < max(1, len(s) // 4):
             continue
         d = (v[ok] - s[ok, 0]) / 100.0
-        out.append(f"    {names.get(c, f'after row step {c - 6:+d}'):22s} {np.median(d):7.2f}  (n {ok.sum()})")
+        med = float(np.median(d))
+        inc = "" if prev is None or c < 3 else f"  +{med - prev:6.2f}"
+        out.append(f"    {names.get(c, f'after row step {c - 6:+d}'):22s} {med:7.2f}{inc}  (n {ok.sum()})")
+        if c >= 2:
+            prev = med
     return "\n".join(out)
 
 
-def summarise(st: np.ndarray, nitems: int, nw: int) -> str:
+def grid_timeline(glob: np.ndarray, steps: np.ndarray, wv_all: np.ndarray) -> str:
+    """Three-step kStamp: the launch around the item walk — kernel entry, the
+    walk, the grid reduction and finalize, and the gap after the previous
+    launch's finalize (µs)."""
+    s = steps.reshape(-1, 32).astype(np.int64)
+    ent = s[:, 1][s[:, 1] > 0]
+    g = glob.astype(np.int64)
+    if not len(ent) or g[2] == 0:
+        return "  (no grid stamps)"
+    t0 = ent.min()
+    wv = wv_all[wv_all[:, 0] > 0]
+    first_items = s[:, 0][s[:, 0] > 0]
+    out = ["  launch timeline (us from the first wave's kernel entry):"]
+    if g[0] > 0:
+        out.append(f"    gap after the previous launch's finalize: {(t0 - g[0]) / 100.0:7.2f}")
+    out.append(f"    wave kernel entry: median {np.median(ent - t0) / 100.0:6.2f}  max {(ent.max() - t0) / 100.0:6.2f}")
+    out.append(f"    walk entry (scalars + ring): median {np.median(wv[:, 0] - t0) / 100.0:6.2f}")
+    out.append(f"    first item start: median {np.median(first_items - t0) / 100.0:6.2f}")
+    out.append(f"    last wave exit {(wv[:, 1].max() - t0) / 100.0:7.2f}; grid reduction start {(g[1] - t0) / 100.0:7.2f}; "
+               f"finalized {(g[2] - t0) / 100.0:7.2f}")
+    return "\n".join(out)
+
+
+def summarise(st: np.ndarray, nitems: int, nw: int, three: bool = False) -> str:
     steps = st[len(st) - 32 * nw:]
+    glob = st[len(st) - 32 * nw - 8: len(st) - 32 * nw]
     st = st[: len(st) - 32 * nw]
     nslots = nitems
     it = st[: 4 * nslots].reshape(nslots, 4).astype(np.int64)
@@ -154,7 +187,9 @@ def summarise(st: np.ndarray, nitems: int, nw: int) -> str:
         ratio = wl_all[m] / wc[m]
         out.append(f"  wave time / static cost: p10 {pct(ratio, 10):.3f} median {np.median(ratio):.3f} p90 {pct(ratio, 90):.3f}"
                    f"  (corr of wave time with cost {np.corrcoef(wl_all[m], wc[m])[0, 1]:.2f})")
-    out.append(step_timeline(steps))
+    out.append(step_timeline(steps, three))
+    if three:
+        out.append(grid_timeline(glob, steps, wv_all))
     return "\n".join(out)
 
 
@@ -179,12 +214,17 @@ def main():
             dt = s.time_iterations(40, False)
             print(f"P={P} {g.Px}x{g.Py} block {blk.nx}x{blk.ny} [{env or 'default'}] ti={s.ti} order={s.order}: "
                   f"{dt / 40 * 1e6:.1f} us/iter (stamped build)", flush=True)
+            three = int(s.sweep_steps) == 3
+            s.clear_stamps()
+            if three:  # (a launch records the previous one's finalize: the gap between launches)
+                s.run_iterations(1, False)
             for sweep in ("deferring", "applying"):  # iterations alternate the two sweep variants
-                s.clear_stamps()
+                if not three:
+                    s.clear_stamps()
                 s.run_iterations(1, False)
                 st = np.asarray(s.stamps())
                 print(f" one {sweep}-parity sweep:")
-                print(summarise(st, s.nitems, s.stamp_waves), flush=True)
+                print(summarise(st, s.nitems, s.stamp_waves, three), flush=True)
             del s, comm
             for k, v in saved.items():
                 if v is None:
