@@ -335,12 +335,6 @@ struct M3Rings {
   bool pushed;
 };
 
-// Row scalars of a uniform row: 1/h1², 1/h2² times the row's face
-// coefficient, and 1/D (0 outside the global interior rows).
-struct URow {
-  double ih1, ih2, d;
-};
-
 template <bool STEADY>
 __device__ __forceinline__ URow urow(const M3Ctx& c, const RowCtx& rx, int q) {
   const int l = (q - rx.segbase) & 63;
@@ -353,12 +347,6 @@ __device__ __forceinline__ URow urow(const M3Ctx& c, const RowCtx& rx, int q) {
     if (!(q >= c.rlo && q <= c.rhi)) r.d = 0.0;
   }
   return r;
-}
-
-// The 5-point operator of a uniform row on the lane's column.
-__device__ __forceinline__ double lapu(const URow& r, double um, double u0, double un) {
-  const double ul = dpp_shr1(u0), ur = dpp_shl1(u0);
-  return ((u0 - um) - (un - u0)) * r.ih1 + ((u0 - ul) - (ur - u0)) * r.ih2;
 }
 
 template <bool PUSH>

@@ -58,12 +58,12 @@ struct DevState {
   // Multi-step sweeps: the unweighted sums of sweep k in fs2[k & 1] — 20
   // (two-step, layout: fused2.hip, sweep2_scalars) or 19 (three-step:
   // fused3.hip, sweep3_scalars).
-  double fs2[2][24];
+  double fs2[2][32];
   // Three-step sweep (fused3.hip): the last sweep's coefficients {zc[3],
   // α[3], β[3], g[3]}; late3 of its iterations (ending at iter) still await
   // their stop tests (decided by the next launch from fs2[wpar]); brk3 > 0:
   // the iteration that breaks down after them (bad3: non-finite scalars).
-  double sc3[12];
+  double sc3[16];
   long long brk3;
   int late3;
   int bad3;
@@ -88,7 +88,7 @@ struct DevState {
 // peers[r] = rank r's buffer (2 × P slots of kP2PSlot doubles: n ≤ kP2PSlot-1
 // values + a sequence flag) mapped into this process, seq = this rank's
 // reduction counter (device), timeout in s_memrealtime ticks (100 MHz).
-constexpr int kP2PSlot = 24;  // ≥ 20 sums of the two-step sweep + the flag
+constexpr int kP2PSlot = 32;  // ≥ 26 sums of the four-step sweep + the flag
 struct PeerSum {
   double* const* peers;
   unsigned long long* seq;

@@ -286,6 +286,19 @@ __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx,
   return lap(k, in0 ? 1.0 : k.inv_eps, um, u0, un, ul, ur);
 }
 
+// Row scalars of a uniform row (fused3.hip / fused4.hip uniform items):
+// 1/h1², 1/h2² times the row's face coefficient, and 1/D (0 outside the
+// global interior rows).
+struct URow {
+  double ih1, ih2, d;
+};
+
+// The 5-point operator of a uniform row on the lane's column.
+__device__ __forceinline__ double lapu(const URow& r, double um, double u0, double un) {
+  const double ul = dpp_shr1(u0), ur = dpp_shl1(u0);
+  return ((u0 - um) - (un - u0)) * r.ih1 + ((u0 - ul) - (ur - u0)) * r.ih2;
+}
+
 __device__ __forceinline__ double dinv_plain1(const KParams& k, const RowCtx& rx, int q, int c0) {
   bool in0, gen;
   row_in1(rx, q, c0, in0, gen);
