@@ -334,12 +334,12 @@ PYBIND11_MODULE(_native, m) {
       py::arg("uid"), py::arg("rank"), py::arg("size"));
   m.def(
       "make_delay_comm",
-      [](int size, double exchange_us, double allreduce_us) {
+      [](int size, double exchange_us, double allreduce_us, bool loopback) {
         auto h = std::make_unique<CommHandle>();
-        h->comm = make_delay_comm(size, exchange_us, allreduce_us);
+        h->comm = make_delay_comm(size, exchange_us, allreduce_us, loopback);
         return h;
       },
-      py::arg("size"), py::arg("exchange_us"), py::arg("allreduce_us"));
+      py::arg("size"), py::arg("exchange_us"), py::arg("allreduce_us"), py::arg("loopback") = false);
   m.def(
       "make_host_staged_comm",
       [](int rank, int size, py::function reduce_fn, py::function exchange_fn, py::function barrier_fn) {

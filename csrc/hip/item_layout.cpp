@@ -339,6 +339,8 @@ void DeviceSolver::setup_items() {
     // three-step layouts: PE_LAYOUT forces one; else the construction's
     // choice (lay_name_: by block size, or by the rows-per-item tuning)
     std::string lay = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : lay_name_;
+    // (the overlap's short boundary pieces: the filling layout, below)
+    if (overlap_ && !std::getenv("PE_LAYOUT")) lay = "fill";
     const bool s3lay = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
     if (!s3lay) lay = "lpt";
     const bool equal = s3lay && lay == "equal";
@@ -529,11 +531,43 @@ void DeviceSolver::setup_items() {
       };
       std::vector<Piece> whole;
       double total = 0.0;
+      // Overlap (2-D blocks): the outputs the exchange sends become short
+      // pieces of their own — the H rows next to a LEFT / RIGHT neighbour per
+      // strip, and a DOWN / UP boundary strip cut into kOvRows-row pieces — so
+      // they all run in the first round and finish within ~(kOvRows + 2H) row
+      // steps; the filling below then tops their waves up with interior rows
+      // (later list positions).  With whole ti-row boundary items and about one
+      // item per wave the boundary items ended with the sweep and a third of
+      // the exchange stayed exposed (4×2 block: 56.8 vs 50.9 µs per
+      // iteration at 15 / 8 µs delays, profiles/r4_overlap.txt).
+      constexpr int64_t kOvRows = 8;
+      const bool ov_split = overlap_ && !(ov_debug_ & 4);
+      auto ystrip = [&](int sx) {
+        const int64_t J = -(HL - 1) + int64_t(sx) * fsw_;
+        const int64_t jlo = std::max<int64_t>(1, J + HL), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + HL - 1);
+        return (blk_.has(DOWN) && jlo <= H) || (blk_.has(UP) && jhi >= blk_.ny - H + 1);
+      };
+      auto add_whole = [&](int64_t a, int64_t rows, int sx, bool bnd) {
+        whole.push_back(Piece{a, rows, sx, pcost(a, rows, sx), bnd});
+        total += whole.back().cost;
+      };
       for (int ch = 0; ch < nchunks; ++ch)
         for (int sx = 0; sx < k.nstrips; ++sx) {
           const int64_t ib = 1 + int64_t(ch) * k.ti, n = std::min<int64_t>(ib + k.ti - 1, blk_.nx) - ib + 1;
-          whole.push_back(Piece{ib, n, sx, pcost(ib, n, sx), is_boundary(ib, ib + n - 1, sx)});
-          total += whole.back().cost;
+          const int64_t ie = ib + n - 1;
+          if (!ov_split || !is_boundary(ib, ie, sx)) {
+            add_whole(ib, n, sx, is_boundary(ib, ie, sx));
+          } else if (ystrip(sx)) {
+            for (int64_t a = ib; a <= ie; a += kOvRows) add_whole(a, std::min<int64_t>(kOvRows, ie - a + 1), sx, true);
+          } else {
+            const int64_t lo = blk_.has(LEFT) ? std::min<int64_t>(ie, H) : ib - 1;             // rows ib .. lo: LEFT's
+            const int64_t hi = blk_.has(RIGHT) ? std::max<int64_t>(ib, blk_.nx - H + 1) : ie + 1;  // hi .. ie: RIGHT's
+            if (lo >= ib) add_whole(ib, lo - ib + 1, sx, true);
+            const int64_t m0 = std::max(ib, lo + 1), m1 = std::min(ie, hi - 1);
+            if (m1 >= m0) add_whole(m0, m1 - m0 + 1, sx, false);
+            const int64_t r0 = std::max(hi, std::max(ib, lo + 1));  // (never a row of the LEFT piece again)
+            if (r0 <= ie) add_whole(r0, ie - r0 + 1, sx, true);
+          }
         }
       const int64_t minr = 8;  // shortest cut piece (its 2H fill rows cost more than it)
       const double minc = double(minr + 2 * H) + overhead;
@@ -603,6 +637,21 @@ void DeviceSolver::setup_items() {
       }
       lay_cuts_ = cuts;
     } else {
+    // Three-step LPT: cost an item by its march KIND — a band item runs every
+    // row step on the band path (≈2.25× a uniform one at 8192²: 221.8 vs
+    // 98.6 µs per 112-row item, profiles/r4_stamps48.txt), not only its band
+    // rows.  Weighted by band rows alone, a band item looked barely heavier
+    // than a uniform one, the LPT order left it among a wave's last items, and
+    // the sweep ended with band items of the last rows (6945-7169) starting
+    // 607-631 µs into a 722 µs span: a 33-40 µs tail.  Costed by kind they
+    // are laid out first.  PE_LPT_KIND=0: the band-row weights.
+    if (steps_ == 3 && !(std::getenv("PE_LPT_KIND") && std::atoi(std::getenv("PE_LPT_KIND")) == 0)) {
+      for (Piece& p : pcs) {
+        const int2 e = entry(p.ib, p.rows, p.s);
+        const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
+        p.cost = double(p.rows + 2 * H) * f + overhead;
+      }
+    }
     per.assign(size_t(W), {});
     load.assign(size_t(W), 0.0);
     std::vector<int> order;

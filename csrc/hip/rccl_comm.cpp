@@ -106,16 +106,28 @@ class RcclComm final : public DeviceComm {
 // Timing-only test transport: every exchange / allreduce is a stream-ordered
 // busy wait of a fixed duration (no data moves).  Lets one GPU measure how
 // much of a given communication latency the halo/interior overlap hides.
+// loopback: the exchange also moves data, asynchronously — after the wait,
+// each message's send buffer is copied into its own receive buffer by a
+// stream-ordered device-to-device copy (a rank that is its own neighbour on
+// every side).  Nothing synchronises the host, as with RCCL, so a run with the
+// halo/interior overlap must end bitwise where the serial one does: any
+// ordering hole (pack before the boundary items' stores, next sweep before
+// the unpack) shows up as different data.
 class DelayComm final : public DeviceComm {
  public:
-  DelayComm(int size, double exchange_us, double allreduce_us)
-      : size_(size), ex_us_(exchange_us), ar_us_(allreduce_us) {}
+  DelayComm(int size, double exchange_us, double allreduce_us, bool loopback)
+      : size_(size), ex_us_(exchange_us), ar_us_(allreduce_us), loop_(loopback) {}
   int rank() const override { return 0; }
   int size() const override { return size_; }
   void allreduce_sum(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
   void allreduce_max(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
   void exchange(const std::vector<Exchange>& ex, hipStream_t s) override {
-    if (!ex.empty()) dev::launch_delay(ex_us_, s);
+    if (ex.empty()) return;
+    dev::launch_delay(ex_us_, s);
+    if (loop_)
+      for (const Exchange& e : ex)
+        if (e.count > 0 && e.send && e.recv && e.send != e.recv)
+          PE_HIP_CHECK(hipMemcpyAsync(e.recv, e.send, sizeof(double) * size_t(e.count), hipMemcpyDeviceToDevice, s));
   }
   void host_max(double*, int, hipStream_t) override {}
   void barrier(hipStream_t) override {}
@@ -125,6 +137,7 @@ class DelayComm final : public DeviceComm {
  private:
   int size_;
   double ex_us_, ar_us_;
+  bool loop_;
 };
 
 class HostStagedComm final : public DeviceComm {
@@ -175,8 +188,8 @@ class HostStagedComm final : public DeviceComm {
 
 }  // namespace
 
-std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us) {
-  return std::make_unique<DelayComm>(size, exchange_us, allreduce_us);
+std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us, bool loopback) {
+  return std::make_unique<DelayComm>(size, exchange_us, allreduce_us, loopback);
 }
 
 std::unique_ptr<DeviceComm> make_callback_device_comm(int rank, int size, CallbackHostComm::ReduceFn reduce,

@@ -96,7 +96,9 @@ std::unique_ptr<DeviceComm> make_rccl_comm_from_handle(void* nccl_comm);
 // for several ranks sharing one GPU (RCCL refuses duplicate devices); the
 // production transport is RCCL.
 // Timing-only test transport (stream-ordered busy waits; no data moves).
-std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us);
+// loopback: the exchange also copies each send buffer into its own receive
+// buffer, stream-ordered (an asynchronous transport that moves data).
+std::unique_ptr<DeviceComm> make_delay_comm(int size, double exchange_us, double allreduce_us, bool loopback = false);
 // One-shot P2P allreduce (IPC-mapped receive buffers, p2p.hip) for the
 // per-iteration sums; everything else through `base` (PE_ALLREDUCE=p2p).
 std::unique_ptr<DeviceComm> make_p2p_allreduce_comm(std::unique_ptr<DeviceComm> base);

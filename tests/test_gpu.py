@@ -899,3 +899,43 @@ def test_fast_coefficients_vs_assembly(gpu, nat, M, N, kw):
     dref = 1.0 / Dt[1:M, 1:N]
     rel = np.abs(di[1:M, 1:N] - dref) / dref
     assert rel.max() <= (inv_eps + 4.0) * np.spacing(1.0)
+
+
+@pytest.mark.parametrize("spec,P", [("4x2", 8), ("2x2", 4)])
+def test_overlap_async_loopback_transport_bitwise(gpu, monkeypatch, spec, P):
+    """the halo/interior overlap through an ASYNCHRONOUS
+    transport that moves data.  The loopback delay transport waits 150 µs on
+    the stream (longer than a sweep of this block), then copies every send
+    buffer into its receive buffer with a stream-ordered device copy — no host
+    synchronisation anywhere, as with RCCL.  The same layout and kernel
+    (kSignal) run once with the exchange serialised on the solver stream
+    (PE_OV_DEBUG=2) and once on the halo stream (kWaitSig → pack → exchange →
+    unpack → event → next sweep): any ordering hole — the pack before the
+    boundary items' stores, the next sweep before the unpack — changes the
+    data, so the two must agree bitwise."""
+    from poisson_ellipse_openmp_mpi_cuda_amd._loader import native
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+    nat = native()
+    M = N = 1024
+    prob = EllipseProblem(M, N)
+    g = D.grid(P, M, N, spec)
+    blk = nat.decompose(M, N, g, P // 2)
+    out = {}
+    for dbg in ("2", "0"):
+        monkeypatch.setenv("PE_OVERLAP", "1")
+        monkeypatch.setenv("PE_OV_DEBUG", dbg)
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        comm = nat.make_delay_comm(P, 150.0, 3.0, True)
+        s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
+        assert s.overlap and s.sweep_steps == 3
+        s.reset()
+        s.run_iterations(45, False)
+        s.synchronize()
+        out[dbg] = (s.state(), s.w())
+        del s, comm
+    (st0, w0), (st1, w1) = out["2"], out["0"]
+    assert st0["iter"] == st1["iter"] and st0["status"] == st1["status"]
+    assert st0["fs2"] == st1["fs2"]
+    np.testing.assert_array_equal(w0, w1)

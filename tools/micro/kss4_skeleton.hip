@@ -35,6 +35,13 @@
 //   I  row t−8  Au₃, Av₃                                  μ7
 // Everything is written for a general S (template parameter, S ≤ 4: the
 // w-partial above covers p₁ only); kS4 instantiates S = 4.
+//
+// STATUS: a register skeleton, not built into the solver (VERDICT r4 item 6,
+// profiles/r5_sstep4.txt).  It compiles to 256 VGPRs + 187..300 spilled at
+// two waves per SIMD, or 304..312 registers at one — the decision record:
+//   hipcc -O3 -std=c++17 -Icsrc/include -Icsrc/hip --offload-arch=gfx950 \
+//     -ffp-contract=off --cuda-device-only -c tools/micro/kss4_skeleton.hip \
+//     -o /tmp/kss4.o -Rpass-analysis=kernel-resource-usage
 #include <cstdlib>
 #include <type_traits>
 
