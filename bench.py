@@ -75,7 +75,7 @@ def parse_args(argv):
     ap.add_argument("--no-random-solve", action="store_true", help="skip the (untimed) random-init solve")
     ap.add_argument("--seed", type=int, default=1234, help="random-init w0 seed")
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused", "two-step", "three-step"))
+    ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused", "two-step", "three-step", "four-step"))
     # eager by default: a 20-step window launched eagerly took 5.29-5.41 ms
     # against 5.30-5.85 ms replayed from its chunk graph (the first replay of
     # a window sometimes paid ~0.5 ms more: profiles/r3_window.txt)
@@ -193,7 +193,7 @@ def main(argv=None) -> int:
     opt = nat.SolveOptions()
     opt.check_tol = False  # fixed work per step in the timed region
     opt.variant = a.variant
-    opt.algo = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4}[a.algo]
+    opt.algo = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4, "four-step": 5}[a.algo]
     solver = nat.DeviceSolver(P, blk, comm, opt)
 
     def barrier():
@@ -339,7 +339,7 @@ def main(argv=None) -> int:
                             + ("(xGMI halo push + P2P sums)" if solver.halo_push else "(RCCL halo)"))
             if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
-            "algo": (f"{['', '', 'two', 'three'][solver.sweep_steps]}-step sweep (1 kernel + 1 reduction per "
+            "algo": (f"{['', '', 'two', 'three', 'four'][solver.sweep_steps]}-step sweep (1 kernel + 1 reduction per "
                      f"{solver.sweep_steps} iterations)" if solver.two_step else
                      "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else
                      "classic (2 kernels, 2 allreduces / iter)"),

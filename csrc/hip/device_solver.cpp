@@ -99,11 +99,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     };
     const bool two_ok = fused_ && (single(8) || slabs(8));
     const bool three_ok = fused_ && (single(8) || slabs(12) || grid2d(12) || vgroup(12));
+    // four-step (fused4.hip): an 8-deep halo — 16 rows / columns per block
+    const bool four_ok = fused_ && (single(16) || slabs(16) || grid2d(16) || vgroup(16));
     if (opt_.algo == 3 && !two_ok)
       throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
     if (opt_.algo == 4 && !three_ok)
       throw std::invalid_argument(
           "three-step sweep: single-rank blocks of >= 8 x 8 nodes, row slabs of >= 12 rows or 2-D blocks of >= 12 x 12");
+    if (opt_.algo == 5 && !four_ok)
+      throw std::invalid_argument(
+          "four-step sweep: single-rank blocks of >= 16 x 16 nodes, row slabs of >= 16 rows or 2-D blocks of >= 16 x 16");
     // auto: every single-rank block the LDS-resident kernel cannot hold
     // (1x MI355X, fresh processes, T_solver two-step vs single sweep:
     // 1600×2400 0.110 vs 0.127 s, 2048² 0.113 vs 0.133, 4096² 0.378 vs 0.584,
@@ -125,11 +130,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     bool auto_ms = slabs(8) || grid2d(12) || vgroup(12) || !resident_likely;
     if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
     int want = 3;
-    if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
+    if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(4, std::atoi(e)));
     steps_ = 1;
     if (opt_.algo == 3) steps_ = 2;
     else if (opt_.algo == 4) steps_ = 3;
-    else if (opt_.algo == 0 && auto_ms) steps_ = (want >= 3 && three_ok) ? 3 : (want >= 2 && two_ok) ? 2 : 1;
+    else if (opt_.algo == 5) steps_ = 4;
+    else if (opt_.algo == 0 && auto_ms)
+      steps_ = (want >= 4 && four_ok) ? 4 : (want >= 3 && three_ok) ? 3 : (want >= 2 && two_ok) ? 2 : 1;
     sstep_ = steps_ > 1;
   }
 
@@ -205,9 +212,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // rows -1 .. nx+4 (two prefetch rows past the halo).  x[b] interleaves the
     // r and p planes by row.  Two-step sweep: halo depth 4 — columns -3 ..
     // 120·nstrips+4, rows -3 .. nx+6.
-    fsw_ = steps_ == 3 ? dev::kFSW3 : steps_ == 2 ? dev::kFSW2 : dev::kFSW;
+    fsw_ = steps_ >= 3 ? dev::kFSW3 : steps_ == 2 ? dev::kFSW2 : dev::kFSW;
     hdep_ = 2 * steps_;
-    xorg_ = steps_ == 3 ? dev::kHL3 - 1 : hdep_ - 1;
+    xorg_ = steps_ >= 3 ? dev::kHL3 - 1 : hdep_ - 1;
     strips = (ny + fsw_ - 1) / fsw_;
     plane_ = ((fsw_ * strips + 2 * hdep_ + 7) / 8) * 8;
     // Three-step: strip s loads columns 48s-7 .. 48s+56 (one per lane) and
@@ -216,7 +223,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // lines and its stores 6 whole 64-B segments of r, p and w (52 outputs of
     // 64 loaded straddled 64-B segments: partial writes from two strips, and
     // 5 lines touched for 4 lines of data).
-    if (steps_ == 3) plane_ = ((xorg_ + fsw_ * (strips - 1) + 64 - dev::kHL3 + 1 + 15) / 16) * 16;
+    if (steps_ >= 3) plane_ = ((xorg_ + fsw_ * (strips - 1) + 64 - dev::kHL3 + 1 + 15) / 16) * 16;
     if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
     const int64_t rows = nx + 2 * hdep_ + 2;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
@@ -239,7 +246,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     rows_hi = sstep_ ? nx + hdep_ + 2 : nx + 3;
     cols_hi = sstep_ ? fsw_ * strips + hdep_ + 3 : dev::kFSW * strips + 3;
     tab_lo_ = sstep_ ? -hdep_ : -1;
-    if (steps_ == 3) {  // the last strip's last lane + 3; the first strip's lane 0 is column -xorg
+    if (steps_ >= 3) {  // the last strip's last lane + 3; the first strip's lane 0 is column -xorg
       cols_hi = fsw_ * (strips - 1) + 64 - dev::kHL3 + 3;
       tab_lo_ = -(xorg_ + 1);
     }
@@ -379,8 +386,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   if (sstep_) {  // static LPT layout only; taller items (2·hdep pipeline-fill rows each)
     // (three-step beyond 2²⁶ nodes: 128 rows — 16384² 978 vs 999 µs/iteration
     // at 80, one placement, profiles/r3_ti_final.txt)
-    if (ti_env == 0) ti = steps_ == 3 ? (huge ? 448 : npts >= double(1 << 25) ? 112 : big ? 80 : 48) : (big ? 40 : 24);
-    ti = std::max(4, std::min(ti, steps_ == 3 ? dev::kTImax3 : dev::kTImax2));
+    if (ti_env == 0) ti = steps_ >= 3 ? (huge ? 448 : npts >= double(1 << 25) ? 112 : big ? 80 : 48) : (big ? 40 : 24);
+    ti = std::max(4, std::min(ti, steps_ >= 3 ? dev::kTImax3 : dev::kTImax2));
     k.order = 0;
   }
   if (const char* e = std::getenv("PE_ORDER")) k.order = std::atoi(e);
@@ -428,10 +435,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // tools/block_probe.py, profiles/r4_ti48.txt.
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
-  const int* tic = steps_ == 3 ? kTiCands3 : kTiCands2;
+  const int* tic = steps_ >= 3 ? kTiCands3 : kTiCands2;
   // (three-step: from 2¹⁷ nodes — the multi-rank blocks of the published
   // grids, e.g. 399×1199 of 800×1200 on 2 ranks, run the streaming sweep)
-  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(steps_ == 3 ? 1 << 17 : 1 << 20) && npts < double(1 << 25);
+  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(steps_ >= 3 ? 1 << 17 : 1 << 20) && npts < double(1 << 25);
   // Three-step static layout by block size, one placement per block
   // (tools/layout_probe.py, profiles/r4_layout2.txt, µs per iteration): the
   // LPT layout of whole items for ≥ 5·10⁷ nodes (8192²: 253 vs 260 filling,
@@ -439,7 +446,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // 137 vs 145-147), the equal-cost one below (4-rank block 83.4-84.2 vs
   // 87.4-87.9 LPT, 8-rank block 45.1 vs 47.6-49.6); tuned blocks also try the
   // other two at their best rows per item.
-  if (steps_ == 3) lay_name_ = npts >= 5e7 ? "lpt" : npts >= 2.5e7 ? "fill" : "equal";
+  if (steps_ >= 3) lay_name_ = npts >= 5e7 ? "lpt" : npts >= 2.5e7 ? "fill" : "equal";
   if (const char* e = std::getenv("PE_TI_TUNE")) tune_ti_ = tune_ti_ && std::atoi(e) != 0;
   // Tuning candidates: the fixed set plus, for q = 1..5 items per wave, the
   // smallest item height that gives every wave at most q items — a static
@@ -459,8 +466,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // at 18, one placement, profiles/r2_ti_big.txt)
     if (npts >= 12e6 && !sstep_) ti_cands.insert(ti_cands.end(), {24, 30});
     const int64_t W = std::max(dev::kWPB, wave_cap_);
-    const int tlo = steps_ == 3 ? 4 : sstep_ ? tic[0] : kTiCands[0], thi = steps_ == 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
-    for (int q = steps_ == 3 ? 1 : 2; q <= 5; ++q)
+    const int tlo = steps_ >= 3 ? 4 : sstep_ ? tic[0] : kTiCands[0], thi = steps_ >= 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
+    for (int q = steps_ >= 3 ? 1 : 2; q <= 5; ++q)
       for (int t = tlo; t <= thi; ++t)
         if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
           ti_cands.push_back(t);
@@ -558,7 +565,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     }
     seg_layout_ = best == 0;
     // three-step: the other static layouts at the best height
-    if (steps_ == 3 && best != 0 && !std::getenv("PE_LAYOUT")) {
+    if (steps_ >= 3 && best != 0 && !std::getenv("PE_LAYOUT")) {
       const std::string base = lay_name_;
       std::string keep = base;
       for (const char* alt : {"equal", "fill", "lpt"}) {
@@ -759,7 +766,7 @@ void DeviceSolver::setup_halo_push() {
 
 void DeviceSolver::relayout(int ti, int order) {
   if (!fused_ || resident_) return;
-  ti = std::max(2, std::min(ti, steps_ == 3 ? dev::kTImax3 : 64));
+  ti = std::max(2, std::min(ti, steps_ >= 3 ? dev::kTImax3 : 64));
   const int ord = (order == 0 || order == 3) ? order : kp_->order;  // static LPT list / dynamic per-XCD queue
   // the item-sum slots of the dynamic order and the fold buffer were sized at
   // construction: a layout that needs more is refused before anything
@@ -1012,7 +1019,7 @@ void DeviceSolver::enqueue_error() { dev::launch_error(*kp_, stream_); }
 // sums them over ranks itself (k.xr, P2P transport).
 void DeviceSolver::enqueue_fs_reduce(int par) {
   if (kp_->xr.peers) return;
-  if (sstep_) comm_->allreduce_sum(st_->fs2[par], steps_ == 3 ? dev::kNS3 : dev::kNS2, stream_);
+  if (sstep_) comm_->allreduce_sum(st_->fs2[par], dev::sweep_sums(steps_), stream_);
   else comm_->allreduce_sum(st_->fs[par], 7, stream_);
 }
 
@@ -1207,7 +1214,7 @@ void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   }
   for (; it < iters; it += per) {
     sampling_ = it < sample_iters;
-    enqueue_iteration(par_, steps_ == 3 && iters - it < per ? iters - it : 0);
+    enqueue_iteration(par_, steps_ >= 3 && iters - it < per ? iters - it : 0);
     par_ ^= 1;
   }
   sampling_ = false;
@@ -1247,7 +1254,7 @@ void DeviceSolver::wait_event(hipEvent_t ev) {
 
 void DeviceSolver::enqueue_wflush() {
   if (!fused_) return;
-  if (steps_ == 3) {  // the last sweep's pending stop tests (and its w fix-up when it converged early)
+  if (steps_ >= 3) {  // the last sweep's pending stop tests (and its w fix-up when it converged early)
     KParams kk = *kp_;
     kk.mlimit = -1;
     dev::launch_S(kk, par_, stream_);
@@ -1331,7 +1338,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
-  res.algo = resident_ ? "resident" : steps_ == 3 ? "three-step" : steps_ == 2 ? "two-step" : fused_ ? "fused" : "classic";
+  res.algo = resident_ ? "resident" : steps_ == 4 ? "four-step" : steps_ == 3 ? "three-step" : steps_ == 2 ? "two-step" : fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   // T_solver spans construction (allocation, tables, placement search) like
@@ -1474,7 +1481,7 @@ SolveResult DeviceSolver::solve() {
     // fix-up (the solve stopped inside the last sweep), the replay launch
     // first recomputes that iterate's r into x[wpar], so w and r belong to the
     // same iterate.
-    const bool three = fused_ && steps_ == 3;
+    const bool three = fused_ && steps_ >= 3;  // (three- or four-step: the moment recurrence)
     enqueue_wflush();
     // (the check below is timed on its own: res.t.check, outside T_iterate / T_solver)
     PE_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1668,7 +1675,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   // `steps` iterations, the exchange after each, the kNS3 sums summed here
   const int steps = s[0]->sweep_steps();
   const bool ms = s[0]->two_step();
-  const int nsum = steps == 3 ? dev::kNS3 : steps == 2 ? dev::kNS2 : 7;
+  const int nsum = dev::sweep_sums(steps);
   std::vector<hipEvent_t> ev(ranks);
   for (auto& e : ev) PE_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
   // Device pointer tables for the cross-rank reduction kernel:
@@ -1811,7 +1818,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   PE_HIP_CHECK(hipFree(dp));
   for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
   res.backend = "hip-group";
-  res.algo = steps == 3 ? "three-step" : steps == 2 ? "two-step" : fused ? "fused" : "classic";
+  res.algo = steps == 4 ? "four-step" : steps == 3 ? "three-step" : steps == 2 ? "two-step" : fused ? "fused" : "classic";
   res.Px = pg.Px;
   res.Py = pg.Py;
   res.t.solver = secs(t_start, clk::now());

@@ -1295,6 +1295,10 @@ static auto with_kS(const KParams& k, F&& f) {
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
+  if (k.steps == 4) {  // four iterations per sweep (fused4.hip)
+    launch_S4(k, par, s);
+    return;
+  }
   if (k.steps == 3) {  // three iterations per sweep (fused3.hip)
     launch_S3(k, par, s);
     return;
@@ -1352,6 +1356,7 @@ void launch_wflush(const KParams& k, hipStream_t s) {
 }
 
 int resident_blocks_S(const KParams& k, int wm) {
+  if (k.steps == 4) return resident_blocks_S4();
   if (k.steps == 3) return resident_blocks_S3();
   if (k.steps == 2) return resident_blocks_S2();
   auto occ = [](auto kern) {

@@ -36,12 +36,12 @@
 // Everything is written for a general S (template parameter, S ≤ 4: the
 // w-partial above covers p₁ only); kS4 instantiates S = 4.
 //
-// STATUS: a register skeleton, not built into the solver (VERDICT r4 item 6,
-// profiles/r5_sstep4.txt).  It compiles to 256 VGPRs + 187..300 spilled at
-// two waves per SIMD, or 304..312 registers at one — the decision record:
-//   hipcc -O3 -std=c++17 -Icsrc/include -Icsrc/hip --offload-arch=gfx950 \
-//     -ffp-contract=off --cuda-device-only -c tools/micro/kss4_skeleton.hip \
-//     -o /tmp/kss4.o -Rpass-analysis=kernel-resource-usage
+// Registers (profiles/r5_sstep4.txt): the march needs 304-312 registers — at
+// two waves per SIMD (256) it spilled 187-300 to scratch — so kS4 runs ONE
+// wave per SIMD (amdgpu_waves_per_eu(1): 256 VGPRs + ~50 AGPRs, no scratch)
+// and keeps more rows of r / p loads in flight per wave instead (kXD4 = 6:
+// the bytes in flight of two waves of three).  Opt-in (PE_STEPS=4 /
+// --algo four-step) until measured against the three-step sweep.
 #include <cstdlib>
 #include <type_traits>
 
@@ -81,7 +81,11 @@ static_assert(SP<3>::NS == kNS3 && SP<3>::pn(1) == 16 && SP<3>::pp(1) == 11, "S 
 constexpr int FSW4 = kFSW3;
 constexpr int HL4 = kHL3, HR4 = 64 - kFSW3 - kHL3;
 static_assert(HL4 >= SP<4>::H && HR4 >= SP<4>::H, "four-step strip: >= 8 halo lanes per side");
-constexpr int kXD4 = 3, kWD4 = 3;  // rows of r / p (w) loads in flight: divisors of the 6-step unroll
+#ifndef PE_S4_XD
+#define PE_S4_XD 6
+#endif
+constexpr int kXD4 = PE_S4_XD, kWD4 = 3;  // rows of r / p (w) loads in flight: divisors of the 6-step unroll
+static_assert(6 % kXD4 == 0, "the r / p prefetch ring's period divides the 6-step unroll");
 
 // Scalars of a sweep (iterations K+1 .. K+m).
 template <int S>
@@ -777,7 +781,7 @@ __device__ __forceinline__ void walkS(const KParams& k, const CoefS<S>& cf, bool
 // previous launch's late stop tests, its fix-up, breakdown / cap, then this
 // sweep; the replay launch; the overlap's boundary signal).
 template <int S, bool PUSH, int MODE = kPlain4>
-__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kSS(KParams k, int par) {
+__global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(1))) void kSS(KParams k, int par) {
   using P = SP<S>;
   constexpr int NS = P::NS;
   constexpr int RING = P::RING;

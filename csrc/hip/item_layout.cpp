@@ -79,7 +79,7 @@ void DeviceSolver::setup_items() {
   overlap_ = false;
   // (the two-step sweep runs without the overlap; the three-step sweep's
   // boundary items count themselves in its kSignal variant, fused3.hip)
-  if (fused_ && (!sstep_ || steps_ == 3) && comm_->size() > 1 && nb && !push_) {
+  if (fused_ && (!sstep_ || steps_ >= 3) && comm_->size() > 1 && nb && !push_) {
     if (e) {
       overlap_ = std::atoi(e) != 0;
     } else {
@@ -120,7 +120,7 @@ void DeviceSolver::setup_items() {
   double gen_cost = double(blk_.nx) * double(blk_.ny) >= double(1 << 24) ? 3.0 : 2.0;
   // three-step LPT at 2²⁵-2²⁶ nodes (8192², 112-row items): 3.25-4 run ≈1 %
   // faster than 3 on three boxes, 5-8 ≈8 % slower (profiles/r4_ti48.txt)
-  if (steps_ == 3 && double(blk_.nx) * double(blk_.ny) >= double(1 << 25) &&
+  if (steps_ >= 3 && double(blk_.nx) * double(blk_.ny) >= double(1 << 25) &&
       double(blk_.nx) * double(blk_.ny) <= double(1 << 26))
     gen_cost = 3.5;
   if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
@@ -132,7 +132,7 @@ void DeviceSolver::setup_items() {
   // columns?  (The kernel's has_gen on the same row-class table.)
   const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step, 6 three-step)
   const int HL = xorg_ + 1;  // a strip's left halo columns (three-step: 8, for aligned loads and stores)
-  const int64_t Wc = steps_ == 3 ? 64 : 128;  // columns a wave strip loads (three-step: one per lane)
+  const int64_t Wc = steps_ >= 3 ? 64 : 128;  // columns a wave strip loads (three-/four-step: one per lane)
   auto row_gen_x = [&](int64_t q, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;  // table index of local row q
@@ -201,7 +201,7 @@ void DeviceSolver::setup_items() {
     // past ny hold that neighbour's columns, which only the lane-tested
     // march keeps out of the sums)
     const bool cut = (blk_.has(UP) && int64_t(s + 1) * fsw_ > blk_.ny);
-    if (flag == 0 && steps_ == 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
+    if (flag == 0 && steps_ >= 3 && !cut && rows_uniform(ib, ib + rows - 1, s)) flag = dev::kUniBit;
     return int2{int(ib) | flag, s | int(rows << 20)};
   };
   // outputs a neighbour needs: first in the layout under the overlap (they
@@ -341,7 +341,7 @@ void DeviceSolver::setup_items() {
     std::string lay = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : lay_name_;
     // (the overlap's short boundary pieces: the filling layout, below)
     if (overlap_ && !std::getenv("PE_LAYOUT")) lay = "fill";
-    const bool s3lay = steps_ == 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
+    const bool s3lay = steps_ >= 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
     if (!s3lay) lay = "lpt";
     const bool equal = s3lay && lay == "equal";
     const bool fill = s3lay && lay == "fill";
@@ -645,7 +645,7 @@ void DeviceSolver::setup_items() {
     // the sweep ended with band items of the last rows (6945-7169) starting
     // 607-631 µs into a 722 µs span: a 33-40 µs tail.  Costed by kind they
     // are laid out first.  PE_LPT_KIND=0: the band-row weights.
-    if (steps_ == 3 && !(std::getenv("PE_LPT_KIND") && std::atoi(std::getenv("PE_LPT_KIND")) == 0)) {
+    if (steps_ >= 3 && !(std::getenv("PE_LPT_KIND") && std::atoi(std::getenv("PE_LPT_KIND")) == 0)) {
       for (Piece& p : pcs) {
         const int2 e = entry(p.ib, p.rows, p.s);
         const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;

@@ -339,6 +339,13 @@ int resident_blocks_S2();
 // launch_S dispatches here when k.steps == 3.
 void launch_S3(const KParams& k, int par, hipStream_t s);
 int resident_blocks_S3();
+// Four-step sweep (fused4.hip): the same protocol for iterations K+1..K+4
+// (8-deep halo, 26 sums; state layout sc3 = {zc[4], α[4], β[4], g[4]});
+// launch_S dispatches here when k.steps == 4.
+void launch_S4(const KParams& k, int par, hipStream_t s);
+int resident_blocks_S4();
+constexpr int kNS4 = 26;         // four-step sweep: sums per sweep
+constexpr int sweep_sums(int steps) { return steps >= 3 ? 7 * steps - 2 : steps == 2 ? kNS2 : 7; }
 // (k.ti / k.order select the kernel variant: set them first)
 int resident_blocks_classic(int variant);
 

@@ -201,7 +201,7 @@ bool DeviceSolver::placement_search(bool retry) {
   // with the aligned strips and 112-row items its classes are 0.709-0.722,
   // 0.74, 0.78-0.79 and 0.83-0.85 ms, the first fast one usually the 5th try —
   // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates)
-  double fast_tbs = steps_ == 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
+  double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
   if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return true;

@@ -88,7 +88,7 @@ class SolveReport:
         return d
 
 
-ALGOS = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4}
+ALGOS = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4, "four-step": 5}
 
 
 def _options(init="zero", seed=1234, threads=1, chunk=0, graph=False, timing=False, check_tol=True, variant=0,

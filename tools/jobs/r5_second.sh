@@ -26,4 +26,14 @@ python3 -c "
 import json
 for n in ('bench1','benchk1','bench2','benchk2','bench3','benchk3'):
     d=json.loads(open('$O/%s.json'%n).read().strip().splitlines()[-1]); print(n, d['value'], d['ms_per_step'], d.get('iters_converged'), d.get('t_iterate_s'), d.get('t_check_s'))"
+# four-step sweep (opt-in): tests, bench, slab / 8192^2 probes
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_four_step.py > $O/tests4.txt 2>&1; rc=$?
+tail -5 $O/tests4.txt; echo "tests4 rc $rc"; [ $rc -eq 0 ] || exit 1
+for i in 1 2; do timeout -k 10 120 python -u bench.py --steps 20 --warmup 5 --algo four-step > $O/bench4_$i.json 2> $O/bench4_$i.err || exit 1; done
+python3 -c "
+import json
+for n in ('bench4_1','bench4_2'):
+    d=json.loads(open('$O/%s.json'%n).read().strip().splitlines()[-1]); print(n, d['value'], d['ms_per_step'], d.get('iters_converged'), d.get('t_iterate_s'), d['config'].get('algo'))"
+PE_STEPS=4 PROBE_CFG=8:device,1:device timeout -k 10 240 python -u tools/stamp_probe.py > $O/stamps4.txt 2>&1 || { tail -20 $O/stamps4.txt; exit 1; }
+grep -h "us/iter" $O/stamps4.txt
 echo EXIT 0
