@@ -34,6 +34,6 @@ python3 -c "
 import json
 for n in ('bench4_1','bench4_2'):
     d=json.loads(open('$O/%s.json'%n).read().strip().splitlines()[-1]); print(n, d['value'], d['ms_per_step'], d.get('iters_converged'), d.get('t_iterate_s'), d['config'].get('algo'))"
-PE_STEPS=4 PROBE_CFG=8:device,1:device timeout -k 10 240 python -u tools/stamp_probe.py > $O/stamps4.txt 2>&1 || { tail -20 $O/stamps4.txt; exit 1; }
+PE_STEPS=4 PROBE_HALO=8 PROBE_CFG=8:device,1:device timeout -k 10 240 python -u tools/stamp_probe.py > $O/stamps4.txt 2>&1 || { tail -20 $O/stamps4.txt; exit 1; }
 grep -h "us/iter" $O/stamps4.txt
 echo EXIT 0
