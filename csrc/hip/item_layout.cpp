@@ -351,6 +351,24 @@ void DeviceSolver::setup_items() {
     std::vector<double> load;
     int nbnd = 0;
     double fband = 2.45, fmixed = 1.3;  // row-step cost of a band / mixed item, uniform = 1 (profiles/r4_stamps*.txt)
+    // Tie-break among equally loaded waves: one wave per workgroup in turn
+    // (wave slot 0 of workgroups 0, 1, 2, …, then slot 1, …), so the pieces
+    // dealt first — the heaviest, band pieces — land on different CUs.  In
+    // wave order they stacked on the waves of a few CUs: the three-step LPT
+    // costed by kind put 8192²'s 505 band items on waves 0..504 (63 CUs, 8
+    // band waves each, two per SIMD) and each ran 456 µs instead of 222
+    // (profiles/r5_stamps_concentrated.txt).  Workgroups are dealt round-robin
+    // over the XCDs, so consecutive ones are on different CUs.
+    // PE_SPREAD=0: ties in wave order (the round-4 layouts).
+    const bool spread = !(std::getenv("PE_SPREAD") && std::atoi(std::getenv("PE_SPREAD")) == 0);
+    auto wfrom = [&](int r, int Wn) {  // the wave of tie-break rank r
+      const int nbw = std::max(1, Wn / dev::kWPB);
+      return spread ? (r % nbw) * dev::kWPB + r / nbw : r;
+    };
+    auto wrank = [&](int w, int Wn) {
+      const int nbw = std::max(1, Wn / dev::kWPB);
+      return spread ? (w % dev::kWPB) * nbw + w / dev::kWPB : w;
+    };
     if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
     if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
     if (equal) {
@@ -503,7 +521,7 @@ void DeviceSolver::setup_items() {
         }
         if (!odd.empty()) {
           std::stable_sort(odd.begin(), odd.end(), [&](int x, int y) { return pcs[size_t(x)].cost > pcs[size_t(y)].cost; });
-          for (int w = 0; w < W; ++w) byload[size_t(w)] = w;
+          for (int r = 0; r < W; ++r) byload[size_t(r)] = wfrom(r, W);
           std::stable_sort(byload.begin(), byload.end(), [&](int x, int y) { return wl[size_t(x)] < wl[size_t(y)]; });
           size_t q = 0;
           for (size_t j = 0; j < odd.size(); ++j) {
@@ -601,12 +619,13 @@ void DeviceSolver::setup_items() {
         }
         using LW = std::pair<double, int>;
         std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
-        for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
+        for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], wrank(w, W)});
         while (!q.empty()) {
           QE e = q.top();
           q.pop();
           const LW t = heap.top();
           heap.pop();
+          const int tw = wfrom(t.second, W);
           const double room = T - t.first;
           Piece give = e.p;
           if (e.p.cost > room && room >= minc && e.p.rows >= 2 * minr) {
@@ -628,7 +647,7 @@ void DeviceSolver::setup_items() {
               ++ncut;
             }
           }
-          per[size_t(t.second)].push_back(int(pcs.size()));
+          per[size_t(tw)].push_back(int(pcs.size()));
           pcs.push_back(give);
           heap.push(LW{t.first + give.cost, t.second});
         }
@@ -668,11 +687,11 @@ void DeviceSolver::setup_items() {
                      [&](int a, int b) { return pcs[size_t(a)].cost > pcs[size_t(b)].cost; });
     using LW = std::pair<double, int>;
     std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
-    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], w});
+    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], wrank(w, W)});
     for (int i : order) {
       const LW t = heap.top();
       heap.pop();
-      per[size_t(t.second)].push_back(i);
+      per[size_t(wfrom(t.second, W))].push_back(i);
       heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
     }
     lay_cuts_ = 0;
