@@ -280,6 +280,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.fused = fused_ ? 1 : 0;
   k.steps = steps_;
   k.hdep = hdep_;
+  k.pre_load = !(std::getenv("PE_PRE") && std::atoi(std::getenv("PE_PRE")) == 0);
+  k.dring = !(std::getenv("PE_DRING") && std::atoi(std::getenv("PE_DRING")) == 0);
   k.xorg = xorg_;
   k.nx = nx;
   k.ny = ny;

@@ -335,6 +335,18 @@ struct M3Rings {
   bool pushed;
 };
 
+// A wave's first item as loaded at kernel entry: its list entry and the
+// row-class entry of its first row window — the two dependent loads in front
+// of its first row loads.  Neither depends on the sweep's scalars, so their
+// latency overlaps the state reads and the scalar algebra instead of
+// following them (kernel entry to the first item's first row step: 5.4-6.9
+// µs, tools/stamp_probe.py, profiles/r5_stamps_concentrated.txt).  (Its first
+// r / p / w rows too: live across the walk loop they spilled 5-11 VGPRs.)
+struct Pre3 {
+  int2 e;  // (rows field 0: no item)
+  int4 rc4;
+};
+
 template <bool STEADY>
 __device__ __forceinline__ URow urow(const M3Ctx& c, const RowCtx& rx, int q) {
   const int l = (q - rx.segbase) & 63;
@@ -608,7 +620,8 @@ __device__ __forceinline__ unsigned long long rtc3() {
 // prologue and every 6-step group into the wave's step stamps)
 template <int KIND, bool PUSH, bool EDGE, bool SST = false>
 __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool fix, int par, int s, int ib, int ie,
-                                       WaveTV3& tvw, double (&sv)[NS], unsigned long long* sst = nullptr) {
+                                       WaveTV3& tvw, double (&sv)[NS], unsigned long long* sst, const Pre3& pre,
+                                       bool use_pre) {
   const int lane = threadIdx.x & 63;
   const int ny = int(k.ny);
   M3Ctx c;
@@ -660,7 +673,8 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   RowCtx rx;
   auto load_seg = [&](int base) { load_rows<KIND == kBand, WaveTV3, 64>(k, rx, tvw, base, ie + H3 + 1, c.J); };
   if (KIND == kBand) load_strip_tables1(k, tvw, c.c0);
-  load_seg(c.t0);
+  if (use_pre) load_rows<KIND == kBand, WaveTV3, 64>(k, rx, tvw, c.t0, ie + H3 + 1, c.J, &pre.rc4);
+  else load_seg(c.t0);
 
   M3Rings x;
   x.pushed = false;
@@ -727,6 +741,18 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   }
 }
 
+// The first list position of wave gwave and that item's first loads (Pre3).
+__device__ __forceinline__ void pre_load3(const KParams& k, int gwave, Pre3& pr) {
+  pr.e = make_int2(0, 0);
+  if (!(gwave < k.lwaves && gwave < k.nslots)) return;
+  pr.e = cload_i2(k.ilist + gwave);
+  const int rows = pr.e.y >> 20;
+  if (rows == 0) return;
+  const int ib = pr.e.x & kRowMask3;
+  const int ie = min(ib + rows - 1, int(k.nx));
+  pr.rc4 = rowcls_entry(k, ib - H3, ie + H3 + 1);
+}
+
 __device__ __forceinline__ Coef3 uni3(const Coef3& c) {
   Coef3 u;
 #pragma unroll
@@ -755,7 +781,7 @@ enum { kPlain = 0, kStamp = 1, kReplay = 2, kSignal = 3 };
 
 template <bool PUSH, int MODE>
 __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fix, int par, WaveTV3& tv, int wid,
-                                      double (&acc)[NS]) {
+                                      double (&acc)[NS], const Pre3& pre, bool have_pre) {
   constexpr bool STAMP = MODE == kStamp;
   const int W = k.lwaves;
   const int gwave = int(blockIdx.x) * kWPB + wid;
@@ -768,10 +794,14 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   // have no list positions; they used to march round r+1's first items twice)
   const int pend = gwave < W ? k.nslots : 0;
   unsigned long long* sst = STAMP ? k.stamps2 + 32 * int64_t(gwave) : nullptr;  // (the first item only)
+  bool p1 = have_pre && !fix;  // (a fix-up marches other inputs than the ones loaded at entry)
   for (int pos = gwave; pos < pend; pos += W) {
-    const int2 e = cload_i2(k.ilist + pos);
+    const int2 e = p1 ? pre.e : cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
-    if (rows == 0) continue;  // empty position of the static layout
+    if (rows == 0) {  // empty position of the static layout
+      p1 = false;
+      continue;
+    }
     const int s = e.y & 0xFFFFF, ib = e.x & kRowMask3;
     const int ie = min(ib + rows - 1, int(k.nx));
     const unsigned long long t_item = STAMP ? rtc3() : 0ull;
@@ -779,17 +809,18 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
       if (sst && l0) sst[0] = t_item;
     }
     if (e.x & kBandBit) {
-      march3<kBand, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
+      march3<kBand, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst, pre, p1);
     } else if (e.x & kUniBit) {
       // edge strips (a global-boundary or padding column in the window) mask z
       const int c0 = -(HL3 - 1) + s * FSW3 + int(threadIdx.x & 63);
       const int64_t g0 = k.gj0 + c0;
       const bool lv = c0 <= int(k.ny) + H3 && g0 >= 1 && g0 <= k.N - 1;
-      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
-      else march3<kUniform, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
+      if (__ballot(lv) == ~0ull) march3<kUniform, PUSH, false, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst, pre, p1);
+      else march3<kUniform, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst, pre, p1);
     } else {
-      march3<kMixed, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst);
+      march3<kMixed, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst, pre, p1);
     }
+    p1 = false;
     if constexpr (STAMP) {
       if (sst && l0) sst[31] = rtc3();
       sst = nullptr;
@@ -834,6 +865,10 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     }
   }
   if (done && !replay) return;
+  // the first item's loads, before the state reads (PE_PRE=0 at construction: off)
+  Pre3 pre;
+  const bool use_pre = !replay && k.pre_load;
+  if (use_pre) pre_load3(k, int(blockIdx.x) * kWPB + wid, pre);
   auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
                             // the slots garbage pipeline-fill rows read stay finite)
     WaveTV3& tv = tvs[wid];
@@ -921,7 +956,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     cf = sc.c;
   }
   zero_ring();
-  walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc);
+  walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc, pre, use_pre);
   if (replay) return;
   if (fix) {
     finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);

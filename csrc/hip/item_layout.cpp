@@ -339,8 +339,14 @@ void DeviceSolver::setup_items() {
     // three-step layouts: PE_LAYOUT forces one; else the construction's
     // choice (lay_name_: by block size, or by the rows-per-item tuning)
     std::string lay = std::getenv("PE_LAYOUT") ? std::getenv("PE_LAYOUT") : lay_name_;
-    // (the overlap's short boundary pieces: the filling layout, below)
-    if (overlap_ && !std::getenv("PE_LAYOUT")) lay = "fill";
+    // (the overlap's short boundary pieces: the filling layout, below — on
+    // blocks of about one item per wave, where whole boundary items end with
+    // the sweep: 4×2 block of 8192² 59.3 µs per iteration at 15 / 8 µs delays
+    // vs 57.5 without delays or overlap.  Larger blocks keep their layout with
+    // whole boundary items first, which already runs them in the first of
+    // several rounds; the filling layout cost the 2×2 block 18 % there —
+    // 108 vs 90.9 µs at zero delay, profiles/r5_overlap.txt)
+    if (overlap_ && !std::getenv("PE_LAYOUT") && double(blk_.nx) * double(blk_.ny) < 1.2e7) lay = "fill";
     const bool s3lay = steps_ >= 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
     if (!s3lay) lay = "lpt";
     const bool equal = s3lay && lay == "equal";

@@ -204,6 +204,10 @@ struct KParams {
   // three-step sweep: > 0 → this launch applies at most mlimit iterations (a
   // run of n iterations ends with a partial sweep when 3 ∤ n)
   int mlimit;
+  // three-step sweep: load each wave's first item at kernel entry (fused3.hip Pre3)
+  int pre_load;
+  // band items: 1/D from the LDS ring (1) or re-formed from the faces (0, PE_DRING=0)
+  int dring;
 };
 constexpr int kFoldGroup = 64;
 // KParams::mlimit of the three-step replay launch (DevState::fixj)

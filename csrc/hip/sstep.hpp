@@ -98,12 +98,20 @@ __device__ __forceinline__ double lap(const KParams& k, double f, double pm, dou
 // Row classes / column tables of rows base .. base+63 (one per lane) into the
 // lane registers (strip window: WIN columns from J) (and, for band items with a boundary row in the window, the
 // wave's LDS tables); rows past `last` get an empty interior interval.
+// The row-class entry of window row `lane` (rows past `last`: an empty interior).
+__device__ __forceinline__ int4 rowcls_entry(const KParams& k, int base, int last) {
+  const int lane = threadIdx.x & 63;
+  return lane < last + 1 - base ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+}
+
+// (pre: the entry already loaded — fused3.hip loads the first item's at kernel entry)
 template <bool BAND, class WT, int WIN = 128>
-__device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw, int base, int last, int J) {
+__device__ __forceinline__ void load_rows(const KParams& k, RowCtx& rx, WT& tvw, int base, int last, int J,
+                                          const int4* pre = nullptr) {
   const int lane = threadIdx.x & 63;
   rx.segbase = base;
   const int nr = last + 1 - base;
-  const int4 rc4 = lane < nr ? *reinterpret_cast<const int4*>(k.rowcls + (base + 1 + lane) * 4) : make_int4(1, 0, 0, -1);
+  const int4 rc4 = pre ? *pre : rowcls_entry(k, base, last);
   rx.rcv = make_int2(rc4.x, rc4.y);
   rx.genmask = 0;
   rx.allin = __ballot(lane < nr && rc4.x <= J && rc4.y >= J + WIN - 1);
@@ -278,7 +286,7 @@ __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx,
   if (BAND && gen) {
     const double a0 = tv.a0r[sl][lane], a1 = tv.a0r[sln][lane];
     const double b0 = tv.b0r[sl][lane], b1 = tv.b0r[sl][lane + 1];
-    const CS x0{a0, a1, b0, b1, tv.d0r[sl][lane]};
+    const CS x0{a0, a1, b0, b1, k.dring ? tv.d0r[sl][lane] : dinv_faces(k, a0, a1, b0, b1)};
     d = x0.d;
     return stencil<false>(k, x0, um, u0, un, ul, ur);
   }
