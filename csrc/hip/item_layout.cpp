@@ -662,20 +662,28 @@ void DeviceSolver::setup_items() {
       }
       lay_cuts_ = cuts;
     } else {
-    // Three-step LPT: cost an item by its march KIND — a band item runs every
-    // row step on the band path (≈2.25× a uniform one at 8192²: 221.8 vs
-    // 98.6 µs per 112-row item, profiles/r4_stamps48.txt), not only its band
-    // rows.  Weighted by band rows alone, a band item looked barely heavier
-    // than a uniform one, the LPT order left it among a wave's last items, and
-    // the sweep ended with band items of the last rows (6945-7169) starting
-    // 607-631 µs into a 722 µs span: a 33-40 µs tail.  Costed by kind they
-    // are laid out first.  PE_LPT_KIND=0: the band-row weights.
-    if (steps_ >= 3 && !(std::getenv("PE_LPT_KIND") && std::atoi(std::getenv("PE_LPT_KIND")) == 0)) {
-      for (Piece& p : pcs) {
-        const int2 e = entry(p.ib, p.rows, p.s);
-        const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
-        p.cost = double(p.rows + 2 * H) * f + overhead;
-      }
+    // Three-/four-step LPT.  A band item runs EVERY row step on the band path
+    // (≈2.25× a uniform one at 8192²: 221.8 vs 98.6 µs per 112-row item,
+    // profiles/r4_stamps48.txt), but costed by its band rows alone it looks
+    // barely heavier than a uniform one, so waves that take one still get as
+    // many items as the rest: the sweep ended with band items of the last rows
+    // (6945-7169) starting 607-631 µs into a 722 µs span (a 33-40 µs tail).
+    // PE_LPT_KIND=1 (default): the items are still dealt in the band-row
+    // order (≈ chunk-major: each round of positions covers a compact window of
+    // rows) but every wave's LOAD counts an item by its kind (rows + 2H fill
+    // steps × the kind's factor), so a wave that took a band item takes fewer
+    // items after it.  PE_LPT_KIND=2: also ORDER by kind cost — every band
+    // item in the first round, all over the grid: 10 % slower at 8192² (the
+    // first round lost its row window; band items ran 4.1 µs per row step
+    // instead of 1.8, profiles/r5_ab_layout.txt).  0: band-row costs only.
+    const int lpt_kind = std::getenv("PE_LPT_KIND") ? std::atoi(std::getenv("PE_LPT_KIND")) : 1;
+    std::vector<double> kcost(pcs.size());
+    for (size_t i = 0; i < pcs.size(); ++i) {
+      Piece& p = pcs[i];
+      const int2 e = entry(p.ib, p.rows, p.s);
+      const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
+      kcost[i] = steps_ >= 3 && lpt_kind > 0 ? double(p.rows + 2 * H) * f + overhead : p.cost;
+      if (steps_ >= 3 && lpt_kind == 2) p.cost = kcost[i];
     }
     per.assign(size_t(W), {});
     load.assign(size_t(W), 0.0);
@@ -683,7 +691,7 @@ void DeviceSolver::setup_items() {
     for (int i = 0; i < int(pcs.size()); ++i) {
       if (pcs[size_t(i)].bnd) {  // boundary pieces: positions 0, 1, … in order
         per[size_t(nbnd % W)].push_back(i);
-        load[size_t(nbnd % W)] += pcs[size_t(i)].cost;
+        load[size_t(nbnd % W)] += kcost[size_t(i)];
         ++nbnd;
       } else {
         order.push_back(i);
@@ -698,7 +706,7 @@ void DeviceSolver::setup_items() {
       const LW t = heap.top();
       heap.pop();
       per[size_t(wfrom(t.second, W))].push_back(i);
-      heap.push(LW{t.first + pcs[size_t(i)].cost, t.second});
+      heap.push(LW{t.first + kcost[size_t(i)], t.second});
     }
     lay_cuts_ = 0;
     }
