@@ -455,11 +455,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // layout's sweep lasts as long as its most loaded wave, and 3.4 items per
   // wave means a quarter of the waves runs a 4th item while the rest idle
   // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78,
-  // tools/stamp_probe.py).  Three-step: down to 4 rows (q = 1) — a block with
-  // fewer strip-rows than ~32 per wave is latency-bound, and one short item
-  // per wave beats 32+-row items on a fraction of the waves despite its 12
-  // pipeline-fill rows (2-rank 1600×2400 block at 80 rows: 21 µs per
-  // iteration, profiles/r5_block_probe_base.txt).
+  // tools/stamp_probe.py).  (Round 5 measured one short item per wave — down
+  // to 4 rows — on the 2-rank blocks of 1600×2400 and 2048²: 86.9-88.2 µs per
+  // sweep against 58.9-64 at 32-96 rows; the 12 pipeline-fill rows of a short
+  // item cost more than the waves it adds — profiles/r5_ab_layout.txt.)
   std::vector<int> ti_cands;
   if (tune_ti_) {
     ti_cands.assign(kTiCands, kTiCands + 4);
@@ -468,8 +467,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // at 18, one placement, profiles/r2_ti_big.txt)
     if (npts >= 12e6 && !sstep_) ti_cands.insert(ti_cands.end(), {24, 30});
     const int64_t W = std::max(dev::kWPB, wave_cap_);
-    const int tlo = steps_ >= 3 ? 4 : sstep_ ? tic[0] : kTiCands[0], thi = steps_ >= 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
-    for (int q = steps_ >= 3 ? 1 : 2; q <= 5; ++q)
+    const int tlo = sstep_ ? tic[0] : kTiCands[0], thi = steps_ >= 3 ? 128 : sstep_ ? dev::kTImax2 : 40;
+    for (int q = 2; q <= 5; ++q)
       for (int t = tlo; t <= thi; ++t)
         if (int64_t(strips) * ((nx + t - 1) / t) <= int64_t(q) * W) {
           ti_cands.push_back(t);

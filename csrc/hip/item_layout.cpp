@@ -365,8 +365,10 @@ void DeviceSolver::setup_items() {
     // band waves each, two per SIMD) and each ran 456 µs instead of 222
     // (profiles/r5_stamps_concentrated.txt).  Workgroups are dealt round-robin
     // over the XCDs, so consecutive ones are on different CUs.
-    // PE_SPREAD=0: ties in wave order (the round-4 layouts).
-    const bool spread = !(std::getenv("PE_SPREAD") && std::atoi(std::getenv("PE_SPREAD")) == 0);
+    // PE_SPREAD=1 (opt-in); default: ties in wave order (the round-4 layouts).
+    // (PE_SPREAD=1 measured neutral to 1 % slower on the 8192² splits and the
+    // round-4 layouts it was made for are the defaults again: off by default)
+    const bool spread = std::getenv("PE_SPREAD") && std::atoi(std::getenv("PE_SPREAD")) == 1;
     auto wfrom = [&](int r, int Wn) {  // the wave of tie-break rank r
       const int nbw = std::max(1, Wn / dev::kWPB);
       return spread ? (r % nbw) * dev::kWPB + r / nbw : r;
@@ -668,15 +670,19 @@ void DeviceSolver::setup_items() {
     // barely heavier than a uniform one, so waves that take one still get as
     // many items as the rest: the sweep ended with band items of the last rows
     // (6945-7169) starting 607-631 µs into a 722 µs span (a 33-40 µs tail).
-    // PE_LPT_KIND=1 (default): the items are still dealt in the band-row
-    // order (≈ chunk-major: each round of positions covers a compact window of
-    // rows) but every wave's LOAD counts an item by its kind (rows + 2H fill
-    // steps × the kind's factor), so a wave that took a band item takes fewer
-    // items after it.  PE_LPT_KIND=2: also ORDER by kind cost — every band
-    // item in the first round, all over the grid: 10 % slower at 8192² (the
-    // first round lost its row window; band items ran 4.1 µs per row step
-    // instead of 1.8, profiles/r5_ab_layout.txt).  0: band-row costs only.
-    const int lpt_kind = std::getenv("PE_LPT_KIND") ? std::atoi(std::getenv("PE_LPT_KIND")) : 1;
+    // Both ways of costing items by kind measured slower, on one box against
+    // the round-4 build (profiles/r5_ab_kernel.txt, profiles/r5_ab_layout.txt):
+    // PE_LPT_KIND=1 — dealt in the band-row order (≈ chunk-major) but every
+    // wave's LOAD counts an item by its kind (rows + 2H fill steps × the kind's
+    // factor): 3632-3644 vs 3985-4005 it/s (the last rows' items then went to
+    // whichever waves were least loaded, a 110-123 µs tail); PE_LPT_KIND=2 —
+    // also ORDERED by kind cost: every band item in the first round, all over
+    // the grid, 3519-3606 (the first round lost its row window; band items ran
+    // 4.1 µs per row step instead of 1.8).  The round-4 tail (late items of the
+    // last rows) is made of UNIFORM items whose waves ran slow — the wave-time
+    // spread the static costs do not predict (r4 stamps: correlation -0.1).
+    // Default 0: band-row costs only.
+    const int lpt_kind = std::getenv("PE_LPT_KIND") ? std::atoi(std::getenv("PE_LPT_KIND")) : 0;
     std::vector<double> kcost(pcs.size());
     for (size_t i = 0; i < pcs.size(); ++i) {
       Piece& p = pcs[i];

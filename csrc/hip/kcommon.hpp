@@ -235,11 +235,26 @@ __device__ __forceinline__ bool publish_last(double* dst, const double (&v)[N], 
 }
 
 // Sum N-tuples of partials [nblocks][N] in block order (deterministic).
+// Two tuples per thread are loaded before either is added (the same sums in
+// the same order): the grid's last block reads 512 tuples written by other
+// XCDs, and one latency per pair instead of per tuple shortens the sweep's
+// epilogue (last wave exit → state finalized: 9-10 µs, tools/stamp_probe.py).
 template <int N>
 __device__ __forceinline__ void reduce_partials(const double* partial, unsigned nblocks, double (&v)[N], double* sm) {
 #pragma unroll
   for (int n = 0; n < N; ++n) v[n] = 0.0;
-  for (unsigned m = threadIdx.x; m < nblocks; m += TJ)
+  unsigned m = threadIdx.x;
+  for (; m + TJ < nblocks; m += 2 * TJ) {
+    double a[N], b[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      a[n] = partial[size_t(m) * N + n];
+      b[n] = partial[size_t(m + TJ) * N + n];
+    }
+#pragma unroll
+    for (int n = 0; n < N; ++n) v[n] = (v[n] + a[n]) + b[n];
+  }
+  if (m < nblocks)
 #pragma unroll
     for (int n = 0; n < N; ++n) v[n] += partial[size_t(m) * N + n];
   block_reduce<N, false>(v, sm);

@@ -119,11 +119,18 @@ class DelayComm final : public DeviceComm {
       : size_(size), ex_us_(exchange_us), ar_us_(allreduce_us), loop_(loopback) {}
   int rank() const override { return 0; }
   int size() const override { return size_; }
-  void allreduce_sum(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
-  void allreduce_max(double*, int, hipStream_t s) override { dev::launch_delay(ar_us_, s); }
+  // (a zero delay launches nothing: one rank's block then runs its sweeps back
+  // to back, as with the in-sweep push and P2P sums — the per-rank block
+  // probes used to pay 2-3 µs of empty delay launches per sweep)
+  void allreduce_sum(double*, int, hipStream_t s) override {
+    if (ar_us_ > 0) dev::launch_delay(ar_us_, s);
+  }
+  void allreduce_max(double*, int, hipStream_t s) override {
+    if (ar_us_ > 0) dev::launch_delay(ar_us_, s);
+  }
   void exchange(const std::vector<Exchange>& ex, hipStream_t s) override {
     if (ex.empty()) return;
-    dev::launch_delay(ex_us_, s);
+    if (ex_us_ > 0) dev::launch_delay(ex_us_, s);
     if (loop_)
       for (const Exchange& e : ex)
         if (e.count > 0 && e.send && e.recv && e.send != e.recv)
