@@ -208,7 +208,10 @@ struct Late3 {
 };
 
 __device__ __forceinline__ double late_diff(const KParams& k, const DevState* st, int i) {
-  const double n2 = fmax(st->fs2[st->wpar][16 + i], 0.0), a = st->sc3[3 + i];
+  // (both parities' ‖p_i‖² loaded and selected: indexing by wpar made the
+  // load wait for wpar's — one more round trip in every launch's prologue)
+  const double s0 = st->fs2[0][16 + i], s1 = st->fs2[1][16 + i];
+  const double n2 = fmax(st->wpar ? s1 : s0, 0.0), a = st->sc3[3 + i];
   const double hh = k.h1 * k.h2;
   return k.weighted ? fabs(a) * sqrt(n2 * hh) : fabs(a) * sqrt(n2);
 }
@@ -795,6 +798,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
   const int pend = gwave < W ? k.nslots : 0;
   unsigned long long* sst = STAMP ? k.stamps2 + 32 * int64_t(gwave) : nullptr;  // (the first item only)
   bool p1 = have_pre && !fix;  // (a fix-up marches other inputs than the ones loaded at entry)
+  bool ring_zeroed = false;
   for (int pos = gwave; pos < pend; pos += W) {
     const int2 e = p1 ? pre.e : cload_i2(k.ilist + pos);
     const int rows = e.y >> 20;
@@ -809,6 +813,16 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
       if (sst && l0) sst[0] = t_item;
     }
     if (e.x & kBandBit) {
+      // the face / 1/D ring: defined contents (the never-written column 64 of
+      // b0 and the slots garbage pipeline-fill rows read stay finite) — before
+      // each band item, not in every wave's launch prologue
+      if (!ring_zeroed) {
+        const int ln = threadIdx.x & 63;
+        for (int i = ln; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
+        for (int i = ln; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
+        for (int i = ln; i < kRing3 * 64; i += 64) (&tv.d0r[0][0])[i] = 0.0;
+        ring_zeroed = true;
+      }
       march3<kBand, PUSH, true, STAMP>(k, cf, fix, par, s, ib, ie, tv, acc, sst, pre, p1);
     } else if (e.x & kUniBit) {
       // edge strips (a global-boundary or padding column in the window) mask z
@@ -869,13 +883,6 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   Pre3 pre;
   const bool use_pre = !replay && k.pre_load;
   if (use_pre) pre_load3(k, int(blockIdx.x) * kWPB + wid, pre);
-  auto zero_ring = [&]() {  // band ring: defined contents (the never-written column 64 of b0 and
-                            // the slots garbage pipeline-fill rows read stay finite)
-    WaveTV3& tv = tvs[wid];
-    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
-    for (int i = lane; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
-    for (int i = lane; i < kRing3 * 64; i += 64) (&tv.d0r[0][0])[i] = 0.0;
-  };
   // terminal paths: every wave has read the state before the last one to
   // arrive writes it
   auto finish = [&](int upto, long long iter, int status, int fixj = 0) {
@@ -955,7 +962,6 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     }
     cf = sc.c;
   }
-  zero_ring();
   walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc, pre, use_pre);
   if (replay) return;
   if (fix) {
