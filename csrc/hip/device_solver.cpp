@@ -438,9 +438,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   static constexpr int kTiCands2[5] = {16, 24, 32, 40, 48};
   static constexpr int kTiCands3[5] = {32, 48, 64, 80, 96};
   const int* tic = steps_ >= 3 ? kTiCands3 : kTiCands2;
-  // (three-step: from 2¹⁷ nodes — the multi-rank blocks of the published
-  // grids, e.g. 399×1199 of 800×1200 on 2 ranks, run the streaming sweep)
-  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(steps_ >= 3 ? 1 << 17 : 1 << 20) && npts < double(1 << 25);
+  // (from 2²⁰ nodes: a tuned layout depends on the timings, so two
+  // constructions of a smaller block — a checkpointed solve and its resume —
+  // could lay it out differently and the resume would not be bitwise; round 5
+  // tuned from 2¹⁷ and test_three_step_checkpoint_resume_bitwise caught it)
+  if (sstep_) tune_ti_ = ti_env == 0 && npts >= double(1 << 20) && npts < double(1 << 25);
   // Three-step static layout by block size, one placement per block
   // (tools/layout_probe.py, profiles/r4_layout2.txt, µs per iteration): the
   // LPT layout of whole items for ≥ 5·10⁷ nodes (8192²: 253 vs 260 filling,

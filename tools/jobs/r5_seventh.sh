@@ -13,4 +13,6 @@ for cb in 2.45 2.8 3.1 3.4; do
 done
 done
 for f in $O/p*.txt; do echo "$(basename $f .txt): $(grep -h 'us/iter' $f | sed 's/tuning.*//' | awk '{print $2, $5, $8}' | tr '\n' ' ')"; done
+timeout -k 10 900 python -u -m pytest -x -q --timeout 300 --timeout-method thread -m gpu tests/test_three_step.py tests/test_layout.py tests/test_residual.py tests/test_four_step.py tests/test_gpu.py::test_overlap_async_loopback_transport_bitwise > $O/tests.txt 2>&1; rc=$?
+tail -3 $O/tests.txt; echo "tests rc $rc"; [ $rc -eq 0 ] || exit 1
 echo EXIT 0
