@@ -356,7 +356,15 @@ void DeviceSolver::setup_items() {
     std::vector<std::vector<int>> per;
     std::vector<double> load;
     int nbnd = 0;
-    double fband = 2.45, fmixed = 1.3;  // row-step cost of a band / mixed item, uniform = 1 (profiles/r4_stamps*.txt)
+    // row-step cost of a band / mixed item, uniform = 1 (profiles/r4_stamps*.txt).
+    // Band 2.8 since round 5 (the equal-cost / filling layouts of mid-size
+    // blocks; one box, two constructions each, µs per iteration at 2.45 / 2.8
+    // / 3.1 / 3.4: 8-rank slab of 8192² 43.0 / 40.4-40.8 / 40.4 / 40.0-40.6,
+    // its 4×2 block 48.0 / 45.3-45.5 / 46.2-46.5 / 44.0-44.3, 4-rank ≈74
+    // throughout, 2048² 28.1-28.7 / 28.4-28.5 / 29.3 / 30.5-30.7 —
+    // profiles/r5_costband.txt; the slab's band row step runs ≈3.0× a uniform
+    // one, 8192²'s 2.25×)
+    double fband = 2.8, fmixed = 1.3;
     // Tie-break among equally loaded waves: one wave per workgroup in turn
     // (wave slot 0 of workgroups 0, 1, 2, …, then slot 1, …), so the pieces
     // dealt first — the heaviest, band pieces — land on different CUs.  In
