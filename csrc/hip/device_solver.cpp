@@ -367,6 +367,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     PE_HIP_CHECK(hipGetDevice(&dev));
     PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
+  cus_ = cus;
   // rows per item and item order first: they select the sweep kernel variant
   // whose occupancy sizes the grid
   const double npts = double(nx) * double(ny);

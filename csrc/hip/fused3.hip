@@ -266,14 +266,49 @@ __device__ __forceinline__ void sweep3_stop(const KParams& k, DevState* st, int 
   st->wpend = 0;
 }
 
+// The pending iterations' records as late3_record writes them, from values
+// a wave of every workgroup read at kernel entry (struct Pend3, LDS): the
+// finalize after the grid reduction then reloads nothing from the state (one
+// L2-missing round trip, ≈1 µs of every sweep's epilogue).
+struct Pend3 {
+  double d[3], a[3], b[3], g[3];
+  long long K0;
+  int n;
+};
+__device__ __forceinline__ void pend3_load(const KParams& k, const DevState* st, int m0, long long K0, Pend3& p) {
+  p.K0 = K0;
+  p.n = m0;
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < m0) {
+      p.d[i] = late_diff(k, st, i);
+      p.a[i] = st->sc3[3 + i];
+      p.b[i] = st->sc3[6 + i];
+      p.g[i] = st->sc3[9 + i];
+    }
+}
+__device__ __forceinline__ void pend3_record(const KParams& k, DevState* st, const Pend3& p) {
+#pragma unroll
+  for (int i = 0; i < 3; ++i)
+    if (i < p.n) {
+      hist_put(k, p.K0 + i + 1, p.d[i]);
+      if (i + 1 == p.n) {
+        st->last_diff = p.d[i];
+        st->alpha = p.a[i];
+        st->beta = p.b[i];
+        st->rz_cur = p.g[i];
+      }
+    }
+}
+
 // State update after a full sweep (one thread; sums t[] global or, with the
 // comm's allreduce after the sweep, this rank's): the previous sweep's
 // pending records (its stop tests passed at this launch's entry), then this
 // sweep's sums, coefficients and tentative iteration count; its own stop
 // tests are pending until the next launch.
 __device__ __forceinline__ void sweep3_finalize(const KParams& k, DevState* st, int par, const Scal3& c,
-                                                const double (&t)[NS]) {
-  if (!c.first) late3_record(k, st, st->late3);
+                                                const double (&t)[NS], const Pend3& pend) {
+  if (!c.first) pend3_record(k, st, pend);
 #pragma unroll
   for (int n = 0; n < NS; ++n) st->fs2[par][n] = t[n];
   // fault hooks (PE_FAULT_INJECT): the sums of the sweep completing iteration F
@@ -705,7 +740,7 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   }
   auto sstamp = [&]() {
     if constexpr (SST) {
-      if (sst && lane == 0 && sg < 31) sst[sg] = rtc3();
+      if (sst && lane == 0 && sg < 30) sst[sg] = rtc3();  // (slot 30: the wave's hardware id)
       ++sg;
     }
   };
@@ -868,6 +903,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   __shared__ double sm[4 * NS];
   __shared__ int sflag;
   __shared__ WaveTV3 tvs[kWPB];
+  __shared__ Pend3 pend;
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   constexpr bool replay = MODE == kReplay;
@@ -875,6 +911,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     const unsigned long long t_in = rtc3();
     if (lane == 0) {
       k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + 1] = t_in;
+      // where the wave runs: HW_ID (wave slot, SIMD, CU, SE) | XCC_ID << 32
+      const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11)), xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
+      k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + 30] = hw | (static_cast<unsigned long long>(xcc) << 32);
       if (blockIdx.x == 0 && wid == 0) k.stamps2[-8] = k.stamps2[-6];
     }
   }
@@ -898,6 +937,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   const int m0 = st->late3;
   const long long K = st->iter, K0 = K - m0;
   const Late3 lt = late3_test(k, st);
+  if (!replay && threadIdx.x == 0) pend3_load(k, st, m0, K0, pend);
   Coef3 cf;
   Scal3 sc = {};
   bool fix = false;
@@ -971,13 +1011,20 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   if (lane < HL3 || lane >= 64 - HR3)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
 #pragma unroll
     for (int n = 0; n < NS; ++n) acc[n] = 0.0;
-  block_reduce<NS, false>(acc, sm);
-  if (publish_last<NS>(k.partial + NS * size_t(blockIdx.x), acc, &st->ticket[0], gridDim.x, &sflag)) {
+  const unsigned long long t_red = MODE == kStamp ? rtc3() : 0ull;
+  if (publish_last_nm<NS>(k.partial, acc, &st->ticket[0], &sflag, sm)) {
     if constexpr (MODE == kStamp) {
-      if (threadIdx.x == 0) k.stamps2[-7] = rtc3();  // the last block starts the grid's reduction
+      if (threadIdx.x == 0) {
+        k.stamps2[-7] = rtc3();  // the last block starts the grid's reduction
+        k.stamps2[-3] = t_red;   // … its block reduction began
+        k.stamps2[-2] = t_red;
+      }
     }
     double t[NS];
-    reduce_partials<NS>(k.partial, gridDim.x, t, sm);
+    reduce_partials_nm<NS>(k.partial, t, sm);
+    if constexpr (MODE == kStamp) {
+      if (threadIdx.x == 0) k.stamps2[-5] = rtc3();  // the 512 partials summed
+    }
     __shared__ double xv[NS + 1];
     __shared__ unsigned long long sseq;
     __shared__ int sok;
@@ -996,7 +1043,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
         for (int n = 0; n < NS; ++n) t[n] = xv[n];
     }
     if (threadIdx.x == 0) {
-      sweep3_finalize(k, st, par, sc, t);
+      if constexpr (MODE == kStamp) k.stamps2[-4] = rtc3();  // (after the cross-rank sum, if any)
+      sweep3_finalize(k, st, par, sc, t, pend);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (MODE == kStamp) k.stamps2[-6] = rtc3();  // finalized
     }

@@ -385,6 +385,25 @@ void DeviceSolver::setup_items() {
       const int nbw = std::max(1, Wn / dev::kWPB);
       return spread ? (w % dev::kWPB) * nbw + w / dev::kWPB : w;
     };
+    // Wave capacity: workgroup b < cus_ is the first one dispatched to its CU,
+    // b ≥ cus_ the second; the SIMDs' age-ordered issue runs the first
+    // workgroup's waves ≈12 % faster per row step at the 8-rank slab of
+    // 8192² and 2048² (0.86 vs 0.97 µs), ≈23 % at 8192² (0.77 vs 0.95) — and
+    // the slow half follows the workgroup, not the rows it marches: with the
+    // lists on the workgroups in reverse order the rows' speeds reverse and
+    // the workgroups' stay (PE_WPERM, tools/stamp_probe.py,
+    // profiles/r5_wave_age.txt).  The fill and LPT layouts can give the first
+    // workgroups' waves rho times the load of the others (PE_YOUNG = rho).
+    // Measured NEUTRAL on the mid-size blocks (8-rank slab 39.5-39.8 µs per
+    // iteration at rho 1.0-1.3, 4×2 43.9-44.1, 4-rank 71.9-72.5) and slower
+    // at 8192² from 1.2 (3975 / 3719 it/s vs 4009): a second-slot wave speeds
+    // up once its SIMD partner is done, so the SIMD stays busy either way
+    // (profiles/r5_epilogue.txt).  Default 1: equal loads.
+    double rho = 1.0;
+    if (const char* e = std::getenv("PE_YOUNG")) rho = std::max(0.5, std::atof(e));
+    auto capw = [&](int w, int Wn) {
+      return (Wn / dev::kWPB > cus_ && w / dev::kWPB < cus_) ? rho : 1.0;
+    };
     if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
     if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
     if (equal) {
@@ -635,14 +654,16 @@ void DeviceSolver::setup_items() {
         }
         using LW = std::pair<double, int>;
         std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
-        for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], wrank(w, W)});
+        double csum = 0.0;
+        for (int w = 0; w < W; ++w) csum += capw(w, W);
+        for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)] / capw(w, W), wrank(w, W)});
         while (!q.empty()) {
           QE e = q.top();
           q.pop();
           const LW t = heap.top();
           heap.pop();
           const int tw = wfrom(t.second, W);
-          const double room = T - t.first;
+          const double room = (rho == 1.0 ? T : T * W * capw(tw, W) / csum) - load[size_t(tw)];
           Piece give = e.p;
           if (e.p.cost > room && room >= minc && e.p.rows >= 2 * minr) {
             // the most rows of e.p that fit the room (binary search; cost grows with rows)
@@ -665,7 +686,8 @@ void DeviceSolver::setup_items() {
           }
           per[size_t(tw)].push_back(int(pcs.size()));
           pcs.push_back(give);
-          heap.push(LW{t.first + give.cost, t.second});
+          load[size_t(tw)] += give.cost;
+          heap.push(LW{load[size_t(tw)] / capw(tw, W), t.second});
         }
         if (ncut == cuts) break;
         cuts = ncut;
@@ -715,12 +737,14 @@ void DeviceSolver::setup_items() {
                      [&](int a, int b) { return pcs[size_t(a)].cost > pcs[size_t(b)].cost; });
     using LW = std::pair<double, int>;
     std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
-    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)], wrank(w, W)});
+    for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)] / capw(w, W), wrank(w, W)});
     for (int i : order) {
       const LW t = heap.top();
       heap.pop();
-      per[size_t(wfrom(t.second, W))].push_back(i);
-      heap.push(LW{t.first + kcost[size_t(i)], t.second});
+      const int tw = wfrom(t.second, W);
+      per[size_t(tw)].push_back(i);
+      load[size_t(tw)] += kcost[size_t(i)];
+      heap.push(LW{load[size_t(tw)] / capw(tw, W), t.second});
     }
     lay_cuts_ = 0;
     }
@@ -755,6 +779,17 @@ void DeviceSolver::setup_items() {
             for (int l = 0; l < dev::kWPB; ++l) phys[i++] = b * dev::kWPB + l;
       } else {
         for (int w = 0; w < W; ++w) phys[i++] = w;
+      }
+      // PE_WPERM (diagnostic: does a slow item stay slow on another wave?):
+      // 1 lists on the workgroups in reverse order, 2 rotated by a quarter of
+      // the grid (other co-resident workgroup pairs)
+      if (const char* e = std::getenv("PE_WPERM"); e && !xmap) {
+        const int m = std::atoi(e);
+        for (int w = 0; w < W; ++w) {
+          const int b = w / dev::kWPB, l = w % dev::kWPB;
+          const int pb = m == 1 ? nb - 1 - b : m == 2 ? (b + nb / 4) % nb : b;
+          phys[size_t(w)] = pb * dev::kWPB + l;
+        }
       }
     }
     std::vector<int2> all(rounds * size_t(W), int2{0, 0});  // {0, 0}: empty entry (0 rows)

@@ -260,6 +260,108 @@ __device__ __forceinline__ void reduce_partials(const double* partial, unsigned 
   block_reduce<N, false>(v, sm);
 }
 
+// ---- the s-step sweeps' grid reduction (kS3 / kSS) -------------------------
+// Wave64 sum of one double by DPP (row_shr 1/2/4/8, then row_bcast 15/31):
+// lane 63 ends with the total, in a fixed order (the same bits in every
+// workgroup; no LDS round trips, unlike the __shfl_xor tree's ds_bpermute
+// pairs).  Identity 0.0 for lanes a step does not feed.
+template <int CTRL, int RM, int BM>
+__device__ __forceinline__ double dpp_d(double v) {
+  const long long x = __builtin_bit_cast(long long, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, int(x), CTRL, RM, BM, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), CTRL, RM, BM, false);
+  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
+}
+__device__ __forceinline__ double wave_sum63(double v) {
+  v += dpp_d<0x111, 0xF, 0xF>(v);  // row_shr:1
+  v += dpp_d<0x112, 0xF, 0xF>(v);  // row_shr:2
+  v += dpp_d<0x114, 0xF, 0xE>(v);  // row_shr:4
+  v += dpp_d<0x118, 0xF, 0xC>(v);  // row_shr:8
+  v += dpp_d<0x142, 0xA, 0xF>(v);  // row_bcast:15
+  v += dpp_d<0x143, 0xC, 0xF>(v);  // row_bcast:31
+  return v;
+}
+
+// Block sums of N values → the grid's partials, laid out n-major
+// (partial[n · nblocks + b]: the last block's loads are coalesced), one store
+// instruction from lanes 0..N-1 of wave 0, then the ticket; true in the block
+// that arrives last (after its acquire).  Replaces block_reduce + publish_last
+// + reduce_partials for the sweeps' 19 sums: block-major tuples made the last
+// block's reduction 9728 single-line lane requests, 4.6 µs of every sweep's
+// epilogue (tools/stamp_probe.py "last block" line, profiles/r5_epilogue.txt).
+template <int N>
+__device__ __forceinline__ bool publish_last_nm(double* partial, const double (&v)[N], unsigned* ticket, int* sflag,
+                                                double* sm) {
+  const int lane = int(threadIdx.x & 63), wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  double w[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) w[n] = wave_sum63(v[n]);
+  if (lane == 63)
+#pragma unroll
+    for (int n = 0; n < N; ++n) sm[n * kWPB + wid] = w[n];
+  __syncthreads();
+  if (wid == 0) {
+    if (lane < N) {
+      double s = sm[lane * kWPB];
+#pragma unroll
+      for (int q = 1; q < kWPB; ++q) s += sm[lane * kWPB + q];
+      __hip_atomic_store(partial + size_t(lane) * gridDim.x + blockIdx.x, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (lane == 0) {
+      const unsigned t = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = (t == gridDim.x - 1);
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      *sflag = last;
+    }
+  }
+  __syncthreads();
+  return *sflag != 0;
+}
+
+// The last block: the N grid sums from publish_last_nm's partials → thread 0.
+// Wave q sums the values n ≡ q (mod kWPB); every lane loads its blocks
+// lane, lane + 64, … (all loads of up to 512 blocks issued before the first
+// add), then a DPP wave sum.  Deterministic: the order depends on nblocks only.
+template <int N>
+__device__ __forceinline__ void reduce_partials_nm(const double* partial, double (&t)[N], double* sm) {
+  const int lane = int(threadIdx.x & 63), wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
+  const unsigned nb = gridDim.x;
+  constexpr int PER = (N + kWPB - 1) / kWPB, U = 8;
+  double s[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) s[j] = 0.0;
+  for (unsigned m0 = 0; m0 < nb; m0 += U * 64) {
+    double x[PER][U];
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int n = wid + kWPB * j;
+        const unsigned m = m0 + unsigned(64 * u + lane);
+        x[j][u] = (n < N && m < nb) ? partial[size_t(n) * nb + m] : 0.0;
+      }
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+#pragma unroll
+      for (int u = 0; u < U; ++u) s[j] += x[j][u];
+  }
+#pragma unroll
+  for (int j = 0; j < PER; ++j) s[j] = wave_sum63(s[j]);
+  __syncthreads();  // (sm: publish_last_nm's reads are done)
+  if (lane == 63)
+#pragma unroll
+    for (int j = 0; j < PER; ++j)
+      if (wid + kWPB * j < N) sm[wid + kWPB * j] = s[j];
+  __syncthreads();
+  if (threadIdx.x == 0)
+#pragma unroll
+    for (int n = 0; n < N; ++n) t[n] = sm[n];
+}
+
 // One p_k value at a single node (strip-edge columns, prologue only).
 template <bool EXACT>
 __device__ __forceinline__ double p_point(const KParams& k, int64_t q, int64_t lj, double beta, const double* pold) {

@@ -92,25 +92,7 @@ struct Coef {
   }
 };
 
-// Wave64 sum of one double by DPP (row_shr 1/2/4/8, then row_bcast 15/31):
-// lane 63 ends with the total, in a fixed order (the same bits in every
-// workgroup).  Identity 0.0 for lanes a step does not feed.
-template <int CTRL, int RM, int BM>
-__device__ __forceinline__ double dpp_d(double v) {
-  const long long x = __builtin_bit_cast(long long, v);
-  const int lo = __builtin_amdgcn_update_dpp(0, int(x), CTRL, RM, BM, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, int(x >> 32), CTRL, RM, BM, false);
-  return __builtin_bit_cast(double, (static_cast<long long>(hi) << 32) | static_cast<unsigned>(lo));
-}
-__device__ __forceinline__ double wave_sum63(double v) {
-  v += dpp_d<0x111, 0xF, 0xF>(v);  // row_shr:1
-  v += dpp_d<0x112, 0xF, 0xF>(v);  // row_shr:2
-  v += dpp_d<0x114, 0xF, 0xE>(v);  // row_shr:4
-  v += dpp_d<0x118, 0xF, 0xC>(v);  // row_shr:8
-  v += dpp_d<0x142, 0xA, 0xF>(v);  // row_bcast:15
-  v += dpp_d<0x143, 0xC, 0xF>(v);  // row_bcast:31
-  return v;
-}
+// (wave_sum63: kcommon.hpp)
 
 __global__ __launch_bounds__(RT, 1) void kResident(KParams k, ResParams rp) {
   extern __shared__ double lds_raw[];

@@ -364,6 +364,7 @@ class DeviceSolver {
   std::vector<int2> ilist_host_;
   std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
+  int cus_ = 256;                  // compute units of the device (a static layout's first cus_ workgroups run first on their CU)
   bool resident_ = false;
   bool resident_fallback_ = false;  // a resident launch aborted (status 5): switched to the streaming sweep
   int stream_chunk_ = 16;           // chunk length of the streaming sweep (after a resident fallback)

@@ -43,6 +43,8 @@ def step_timeline(steps: np.ndarray, three: bool = False) -> str:
     out = ["  first-item timeline (median us after item start, n waves; per-group increment):"]
     prev = None
     for c in range(1, 32):
+        if three and c == 30:  # (slot 30: the wave's hardware id)
+            continue
         v = s[:, c]
         ok = v > 0
         if ok.sum() < max(1, len(s) // 4):
@@ -76,6 +78,48 @@ def grid_timeline(glob: np.ndarray, steps: np.ndarray, wv_all: np.ndarray) -> st
     out.append(f"    first item start: median {np.median(first_items - t0) / 100.0:6.2f}")
     out.append(f"    last wave exit {(wv[:, 1].max() - t0) / 100.0:7.2f}; grid reduction start {(g[1] - t0) / 100.0:7.2f}; "
                f"finalized {(g[2] - t0) / 100.0:7.2f}")
+    if g[5] > 0 and g[6] > 0:  # the last block: block reduction, publish, partials summed, finalize start
+        out.append(f"    last block: block reduce {(g[5] - t0) / 100.0:7.2f}, publish {(g[6] - t0) / 100.0:7.2f}, ticket won "
+                   f"{(g[1] - t0) / 100.0:7.2f}, partials summed {(g[3] - t0) / 100.0:7.2f}, finalize start "
+                   f"{(g[4] - t0) / 100.0:7.2f}, done {(g[2] - t0) / 100.0:7.2f}")
+    return "\n".join(out)
+
+
+def simd_tail(steps: np.ndarray, wv_all: np.ndarray) -> str:
+    """Three-step kStamp: slot 30 holds the wave's HW_ID | XCC_ID << 32 — the
+    exits per SIMD (the last of its waves) and per CU: is the tail whole
+    SIMDs idle, or a SIMD running one wave instead of two?"""
+    s = steps.reshape(-1, 32).astype(np.int64)
+    hw = s[:, 30]
+    live = (wv_all[: len(hw), 0] > 0) & (s[:, 1] > 0)
+    if not live.any():
+        return "  (no hardware ids)"
+    hw, ex = hw[live], wv_all[: len(live)][live, 1]
+    t0 = s[live, 1].min()
+    simd = (hw >> 4) & 3
+    cu = (hw >> 8) & 15
+    sh = (hw >> 12) & 1
+    se = (hw >> 13) & 7
+    xcc = (hw >> 32) & 15
+    cuk = ((xcc * 8 + se) * 2 + sh) * 16 + cu
+    simdk = cuk * 4 + simd
+    out = [f"  placement: {len(np.unique(cuk))} CUs, {len(np.unique(simdk))} SIMDs, {len(np.unique(xcc))} XCCs; "
+           f"waves per SIMD max {np.bincount(np.unique(simdk, return_inverse=True)[1]).max()}"]
+    for name, key in (("SIMD", simdk), ("CU", cuk)):
+        u, inv = np.unique(key, return_inverse=True)
+        last = np.zeros(len(u), dtype=np.int64)
+        np.maximum.at(last, inv, ex)
+        e = (last - t0) / 100.0
+        out.append(f"  {name} exit (its last wave): min {e.min():6.1f} p10 {pct(e, 10):6.1f} median {np.median(e):6.1f} "
+                   f"p90 {pct(e, 90):6.1f} max {e.max():6.1f} us")
+    # per SIMD: first and last wave exit (one wave alone for how long)
+    u, inv = np.unique(simdk, return_inverse=True)
+    first = np.full(len(u), np.iinfo(np.int64).max)
+    last = np.zeros(len(u), dtype=np.int64)
+    np.minimum.at(first, inv, ex)
+    np.maximum.at(last, inv, ex)
+    alone = (last - first) / 100.0
+    out.append(f"  SIMD with one wave left: median {np.median(alone):6.1f} p90 {pct(alone, 90):6.1f} us (last minus first wave exit)")
     return "\n".join(out)
 
 
@@ -168,6 +212,19 @@ def summarise(st: np.ndarray, nitems: int, nw: int, three: bool = False) -> str:
         slot = gw % 4
         out.append("  uniform us/step by XCD: " + " ".join(f"{np.median(per_step[uni & (xcd == x)]):.3f}" for x in range(8)))
         out.append("  uniform us/step by wave slot: " + " ".join(f"{np.median(per_step[uni & (slot == x)]):.3f}" for x in range(4)))
+        # by the item's first row (deciles of the block) and by its physical workgroup (deciles of the grid):
+        # a position effect (memory) follows the rows under a permuted wave map (PE_WPERM), a hardware one the waves
+        r0 = geo & 0xFFFFFFFF
+        rb = np.minimum(9, (r0 * 10) // max(1, int(r0.max()) + 1))
+        out.append("  uniform us/step by row decile: " + " ".join(f"{np.median(per_step[uni & (rb == x)]):.3f}"
+                                                              if (uni & (rb == x)).any() else "  -  " for x in range(10)))
+        nwg = int(gw.max()) // 4 + 1
+        bb = np.minimum(9, ((gw // 4) * 10) // nwg)
+        out.append("  uniform us/step by workgroup decile: " + " ".join(f"{np.median(per_step[uni & (bb == x)]):.3f}"
+                                                                    if (uni & (bb == x)).any() else "  -  " for x in range(10)))
+        sb = np.minimum(9, (strip * 10) // max(1, int(strip.max()) + 1))
+        out.append("  uniform us/step by strip decile: " + " ".join(f"{np.median(per_step[uni & (sb == x)]):.3f}"
+                                                                for x in range(10) if (uni & (sb == x)).any()))
         # position in the wave's list (round): early rounds run with the whole chip busy
         rnd = np.zeros(len(it), dtype=int)
         order = np.lexsort((it[:, 0], gw))
@@ -187,10 +244,57 @@ def summarise(st: np.ndarray, nitems: int, nw: int, three: bool = False) -> str:
         ratio = wl_all[m] / wc[m]
         out.append(f"  wave time / static cost: p10 {pct(ratio, 10):.3f} median {np.median(ratio):.3f} p90 {pct(ratio, 90):.3f}"
                    f"  (corr of wave time with cost {np.corrcoef(wl_all[m], wc[m])[0, 1]:.2f})")
+    if three:
+        out.append(simd_tail(steps, wv_all))
     out.append(step_timeline(steps, three))
     if three:
         out.append(grid_timeline(glob, steps, wv_all))
     return "\n".join(out)
+
+
+def item_times(st: np.ndarray, nitems: int, nw: int):
+    """Per item slot: duration (µs, 0 for an empty slot) and wave; per wave: exit time after the first entry."""
+    body = st[: len(st) - 32 * nw - 8]
+    it = body[: 4 * nitems].reshape(nitems, 4).astype(np.int64)
+    wv = body[4 * nitems: 4 * nitems + 2 * nw].reshape(-1, 2).astype(np.int64)
+    dur = np.where(it[:, 0] > 0, (it[:, 1] - it[:, 0]) / 100.0, 0.0)
+    live = wv[:, 0] > 0
+    ex = np.where(live, (wv[:, 1] - wv[live, 0].min()) / 100.0, np.nan)
+    return dur, ex
+
+
+def persistence(durs) -> str:
+    """Is a slow item (or wave) slow again in the next sweep?  Correlations of
+    per-item durations and per-wave exit times between consecutive sweeps of
+    one process (same layout, same memory): high values would let a layout be
+    rebalanced from measured times; low values mean the spread is noise."""
+    out = ["  persistence across sweeps (consecutive pairs):"]
+    for a in range(len(durs) - 1):
+        (d0, e0), (d1, e1) = durs[a], durs[a + 1]
+        m = (d0 > 0) & (d1 > 0)
+        w = np.isfinite(e0) & np.isfinite(e1)
+        # relative duration: item time over the median of its row count is unknown here, use raw
+        out.append(f"    sweeps {a}->{a + 1}: item duration corr {np.corrcoef(d0[m], d1[m])[0, 1]:5.2f}  "
+                   f"wave exit corr {np.corrcoef(e0[w], e1[w])[0, 1]:5.2f}  "
+                   f"late-decile overlap {late_overlap(e0[w], e1[w]):4.2f}")
+    e = np.stack([x[1] for x in durs])
+    w = np.all(np.isfinite(e), 0)
+    mean_ex = e[:, w].mean(0)
+    out.append(f"    wave exit averaged over {len(durs)} sweeps: median {np.median(mean_ex):6.1f}  max {mean_ex.max():6.1f}"
+               f"  (single sweeps: max - median {np.mean([np.nanmax(x) - np.nanmedian(x) for x in e]):5.1f}; "
+               f"averaged: {mean_ex.max() - np.median(mean_ex):5.1f} us)")
+    gw = np.nonzero(w)[0]
+    xcd = (gw // 4) % 8
+    out.append("    mean wave exit by XCD: " + " ".join(f"{np.median(mean_ex[xcd == x]):6.1f}" for x in range(8)))
+    return "\n".join(out)
+
+
+def late_overlap(e0, e1) -> float:
+    """Fraction of the last-finishing 10 % of waves in one sweep that are also in the last 10 % of the other."""
+    k = max(1, len(e0) // 10)
+    a = set(np.argsort(e0)[-k:])
+    b = set(np.argsort(e1)[-k:])
+    return len(a & b) / k
 
 
 def main():
@@ -218,13 +322,20 @@ def main():
             s.clear_stamps()
             if three:  # (a launch records the previous one's finalize: the gap between launches)
                 s.run_iterations(1, False)
-            for sweep in ("deferring", "applying"):  # iterations alternate the two sweep variants
+            durs = []
+            nrep = int(os.environ.get("PROBE_REPEAT", "2"))
+            for rep in range(nrep):  # iterations alternate the two sweep variants
+                sweep = ("deferring", "applying")[rep % 2]
                 if not three:
                     s.clear_stamps()
                 s.run_iterations(1, False)
                 st = np.asarray(s.stamps())
-                print(f" one {sweep}-parity sweep:")
-                print(summarise(st, s.nitems, s.stamp_waves, three), flush=True)
+                if rep < 2:
+                    print(f" one {sweep}-parity sweep:")
+                    print(summarise(st, s.nitems, s.stamp_waves, three), flush=True)
+                durs.append(item_times(st, s.nitems, s.stamp_waves))
+            if nrep > 2:
+                print(persistence(durs), flush=True)
             del s, comm
             for k, v in saved.items():
                 if v is None:
