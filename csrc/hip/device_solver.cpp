@@ -282,6 +282,14 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.hdep = hdep_;
   k.pre_load = !(std::getenv("PE_PRE") && std::atoi(std::getenv("PE_PRE")) == 0);
   k.dring = !(std::getenv("PE_DRING") && std::atoi(std::getenv("PE_DRING")) == 0);
+  // SIMD priority turns (fused3.hip prio_turn): on by default below 6·10⁶
+  // nodes, where the sweep ends with one item per wave and the second-slot
+  // waves marching alone (2048²: T_iterate 0.0463-0.0467 s at PE_PRIO=8/10 vs
+  // 0.0471-0.0472 off); off above (8192²: 3776-3834 it/s vs 3973-4019 — the
+  // older waves' head start is worth more there; the 8-rank slab and 4×2
+  // blocks neutral) — profiles/r5_prio.txt
+  k.prio = std::getenv("PE_PRIO") ? std::max(0, std::min(20, std::atoi(std::getenv("PE_PRIO"))))
+                                  : (double(nx) * double(ny) < 6e6 ? 10 : 0);
   k.xorg = xorg_;
   k.nx = nx;
   k.ny = ny;
@@ -368,6 +376,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     PE_HIP_CHECK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   }
   cus_ = cus;
+  k.ncu = cus;
   // rows per item and item order first: they select the sweep kernel variant
   // whose occupancy sizes the grid
   const double npts = double(nx) * double(ny);

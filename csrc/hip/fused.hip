@@ -965,10 +965,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
   }
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
-  block_reduce<7, false>(v, sm);
-  if (publish_last<7>(k.partial + 7 * size_t(blockIdx.x), v, &st->ticket[0], gridDim.x, &sflag)) {
+  if (publish_last_nm<7>(k.partial, v, &st->ticket[0], &sflag, sm)) {  // (kcommon.hpp: n-major partials)
     double t[7];
-    reduce_partials<7>(k.partial, gridDim.x, t, sm);
+    reduce_partials_nm<7>(k.partial, t, sm);
     finalize_block<WM>(k, st, par, sc, t);
     if (threadIdx.x == 0) __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
@@ -1024,10 +1023,9 @@ __global__ __launch_bounds__(TJ) void kRed(KParams k, int par) {
       v[6] += in ? b[u].z : 0.0;
     }
   }
-  block_reduce<7, false>(v, sm);
-  if (publish_last<7>(k.partial + 7 * size_t(blockIdx.x), v, &st->ticket[1], gridDim.x, &sflag)) {
+  if (publish_last_nm<7>(k.partial, v, &st->ticket[1], &sflag, sm)) {  // (kcommon.hpp: n-major partials)
     double t[7];
-    reduce_partials<7>(k.partial, gridDim.x, t, sm);
+    reduce_partials_nm<7>(k.partial, t, sm);
     finalize_block<WM>(k, st, par, sc, t);
     if (threadIdx.x == 0) __hip_atomic_store(&st->ticket[1], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }

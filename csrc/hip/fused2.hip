@@ -488,10 +488,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   if (lane < 2 || lane > 61)  // strip halo lanes: recomputed copies of the neighbouring strips' columns
 #pragma unroll
     for (int n = 0; n < NS; ++n) acc[n] = 0.0;
-  block_reduce<NS, false>(acc, sm);
-  if (publish_last<NS>(k.partial + NS * size_t(blockIdx.x), acc, &st->ticket[0], gridDim.x, &sflag)) {
+  if (publish_last_nm<NS>(k.partial, acc, &st->ticket[0], &sflag, sm)) {  // (kcommon.hpp: n-major partials)
     double t[NS];
-    reduce_partials<NS>(k.partial, gridDim.x, t, sm);
+    reduce_partials_nm<NS>(k.partial, t, sm);
     __shared__ double xv[NS + 1];
     __shared__ unsigned long long sseq;
     __shared__ int sok;

@@ -654,6 +654,21 @@ __device__ __forceinline__ unsigned long long rtc3() {
   return t;
 }
 
+// PE_PRIO (KParams::prio > 0, experimental): the two waves on a SIMD — one of
+// a CU's first workgroup, one of its second — take turns at issue priority
+// every 2^prio ticks of the 100 MHz clock.  By default the older wave wins
+// every tie and runs ≈12-23 % faster per row step, then the younger one
+// marches alone at the end of the sweep (tools/stamp_probe.py "SIMD with one
+// wave left", profiles/r5_wave_age.txt).
+__device__ __forceinline__ void prio_turn(const KParams& k) {
+  if (k.prio > 0) {
+    const unsigned long long t = rtc3();
+    const bool young = int(blockIdx.x) >= k.ncu;
+    if ((((t >> k.prio) & 1ull) != 0) != young) __builtin_amdgcn_s_setprio(1);
+    else __builtin_amdgcn_s_setprio(0);
+  }
+}
+
 // (SST, the diagnostic build only: sst != nullptr stamps this item's
 // prologue and every 6-step group into the wave's step stamps)
 template <int KIND, bool PUSH, bool EDGE, bool SST = false>
@@ -743,6 +758,7 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
       if (sst && lane == 0 && sg < 30) sst[sg] = rtc3();  // (slot 30: the wave's hardware id)
       ++sg;
     }
+    prio_turn(k);
   };
   // steady groups (uniform items): stage rows t-6 .. t and the prefetched
   // rows inside the item for all six steps (n ≥ 12, n ≤ rows + 4); the fill
@@ -1003,6 +1019,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     cf = sc.c;
   }
   walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc, pre, use_pre);
+  if (k.prio > 0) __builtin_amdgcn_s_setprio(0);
   if (replay) return;
   if (fix) {
     finish(lt.stop, K0 + lt.stop, lt.status, lt.stop);
