@@ -282,14 +282,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.hdep = hdep_;
   k.pre_load = !(std::getenv("PE_PRE") && std::atoi(std::getenv("PE_PRE")) == 0);
   k.dring = !(std::getenv("PE_DRING") && std::atoi(std::getenv("PE_DRING")) == 0);
-  // SIMD priority turns (fused3.hip prio_turn): on by default below 6·10⁶
-  // nodes, where the sweep ends with one item per wave and the second-slot
-  // waves marching alone (2048²: T_iterate 0.0463-0.0467 s at PE_PRIO=8/10 vs
-  // 0.0471-0.0472 off); off above (8192²: 3776-3834 it/s vs 3973-4019 — the
-  // older waves' head start is worth more there; the 8-rank slab and 4×2
-  // blocks neutral) — profiles/r5_prio.txt
-  k.prio = std::getenv("PE_PRIO") ? std::max(0, std::min(20, std::atoi(std::getenv("PE_PRIO"))))
-                                  : (double(nx) * double(ny) < 6e6 ? 10 : 0);
+  // SIMD priority turns (fused3.hip prio_turn), opt-in: 1-GPU 2048² and
+  // 1600×2400 T_iterate −0.8-1.5 % at PE_PRIO=10, but the 2-rank blocks of
+  // 2048² / 1600×2400 +2-7 % (20.2 vs 18.9 µs per iteration), 8192² −4-6 %
+  // it/s, the 8-rank slab and 4×2 blocks neutral — profiles/r5_prio.txt
+  k.prio = std::getenv("PE_PRIO") ? std::max(0, std::min(20, std::atoi(std::getenv("PE_PRIO")))) : 0;
   k.xorg = xorg_;
   k.nx = nx;
   k.ny = ny;
@@ -578,9 +575,16 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     }
     seg_layout_ = best == 0;
     // three-step: the other static layouts at the best height
+    std::string keep = lay_name_;
+    struct Tried {
+      int ti;
+      std::string lay;
+      float ms;
+    };
+    std::vector<Tried> tried;
+    for (size_t i = 0; i < ti_rows_.size(); ++i) tried.push_back(Tried{ti_rows_[i], lay_name_, ti_ms_[i] * float(kTimed)});
     if (steps_ >= 3 && best != 0 && !std::getenv("PE_LAYOUT")) {
       const std::string base = lay_name_;
-      std::string keep = base;
       for (const char* alt : {"equal", "fill", "lpt"}) {
         if (base == alt) continue;
         lay_name_ = alt;
@@ -589,13 +593,35 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
         const float ms = time_layout();
         ti_ms_.push_back(ms / float(kTimed));
         ti_rows_.push_back(-best);  // (negative: a layout candidate at that height)
+        tried.push_back(Tried{best, alt, ms});
         if (ms < best_ms) {
           best_ms = ms;
           keep = alt;
         }
       }
-      lay_name_ = keep;
     }
+    // Finalists: the two fastest candidates timed once more, each keeping its
+    // faster timing — the GPU clock ramps up during construction, so the first
+    // candidates were timed slow, and two within ≈2 % swapped places from one
+    // process to the next (2400×3200: equal layout at 80 rows or filling at
+    // 96, T_iterate 0.099 vs 0.095 s, profiles/r5_prio.txt).  Three-step only.
+    if (steps_ >= 3 && best != 0 && tried.size() >= 2) {
+      std::stable_sort(tried.begin(), tried.end(), [](const Tried& a, const Tried& b) { return a.ms < b.ms; });
+      for (int f = 0; f < 2; ++f) {
+        Tried& t = tried[size_t(f)];
+        lay_name_ = t.lay;
+        set_items(t.ti);
+        setup_items();
+        const float ms = time_layout();
+        ti_ms_.push_back(ms / float(kTimed));
+        ti_rows_.push_back(t.lay == keep && t.ti == best ? best : -t.ti);
+        t.ms = std::min(t.ms, ms);
+      }
+      const Tried& w = tried[0].ms <= tried[1].ms ? tried[0] : tried[1];
+      best = w.ti;
+      keep = w.lay;
+    }
+    lay_name_ = keep;
     set_items(best == 0 ? ti : best);
     setup_items();
   }

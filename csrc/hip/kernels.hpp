@@ -208,7 +208,7 @@ struct KParams {
   int pre_load;
   // band items: 1/D from the LDS ring (1) or re-formed from the faces (0, PE_DRING=0)
   int dring;
-  // three-step sweep, PE_PRIO (experimental): > 0 → the two waves sharing a
+  // three-step sweep, PE_PRIO (opt-in): > 0 → the two waves sharing a
   // SIMD take turns at issue priority (s_setprio), switching every
   // 2^prio × 10 ns; ncu: workgroups ≥ ncu are the second ones on their CU
   int prio;

@@ -54,7 +54,8 @@ def _boundary_first(s, blk):
                                         (1, "device", {"PE_LAYOUT": "fill"}), (8, "device", {}),
                                         (2, "device", {}), (4, "device", {"PE_LAYOUT": "equal"}),
                                         (8, "4x2", {"PE_OVERLAP": "1"}), (6, "2x3", {"PE_OVERLAP": "1"}),
-                                        (4, "2x2", {"PE_OVERLAP": "1", "PE_LAYOUT": "lpt"})])
+                                        (4, "2x2", {"PE_OVERLAP": "1", "PE_LAYOUT": "lpt"}),
+                                        (8, "device", {"PE_YOUNG": "1.25"}), (1, "device", {"PE_YOUNG": "1.25"})])
 def test_layout_covers_every_row_once(gpu, nat, monkeypatch, P, spec, env):
     for k, v in env.items():
         monkeypatch.setenv(k, v)
@@ -107,3 +108,33 @@ def test_overlap_full_grid_launches(gpu, nat, monkeypatch):
         del s, comm
     scale = np.abs(ws[0]).max()
     assert scale > 0 and np.abs(ws[0] - ws[1]).max() <= 1e-9 * scale
+
+
+def test_priority_turns_and_wave_map_keep_the_sums(gpu, nat, monkeypatch):
+    """SIMD priority turns (PE_PRIO, fused3.hip prio_turn) change only when
+    waves issue: 30 iterations give the same bits with and without them.  A
+    permuted list -> workgroup map (PE_WPERM) groups other items into each
+    workgroup's partial sum: the same w to rounding.  2048² on one GPU, fixed
+    rows per item (no timing-dependent tuning)."""
+    monkeypatch.setenv("PE_TI", "64")
+    monkeypatch.setenv("PE_LAYOUT", "equal")
+    ws = {}
+    for name, env in (("off", {"PE_PRIO": "0"}), ("turns", {"PE_PRIO": "10"}), ("fast", {"PE_PRIO": "7"}),
+                      ("perm", {"PE_PRIO": "0", "PE_WPERM": "1"})):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        blk = nat.decompose(2048, 2048, D.grid(1, 2048, 2048, "device"), 0)
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        s = nat.DeviceSolver(EllipseProblem(2048, 2048).to_native(), blk, None, opt)
+        assert s.sweep_steps == 3 and not s.resident
+        s.reset()
+        s.run_iterations(30, False)
+        s.synchronize()
+        ws[name] = np.array(s.w())
+        del s
+        monkeypatch.delenv("PE_WPERM", raising=False)
+    scale = np.abs(ws["off"]).max()
+    assert scale > 0
+    assert np.array_equal(ws["off"], ws["turns"]) and np.array_equal(ws["off"], ws["fast"])
+    assert np.abs(ws["off"] - ws["perm"]).max() <= 1e-9 * scale
