@@ -3,7 +3,7 @@
 # round-4 layouts (LPT, filling, equal-cost) on 8192^2 and the 8-rank
 # slab block (GRID=1024 8191) -> profiles/r4_dram.txt
 set -o pipefail
-R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r4dram; mkdir -p $O
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/${DRAM_OUT:-r4dram}; mkdir -p $O
 BIN=$R/bin/pe_hip
 cd /tmp && export TMPDIR=/tmp
 i=0
