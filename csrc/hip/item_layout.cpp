@@ -772,8 +772,16 @@ void DeviceSolver::setup_items() {
     {
       const bool xmap = std::getenv("PE_XCD_MAP") && std::atoi(std::getenv("PE_XCD_MAP")) == 1;
       const int nb = W / dev::kWPB;
+      // PE_XCD_GROUP=g (opt-in): runs of g consecutive lists' workgroups on one
+      // XCD (g = 1: the default round-robin; PE_XCD_MAP=1 ≈ nb / 8)
+      const int xg = std::getenv("PE_XCD_GROUP") ? std::max(1, std::atoi(std::getenv("PE_XCD_GROUP"))) : 1;
       size_t i = 0;
-      if (xmap) {
+      if (!xmap && xg > 1 && nb % (8 * xg) == 0) {
+        for (int lb = 0; lb < nb; ++lb) {
+          const int G = lb / xg, x = G % 8, slot = (G / 8) * xg + lb % xg;
+          for (int l = 0; l < dev::kWPB; ++l) phys[i++] = (slot * 8 + x) * dev::kWPB + l;
+        }
+      } else if (xmap) {
         for (int x = 0; x < 8; ++x)
           for (int b = x; b < nb; b += 8)
             for (int l = 0; l < dev::kWPB; ++l) phys[i++] = b * dev::kWPB + l;
