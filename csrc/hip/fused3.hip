@@ -755,7 +755,7 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   }
   auto sstamp = [&]() {
     if constexpr (SST) {
-      if (sst && lane == 0 && sg < 30) sst[sg] = rtc3();  // (slot 30: the wave's hardware id)
+      if (sst && lane == 0 && sg < 28) sst[sg] = rtc3();  // (slots 28/29: shader clock at entry / exit, 30: hardware id)
       ++sg;
     }
     prio_turn(k);
@@ -908,7 +908,10 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
     }
   }
   if constexpr (STAMP) {
-    if (l0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc3();
+    if (l0) {
+      k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc3();
+      k.stamps2[32 * int64_t(gwave) + 29] = __builtin_amdgcn_s_memtime();  // (shader clock: Δ / Δ realtime)
+    }
   }
 }
 
@@ -930,6 +933,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
       // where the wave runs: HW_ID (wave slot, SIMD, CU, SE) | XCC_ID << 32
       const unsigned hw = __builtin_amdgcn_s_getreg(4 | (31 << 11)), xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11));
       k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + 30] = hw | (static_cast<unsigned long long>(xcc) << 32);
+      k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + 28] = __builtin_amdgcn_s_memtime();
       if (blockIdx.x == 0 && wid == 0) k.stamps2[-8] = k.stamps2[-6];
     }
   }

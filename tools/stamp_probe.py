@@ -43,7 +43,7 @@ def step_timeline(steps: np.ndarray, three: bool = False) -> str:
     out = ["  first-item timeline (median us after item start, n waves; per-group increment):"]
     prev = None
     for c in range(1, 32):
-        if three and c == 30:  # (slot 30: the wave's hardware id)
+        if three and c >= 28 and c <= 30:  # (slots 28/29: shader clock, 30: the wave's hardware id)
             continue
         v = s[:, c]
         ok = v > 0
@@ -120,6 +120,14 @@ def simd_tail(steps: np.ndarray, wv_all: np.ndarray) -> str:
     np.maximum.at(last, inv, ex)
     alone = (last - first) / 100.0
     out.append(f"  SIMD with one wave left: median {np.median(alone):6.1f} p90 {pct(alone, 90):6.1f} us (last minus first wave exit)")
+    # shader clock over each wave's life: Δ s_memtime (cycles) / Δ s_memrealtime (100 MHz)
+    mt0, mt1 = s[live, 28], s[live, 29]
+    rt0, rt1 = s[live, 1], wv_all[: len(live)][live, 1]
+    ok = (mt1 > mt0) & (rt1 > rt0 + 1000)
+    if ok.any():
+        ghz = (mt1[ok] - mt0[ok]) / ((rt1[ok] - rt0[ok]) * 10.0)  # cycles per 10 ns tick -> GHz
+        out.append(f"  shader clock over a wave's life: median {np.median(ghz):5.3f} GHz  p10 {pct(ghz, 10):5.3f}  p90 {pct(ghz, 90):5.3f}"
+                   f"  (by XCC: {' '.join(f'{np.median(ghz[xcc[ok] == x]):.2f}' for x in range(8) if (xcc[ok] == x).any())})")
     return "\n".join(out)
 
 
