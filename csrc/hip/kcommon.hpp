@@ -292,6 +292,7 @@ __device__ __forceinline__ double wave_sum63(double v) {
 template <int N>
 __device__ __forceinline__ bool publish_last_nm(double* partial, const double (&v)[N], unsigned* ticket, int* sflag,
                                                 double* sm) {
+  static_assert(N <= 64, "one store instruction: lanes 0..N-1 of wave 0");
   const int lane = int(threadIdx.x & 63), wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   double w[N];
 #pragma unroll
