@@ -956,7 +956,20 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   // 1. the previous sweep's pending stop tests
   const int m0 = st->late3;
   const long long K = st->iter, K0 = K - m0;
+  // (kStamp: prologue points into the wave's step-stamp slots 24-27 — state
+  // read and the stop tests decided / scalars formed / walk entered)
+  auto pstamp = [&](int slot, double dep) {
+    if constexpr (MODE == kStamp) {
+      if (lane == 0) {
+        // (dep: a value of the phase — the empty asm needs it in a register
+        // before the clock read, which stays after it: both volatile)
+        asm volatile("" ::"v"(dep));
+        k.stamps2[32 * (int64_t(blockIdx.x) * kWPB + wid) + slot] = rtc3();
+      }
+    }
+  };
   const Late3 lt = late3_test(k, st);
+  pstamp(24, double(lt.stop) + double(m0) + double(K));
   if (!replay && threadIdx.x == 0) pend3_load(k, st, m0, K0, pend);
   Coef3 cf;
   Scal3 sc = {};
@@ -1016,6 +1029,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     }
     // 3. this sweep's iterations
     sc = sweep3_scalars(k, st, par);
+    pstamp(25, sc.c.a[2] + sc.c.b[2] + sc.g[2]);
     if (sc.m == 0 && !sc.first) {  // iteration K+1 breaks down before its update
       finish(m0, K + 1, sc.bad ? 4 : 2);
       return;

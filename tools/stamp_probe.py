@@ -43,7 +43,7 @@ def step_timeline(steps: np.ndarray, three: bool = False) -> str:
     out = ["  first-item timeline (median us after item start, n waves; per-group increment):"]
     prev = None
     for c in range(1, 32):
-        if three and c >= 28 and c <= 30:  # (slots 28/29: shader clock, 30: the wave's hardware id)
+        if three and c >= 24 and c <= 30:  # (24-27: prologue points, 28/29: shader clock, 30: hardware id)
             continue
         v = s[:, c]
         ok = v > 0
@@ -74,6 +74,11 @@ def grid_timeline(glob: np.ndarray, steps: np.ndarray, wv_all: np.ndarray) -> st
     if g[0] > 0:
         out.append(f"    gap after the previous launch's finalize: {(t0 - g[0]) / 100.0:7.2f}")
     out.append(f"    wave kernel entry: median {np.median(ent - t0) / 100.0:6.2f}  max {(ent.max() - t0) / 100.0:6.2f}")
+    for slot, nm in ((24, "state read, stop tests decided"), (25, "step scalars formed")):
+        v = s[:, slot][s[:, slot] > 0]
+        if len(v):
+            out.append(f"    {nm}: median {np.median(v - t0) / 100.0:6.2f}  (after the wave's own entry: "
+                       f"{np.median((s[:, slot] - s[:, 1])[s[:, slot] > 0]) / 100.0:5.2f})")
     out.append(f"    walk entry (scalars + ring): median {np.median(wv[:, 0] - t0) / 100.0:6.2f}")
     out.append(f"    first item start: median {np.median(first_items - t0) / 100.0:6.2f}")
     out.append(f"    last wave exit {(wv[:, 1].max() - t0) / 100.0:7.2f}; grid reduction start {(g[1] - t0) / 100.0:7.2f}; "
