@@ -124,12 +124,49 @@ __device__ __forceinline__ double mform(const double (&xz)[3], const double (&xp
   return s;
 }
 
+// The state a launch's prologue reads, loaded in one batch at kernel entry:
+// plain loads in straight-line code, so every one is in flight before the
+// first wait (the stop tests, the breakdown / cap checks and the scalar
+// algebra each waited for their own loads — several serial round trips to
+// memory in front of every wave's first item).
+struct St3 {
+  long long iter, brk3, k0;
+  int done, late3, wpar, started, bad3;
+  double gprev;
+  double n2[2][3];  // fs2[0 / 1][16 + i]: the last sweep's ‖p_i‖² (either parity)
+  double sc[12];    // sc3[0 .. 11]: that sweep's {zc, α, β, g}
+  double R[16];     // fs2[par ^ 1][0 .. 15]: its moment sums
+};
+__device__ __forceinline__ St3 st3_load(const DevState* st, int par) {
+  St3 S;
+  S.done = st->done;
+  S.iter = st->iter;
+  S.late3 = st->late3;
+  S.wpar = st->wpar;
+  S.started = st->started;
+  S.bad3 = st->bad3;
+  S.brk3 = st->brk3;
+  S.k0 = st->k0;
+  S.gprev = st->gprev;
+#pragma unroll
+  for (int i = 0; i < 3; ++i) {
+    S.n2[0][i] = st->fs2[0][16 + i];
+    S.n2[1][i] = st->fs2[1][16 + i];
+  }
+#pragma unroll
+  for (int i = 0; i < 12; ++i) S.sc[i] = st->sc3[i];
+  const double* R = st->fs2[par ^ 1];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) S.R[i] = R[i];
+  return S;
+}
+
 // From the previous sweep's 19 unweighted sums (a pure function of the state:
 // every wave evaluates it and gets the same bits).
-__device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState* st, int par) {
+__device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const St3& st, int par) {
   Scal3 c;
-  c.first = st->started == 0;
-  c.K = st->iter;
+  c.first = st.started == 0;
+  c.K = st.iter;
   c.m = 0;
   c.brk = 0;
   c.bad = false;
@@ -143,7 +180,7 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
   }
   if (c.first) return c;
   const double hh = k.h1 * k.h2;
-  const double* R = st->fs2[par ^ 1];
+  const double* R = st.R;
   const double mzz[6] = {R[0], R[1], R[2], R[3], R[4], R[5]};
   const double mzp[6] = {0.0, R[6], R[7], R[8], R[9], R[10]};
   const double mpp[6] = {0.0, R[11], R[12], R[13], R[14], R[15]};
@@ -153,12 +190,12 @@ __device__ __forceinline__ Scal3 sweep3_scalars(const KParams& k, const DevState
   double zz[3] = {1.0, 0.0, 0.0}, zp[3] = {0.0, 0.0, 0.0};  // z_{i-1}
   double pz[3] = {0.0, 0.0, 0.0}, pp[3] = {1.0, 0.0, 0.0};  // p_{i-1}
   double g = mform(zz, zp, mzz, mzp, mpp, 0) * hh;
-  double gprev = st->gprev;
+  double gprev = st.gprev;
   bool live = true;  // (fully unrolled, no early exit: the arrays stay in registers)
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     live = live && i < lim;
-    const double beta = c.K + i == st->k0 ? 0.0 : g / gprev;  // (k0: 0, or a restart's iteration)
+    const double beta = c.K + i == st.k0 ? 0.0 : g / gprev;  // (k0: 0, or a restart's iteration)
 #pragma unroll
     for (int q = 0; q < 3; ++q) {
       pz[q] = zz[q] + beta * pz[q];
@@ -216,9 +253,15 @@ __device__ __forceinline__ double late_diff(const KParams& k, const DevState* st
   return k.weighted ? fabs(a) * sqrt(n2 * hh) : fabs(a) * sqrt(n2);
 }
 
-__device__ __forceinline__ Late3 late3_test(const KParams& k, const DevState* st) {
+__device__ __forceinline__ double late_diff(const KParams& k, const St3& st, int i) {
+  const double n2 = fmax(st.wpar ? st.n2[1][i] : st.n2[0][i], 0.0), a = st.sc[3 + i];
+  const double hh = k.h1 * k.h2;
+  return k.weighted ? fabs(a) * sqrt(n2 * hh) : fabs(a) * sqrt(n2);
+}
+
+__device__ __forceinline__ Late3 late3_test(const KParams& k, const St3& st) {
   Late3 r{0, 0};
-  const int m = st->late3;
+  const int m = st.late3;
 #pragma unroll
   for (int i = 0; i < 3; ++i) {
     if (r.stop == 0 && i < m) {
@@ -275,16 +318,16 @@ struct Pend3 {
   long long K0;
   int n;
 };
-__device__ __forceinline__ void pend3_load(const KParams& k, const DevState* st, int m0, long long K0, Pend3& p) {
+__device__ __forceinline__ void pend3_load(const KParams& k, const St3& st, int m0, long long K0, Pend3& p) {
   p.K0 = K0;
   p.n = m0;
 #pragma unroll
   for (int i = 0; i < 3; ++i)
     if (i < m0) {
       p.d[i] = late_diff(k, st, i);
-      p.a[i] = st->sc3[3 + i];
-      p.b[i] = st->sc3[6 + i];
-      p.g[i] = st->sc3[9 + i];
+      p.a[i] = st.sc[3 + i];
+      p.b[i] = st.sc[6 + i];
+      p.g[i] = st.sc[9 + i];
     }
 }
 __device__ __forceinline__ void pend3_record(const KParams& k, DevState* st, const Pend3& p) {
@@ -918,7 +961,8 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
 template <bool PUSH, int MODE = kPlain>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS3(KParams k, int par) {
   DevState* st = k.st;
-  const int done = st->done;
+  const St3 S = st3_load(st, par);  // (replay: only done is used from it)
+  const int done = S.done;
   __shared__ double sm[4 * NS];
   __shared__ int sflag;
   __shared__ WaveTV3 tvs[kWPB];
@@ -954,8 +998,8 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
 #pragma unroll
   for (int n = 0; n < NS; ++n) acc[n] = 0.0;
   // 1. the previous sweep's pending stop tests
-  const int m0 = st->late3;
-  const long long K = st->iter, K0 = K - m0;
+  const int m0 = S.late3;
+  const long long K = S.iter, K0 = K - m0;
   // (kStamp: prologue points into the wave's step-stamp slots 24-27 — state
   // read and the stop tests decided / scalars formed / walk entered)
   auto pstamp = [&](int slot, double dep) {
@@ -968,9 +1012,9 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
       }
     }
   };
-  const Late3 lt = late3_test(k, st);
+  const Late3 lt = late3_test(k, S);
   pstamp(24, double(lt.stop) + double(m0) + double(K));
-  if (!replay && threadIdx.x == 0) pend3_load(k, st, m0, K0, pend);
+  if (!replay && threadIdx.x == 0) pend3_load(k, S, m0, K0, pend);
   Coef3 cf;
   Scal3 sc = {};
   bool fix = false;
@@ -1002,17 +1046,17 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     // inlined copy of the marches costs the whole register budget)
 #pragma unroll
     for (int i = 0; i < 3; ++i) {
-      cf.zc[i] = st->sc3[i];
-      cf.a[i] = st->sc3[3 + i];
-      cf.b[i] = st->sc3[6 + i];
-      cf.cw[i] = (i >= lt.stop && i < m0) ? -st->sc3[3 + i] : 0.0;
+      cf.zc[i] = S.sc[i];
+      cf.a[i] = S.sc[3 + i];
+      cf.b[i] = S.sc[6 + i];
+      cf.cw[i] = (i >= lt.stop && i < m0) ? -S.sc[3 + i] : 0.0;
     }
     fix = true;
-    rpar = st->wpar;
+    rpar = S.wpar;
   } else {
     // 2. the breakdown / cap that sweep saw coming
-    if (st->brk3) {
-      finish(m0, st->brk3, st->bad3 ? 4 : 2);
+    if (S.brk3) {
+      finish(m0, S.brk3, S.bad3 ? 4 : 2);
       return;
     }
     if (m0 > 0 && K >= k.max_iter) {
@@ -1028,7 +1072,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
       return;
     }
     // 3. this sweep's iterations
-    sc = sweep3_scalars(k, st, par);
+    sc = sweep3_scalars(k, S, par);
     pstamp(25, sc.c.a[2] + sc.c.b[2] + sc.g[2]);
     if (sc.m == 0 && !sc.first) {  // iteration K+1 breaks down before its update
       finish(m0, K + 1, sc.bad ? 4 : 2);
