@@ -287,6 +287,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // 2048² / 1600×2400 +2-7 % (20.2 vs 18.9 µs per iteration), 8192² −4-6 %
   // it/s, the 8-rank slab and 4×2 blocks neutral — profiles/r5_prio.txt
   k.prio = std::getenv("PE_PRIO") ? std::max(0, std::min(20, std::atoi(std::getenv("PE_PRIO")))) : 0;
+  k.stage = !(std::getenv("PE_STAGE") && std::atoi(std::getenv("PE_STAGE")) == 0);
   k.xorg = xorg_;
   k.nx = nx;
   k.ny = ny;

@@ -426,6 +426,7 @@ struct M3Rings {
 struct Pre3 {
   int2 e;  // (rows field 0: no item)
   int4 rc4;
+  bool staged;  // its first r / p / w rows were sent into the wave's LDS (stage_first3)
 };
 
 template <bool STEADY>
@@ -775,15 +776,29 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
   M3Rings x;
   x.pushed = false;
   constexpr int XD = kS3XD, WD = kS3WD;
+  static_assert(WD <= 6, "the first WD w rows are all row ib (t0 - 2 + q < ib)");
+  if (use_pre && pre.staged && KIND != kBand) {  // (stage_first3: rows t0 .. t0+XD-1 ≤ tmax, w row ib)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const double* L = &tvw.a0r[0][0];
 #pragma unroll
-  for (int q = 0; q < XD; ++q) {
-    const int t = min(c.t0 + q, c.tmax);
-    x.RQ[q] = ldx3<PUSH>(k, c, t, c.off);
-    x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off);
+    for (int q = 0; q < XD; ++q) {
+      x.RQ[q] = L[q * 128 + lane];
+      x.PQ[q] = L[q * 128 + 64 + lane];
+    }
+    const double w0 = L[XD * 128 + lane];
+#pragma unroll
+    for (int q = 0; q < WD; ++q) x.WQ[q] = c.o0 ? w0 : 0.0;
+  } else {
+#pragma unroll
+    for (int q = 0; q < XD; ++q) {
+      const int t = min(c.t0 + q, c.tmax);
+      x.RQ[q] = ldx3<PUSH>(k, c, t, c.off);
+      x.PQ[q] = ldx3<PUSH>(k, c, t, unsigned(c.poff) + c.off);
+    }
+#pragma unroll
+    for (int q = 0; q < WD; ++q)
+      x.WQ[q] = c.o0 ? ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off) : 0.0;
   }
-#pragma unroll
-  for (int q = 0; q < WD; ++q)
-    x.WQ[q] = c.o0 ? ldnt1(c.Wm + int64_t(min(max(c.t0 - 2 + q, ib), ie)) * c.wp + c.off) : 0.0;
 #pragma unroll
   for (int q = 0; q < 3; ++q) x.P1[q] = x.P2[q] = x.P3[q] = x.Z[q] = x.U[q] = x.V[q] = x.UU[q] = x.VV[q] = 0.0;
 #pragma unroll
@@ -850,6 +865,45 @@ __device__ __forceinline__ void pre_load3(const KParams& k, int gwave, Pre3& pr)
   pr.rc4 = rowcls_entry(k, ib - H3, ie + H3 + 1);
 }
 
+// The first item's first rows — r / p rows t0 .. t0+XD-1 and its w row ib —
+// sent straight into the wave's LDS by LDS-DMA (global_load_lds: no VGPRs,
+// so nothing is live across the walk loop) at kernel entry, where their DRAM
+// latency overlaps the three iterations' scalar algebra instead of following
+// it; march3 reads them from there (use_pre && staged).  The LDS is the band
+// face ring's a0r (3.5 KB), free until the wave's first band item zeroes it:
+// only items that are not band items are staged, and only rows of x itself
+// (PUSH: not the receive buffer's halo rows).  PE_STAGE=0: off.
+template <bool PUSH>
+__device__ __forceinline__ void stage_first3(const KParams& k, int par, WaveTV3& tv, Pre3& pr) {
+  pr.staged = false;
+  const int rows = pr.e.y >> 20;
+  if (rows == 0 || !k.stage || (pr.e.x & kBandBit)) return;
+  const int sx = pr.e.y & 0xFFFFF, ib = pr.e.x & kRowMask3;
+  const int t0 = ib - H3;
+  if (PUSH && (t0 < 1 || t0 + kS3XD - 1 > int(k.nx))) return;
+  typedef __attribute__((address_space(3))) void* lds_ptr;
+  typedef __attribute__((address_space(1))) const void* g_ptr;
+  const int lane = threadIdx.x & 63;
+  const double* Xm = k.x[par ^ 1] - (HL3 - 1) + sx * FSW3;  // the strip's element 0 (march3: c.Xm + c.J + HL3 - 1)
+  const double* Wm = k.w - (HL3 - 1) + sx * FSW3;
+  double* L = &tv.a0r[0][0];  // [q][r 64 | p 64] for q < XD, then [w 64]
+#pragma unroll
+  for (int q = 0; q < kS3XD; ++q) {
+    const char* rr = reinterpret_cast<const char*>(Xm + int64_t(t0 + q) * k.pitch);
+    const char* pp = reinterpret_cast<const char*>(Xm + int64_t(t0 + q) * k.pitch + k.poff);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {  // 4 bytes per lane: two instructions per 512-B row
+      __builtin_amdgcn_global_load_lds((g_ptr)(rr + 256 * h + 4 * lane), (lds_ptr)(L + q * 128 + 32 * h), 4, 0, 0);
+      __builtin_amdgcn_global_load_lds((g_ptr)(pp + 256 * h + 4 * lane), (lds_ptr)(L + q * 128 + 64 + 32 * h), 4, 0, 0);
+    }
+  }
+  const char* wr = reinterpret_cast<const char*>(Wm + int64_t(ib) * k.wpitch);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+    __builtin_amdgcn_global_load_lds((g_ptr)(wr + 256 * h + 4 * lane), (lds_ptr)(L + kS3XD * 128 + 32 * h), 4, 0, 0);
+  pr.staged = true;
+}
+
 __device__ __forceinline__ Coef3 uni3(const Coef3& c) {
   Coef3 u;
 #pragma unroll
@@ -911,6 +965,7 @@ __device__ __forceinline__ void walk3(const KParams& k, const Coef3& cf, bool fi
       // b0 and the slots garbage pipeline-fill rows read stay finite) — before
       // each band item, not in every wave's launch prologue
       if (!ring_zeroed) {
+        if (have_pre && pre.staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (a0r: the staged rows' LDS)
         const int ln = threadIdx.x & 63;
         for (int i = ln; i < kRing3 * 64; i += 64) (&tv.a0r[0][0])[i] = 0.0;
         for (int i = ln; i < kRing3 * 66; i += 64) (&tv.b0r[0][0])[i] = 0.0;
@@ -985,7 +1040,12 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   // the first item's loads, before the state reads (PE_PRE=0 at construction: off)
   Pre3 pre;
   const bool use_pre = !replay && k.pre_load;
-  if (use_pre) pre_load3(k, int(blockIdx.x) * kWPB + wid, pre);
+  if (use_pre) {
+    pre_load3(k, int(blockIdx.x) * kWPB + wid, pre);
+    stage_first3<PUSH>(k, par, tvs[wid], pre);
+  } else {
+    pre.staged = false;
+  }
   // terminal paths: every wave has read the state before the last one to
   // arrive writes it
   auto finish = [&](int upto, long long iter, int status, int fixj = 0) {

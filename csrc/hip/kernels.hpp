@@ -213,6 +213,9 @@ struct KParams {
   // 2^prio × 10 ns; ncu: workgroups ≥ ncu are the second ones on their CU
   int prio;
   int ncu;
+  // three-step sweep: stage each wave's first item's first rows into LDS at
+  // kernel entry (fused3.hip stage_first3; PE_STAGE=0: off)
+  int stage;
 };
 constexpr int kFoldGroup = 64;
 // KParams::mlimit of the three-step replay launch (DevState::fixj)

@@ -112,7 +112,8 @@ def test_overlap_full_grid_launches(gpu, nat, monkeypatch):
 
 def test_priority_turns_and_wave_map_keep_the_sums(gpu, nat, monkeypatch):
     """SIMD priority turns (PE_PRIO, fused3.hip prio_turn) change only when
-    waves issue: 30 iterations give the same bits with and without them.  A
+    waves issue: 30 iterations give the same bits with and without them, and
+    with and without the first rows staged into LDS (PE_STAGE).  A
     permuted list -> workgroup map (PE_WPERM) groups other items into each
     workgroup's partial sum: the same w to rounding.  2048² on one GPU, fixed
     rows per item (no timing-dependent tuning)."""
@@ -120,6 +121,7 @@ def test_priority_turns_and_wave_map_keep_the_sums(gpu, nat, monkeypatch):
     monkeypatch.setenv("PE_LAYOUT", "equal")
     ws = {}
     for name, env in (("off", {"PE_PRIO": "0"}), ("turns", {"PE_PRIO": "10"}), ("fast", {"PE_PRIO": "7"}),
+                      ("nostage", {"PE_PRIO": "0", "PE_STAGE": "0"}),
                       ("perm", {"PE_PRIO": "0", "PE_WPERM": "1"})):
         for k, v in env.items():
             monkeypatch.setenv(k, v)
@@ -134,7 +136,10 @@ def test_priority_turns_and_wave_map_keep_the_sums(gpu, nat, monkeypatch):
         ws[name] = np.array(s.w())
         del s
         monkeypatch.delenv("PE_WPERM", raising=False)
+        monkeypatch.delenv("PE_STAGE", raising=False)
     scale = np.abs(ws["off"]).max()
     assert scale > 0
     assert np.array_equal(ws["off"], ws["turns"]) and np.array_equal(ws["off"], ws["fast"])
+    # the first rows staged into LDS at kernel entry (default) or loaded by the march (PE_STAGE=0): same bits
+    assert np.array_equal(ws["off"], ws["nostage"])
     assert np.abs(ws["off"] - ws["perm"]).max() <= 1e-9 * scale
