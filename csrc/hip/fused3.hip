@@ -1022,6 +1022,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
   __shared__ int sflag;
   __shared__ WaveTV3 tvs[kWPB];
   __shared__ Pend3 pend;
+  __shared__ Scal3 scl;
   const int lane = int(threadIdx.x & 63);
   const int wid = __builtin_amdgcn_readfirstlane(int(threadIdx.x >> 6));
   constexpr bool replay = MODE == kReplay;
@@ -1139,6 +1140,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
       return;
     }
     cf = sc.c;
+    if (threadIdx.x == 0) scl = sc;  // (the finalize's copy: sc need not live across the walk)
   }
   walk3<PUSH, MODE>(k, uni3(cf), fix, rpar, tvs[wid], wid, acc, pre, use_pre);
   if (k.prio > 0) __builtin_amdgcn_s_setprio(0);
@@ -1183,7 +1185,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(2))) void kS
     }
     if (threadIdx.x == 0) {
       if constexpr (MODE == kStamp) k.stamps2[-4] = rtc3();  // (after the cross-rank sum, if any)
-      sweep3_finalize(k, st, par, sc, t, pend);
+      sweep3_finalize(k, st, par, scl, t, pend);
       __hip_atomic_store(&st->ticket[0], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if constexpr (MODE == kStamp) k.stamps2[-6] = rtc3();  // finalized
     }
