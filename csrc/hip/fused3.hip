@@ -886,7 +886,8 @@ __device__ __forceinline__ void stage_first3(const KParams& k, int par, WaveTV3&
   const int lane = threadIdx.x & 63;
   const double* Xm = k.x[par ^ 1] - (HL3 - 1) + sx * FSW3;  // the strip's element 0 (march3: c.Xm + c.J + HL3 - 1)
   const double* Wm = k.w - (HL3 - 1) + sx * FSW3;
-  double* L = &tv.a0r[0][0];  // [q][r 64 | p 64] for q < XD, then [w 64]
+  static_assert((kS3XD * 128 + 64) * sizeof(double) <= sizeof(tv.a0r) + sizeof(tv.b0r), "staged rows fit the face ring");
+  double* L = &tv.a0r[0][0];  // [q][r 64 | p 64] for q < XD, then [w 64] (a0r, then b0r right after it)
 #pragma unroll
   for (int q = 0; q < kS3XD; ++q) {
     const char* rr = reinterpret_cast<const char*>(Xm + int64_t(t0 + q) * k.pitch);
