@@ -722,6 +722,24 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 // map_peer_buffers (collective) or none does.  PE_HALO=exchange opts out.
 void DeviceSolver::setup_halo_push() {
   push_ = false;
+  // PE_PUSH_LOOPBACK=1 (diagnostic, tools/block_probe.py on one GPU): the
+  // push kernel's work without peers — every push lands in this rank's own
+  // receive buffer and the halo rows are read back from it (wrong values,
+  // the real stores and loads), so a row slab's per-rank time includes what
+  // the 8-GPU job's push kernel does
+  if (const char* e = std::getenv("PE_PUSH_LOOPBACK");
+      e && std::atoi(e) == 1 && comm_->size() > 1 && fused_ && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= 2 * hdep_) {
+    const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);
+    void* buf = nullptr;
+    PE_HIP_CHECK(hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained));
+    PE_HIP_CHECK(hipMemsetAsync(buf, 0, bytes, stream_));
+    PE_HIP_CHECK(hipDeviceSynchronize());
+    hrecv_ = static_cast<double*>(buf);
+    hpeers_.assign(size_t(comm_->size()), buf);
+    push_ = true;
+    push_status_ = "loopback (diagnostic)";
+    return;
+  }
   push_status_ = comm_->size() < 2 ? "off: one rank" : !fused_ ? "off: classic path" : !comm_->peer_sum()
                  ? "off: no P2P transport (" + p2p_setup_status() + ")" : blk_.Py != 1 ? "off: 2-D blocks (RCCL exchange)"
                  : "";

@@ -4,6 +4,7 @@ eager) under a list of kernel configurations.
 
     PROBE_CFG=8:aspect,4:aspect PROBE_ENV="PE_TI=8 PE_ORDER=0;PE_TI=16 PE_ORDER=3" python tools/block_probe.py
     PROBE_RANKS=all (every rank's block in turn; default: rank P//2)
+    PE_PUSH_LOOPBACK=1: row slabs run the halo-push kernel, pushing into their own receive buffer
 """
 import os
 import sys
@@ -41,7 +42,8 @@ for P, spec in configs:
             dt = s.time_iterations(iters, False)
             tune = " ".join(f"{x * 1e3:.1f}" for x in s.ti_tuning_ms)
             print(f"P={P} {g.Px}x{g.Py} rank {rank} block {blk.nx}x{blk.ny} [{env or 'default'}]: {dt / iters * 1e6:7.1f} us/iter "
-                  f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)  ti {s.ti}" + (f"  tuning us/sweep [{tune}]" if tune else ""),
+                  f"({blk.nx * blk.ny / (dt / iters) / 1e9:6.2f} Gpt/s)  ti {s.ti}" + (f"  tuning us/sweep [{tune}]" if tune else "")
+                  + (f"  push {s.push_status}" if os.environ.get("PE_PUSH_LOOPBACK") == "1" else ""),
                   flush=True)
             del s, comm
             for k, v in saved.items():
