@@ -914,11 +914,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       }
     }
     if constexpr (PUSH) {
-      if (pushed) {  // delivered before this wave arrives anywhere
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
+      if (pushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (system-scope atomic stores: fused3.hip march3)
     }
     if (persum) {
       // per-item sums (wave-reduced) in a fixed slot: the reduction kernel

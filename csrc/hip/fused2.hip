@@ -437,11 +437,7 @@ __device__ __forceinline__ void march(const KParams& k, const Scal2& sc, int par
     }
   }
   if constexpr (PUSH) {
-    if (pushed) {  // delivered before this wave arrives anywhere
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (pushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (system-scope atomic stores: fused3.hip march3)
   }
 }
 

@@ -845,11 +845,15 @@ __device__ __forceinline__ void march3(const KParams& k, const Coef3& cf, bool f
     }
   }
   if constexpr (PUSH) {
-    if (x.pushed) {  // delivered before this wave arrives anywhere
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // The pushed rows went out as system-scope atomic stores (sc0 sc1: write-
+    // through to the neighbour's fine-grained buffer), so their completion is
+    // their delivery: drained here, before this wave's ticket, and the last
+    // block's flags (peer_sum_block's own release) follow them.  A system-
+    // scope release fence here also wrote the XCD's whole L2 back
+    // (buffer_wbl2) once per pushing item — 2 × 171 of them per sweep at the
+    // 8-rank slab of 8192²: 70 → 65 µs per iteration with the push kernel
+    // (PE_PUSH_LOOPBACK, profiles/r5_push_release.txt).
+    if (x.pushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
 }
 

@@ -694,11 +694,7 @@ __device__ __forceinline__ void marchS(const KParams& k, const CoefS<S>& cf, boo
     }
   }
   if constexpr (PUSH) {
-    if (x.pushed) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    if (x.pushed) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (system-scope atomic stores: fused3.hip march3)
   }
 }
 
