@@ -207,11 +207,16 @@ void DeviceSolver::setup_items() {
   // outputs a neighbour needs: first in the layout under the overlap (they
   // feed the exchange) and under the halo push (their xGMI stores then
   // overlap the rest of the sweep instead of ending it)
+  // The halo push keeps the plain layout: cutting its boundary pieces off and
+  // dealing them first (PE_PUSH_FIRST=1, the earlier default) cost the push
+  // kernel 10 % at the 8-rank slab of 8192² (64.6-65.1 vs 58.2 µs per
+  // iteration) and 4 % at 4 ranks, loopback probe, profiles/r5_push_release.txt
+  const bool push_first = push_ && std::getenv("PE_PUSH_FIRST") && std::atoi(std::getenv("PE_PUSH_FIRST")) == 1;
   auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t jlo = std::max<int64_t>(1, J + HL), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + HL - 1);
     // (the H owned rows / columns next to a neighbour: what the exchange sends)
-    return ((overlap_ && !(ov_debug_ & 4)) || push_) &&
+    return ((overlap_ && !(ov_debug_ & 4)) || push_first) &&
            ((blk_.has(LEFT) && ib <= H) || (blk_.has(RIGHT) && ie >= blk_.nx - H + 1) || (blk_.has(DOWN) && jlo <= H) ||
             (blk_.has(UP) && jhi >= blk_.ny - H + 1));
   };
@@ -442,7 +447,7 @@ void DeviceSolver::setup_items() {
           const int kq = q <= nx ? kind(q) : -1;
           // (pieces: also split where a neighbour's halo rows begin, so the push /
           // overlap boundary pieces stay small)
-          const bool cut_b = (push_ || overlap_) && ((blk_.has(LEFT) && q == H + 1) || (blk_.has(RIGHT) && q == nx - H + 1));
+          const bool cut_b = (push_first || overlap_) && ((blk_.has(LEFT) && q == H + 1) || (blk_.has(RIGHT) && q == nx - H + 1));
           if (kq != ka || cut_b) {
             segs.push_back(Seg{a, q - a, sx, ka == 2 ? fband : ka == 1 ? fmixed : 1.0, false, 1});
             a = q;
