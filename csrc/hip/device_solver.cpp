@@ -748,8 +748,14 @@ void DeviceSolver::setup_halo_push() {
   if ((prob_.M - 1) / blk_.Px < 2 * hdep_) return;  // edge rows 1..h and nx-h+1..nx distinct
   push_status_ = "off: PE_XR=0";
   if (const char* e = std::getenv("PE_XR"); e && std::atoi(e) == 0) return;
-  push_status_ = "off: PE_HALO=exchange";
-  if (const char* e = std::getenv("PE_HALO"); e && std::string(e) == "exchange") return;
+  // Opt-in since round 5 (PE_HALO=push): timed on one GPU (PE_PUSH_LOOPBACK)
+  // the push kernel's per-rank iteration is 58 µs at the 8-rank slab of 8192²
+  // and 109 at 4 ranks, against 45-47 / 79-81 for the plain sweep with the
+  // exchange at 15 / 8 µs exchange / sum delays per sweep (overlapped or not;
+  // profiles/r5_push_release.txt): the push kernel's register pressure and
+  // uncached halo traffic cost more than the exchange it saves
+  push_status_ = "off: exchange (PE_HALO=push pushes from the sweep)";
+  if (const char* e = std::getenv("PE_HALO"); !(e && std::string(e) == "push")) return;
   push_status_ = "fallback: the receive buffers could not be mapped on every rank";
   const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);  // [parity][side][hdep rows]
   void* buf = nullptr;

@@ -414,7 +414,7 @@ def test_halo_push_selftest_failure_falls_back(gpu):
     makes every rank keep the exchange: the job still solves correctly."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60",
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push",
                PE_FAULT_INJECT="pushtest@rank:1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
            "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
@@ -458,7 +458,7 @@ def test_halo_push_checkpoint_resume_bitwise(gpu, tmp_path):
     ends bitwise where the uninterrupted one does."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push")
     ck = str(tmp_path / "ck")
 
     def run(*extra):
@@ -491,7 +491,7 @@ def test_bench_halo_push_graphs(gpu, nproc):
 
     M = N = 1024
     one = solve(EllipseProblem(M, N), backend="hip")
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc), "--steps", "40", "--warmup", "4", "--grid", str(M), str(N), "--decomp", "rows",
@@ -516,7 +516,7 @@ def test_bench_reports_transport_fallbacks(gpu, fault):
     the set-up outcome and the transport the sweep finally uses."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_FAULT_INJECT=fault)
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push", PE_FAULT_INJECT=fault)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3",
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", "3", "--steps", "12", "--warmup", "3", "--grid", "400", "600", "--decomp", "rows",
@@ -597,7 +597,7 @@ def test_slow_rank_shows_in_tmpi(gpu):
     from conftest import free_port
 
     def run(fault):
-        env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60")
+        env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push")
         if fault:
             env["PE_FAULT_INJECT"] = fault
         cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",

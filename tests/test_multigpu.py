@@ -131,12 +131,13 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     c = d["config"]
     assert c["decomposition"]["Px"] * c["decomposition"]["Py"] == nproc
     assert "rccl" in c["transport"]
-    # 2047 rows: slabs while every rank keeps >= 32 rows (decomp.cpp: every N here) → the
-    # halo is pushed by the sweep and the iterations run as captured graphs
-    assert c["halo"].startswith("in-sweep xGMI push") == (c["decomposition"]["Py"] == 1)
+    # 2047 rows: slabs while every rank keeps >= 32 rows (decomp.cpp: every N here); the
+    # halo is exchanged (the sweep pushes it only with PE_HALO=push, round 5)
+    assert c["halo"].startswith("exchange")
     for r in c["ranks"]:  # per-rank diagnostics of the first cross-device run
         assert r["p2p_sum_setup"] == "ok" and r["sums"] == "in-sweep P2P over xGMI"
-        assert r["halo_push"] == ("on" if c["decomposition"]["Py"] == 1 else "off: 2-D blocks (RCCL exchange)")
+        assert r["halo_push"] == ("off: exchange (PE_HALO=push pushes from the sweep)" if c["decomposition"]["Py"] == 1
+                                  else "off: 2-D blocks (RCCL exchange)")
         assert all(v == 1 for k, v in r["peer_access"].items() if int(k) != r["rank"])
 
 

@@ -105,7 +105,7 @@ def test_16384_residual_gap(gpu):
     assert rep.restarts == 0 and 0 <= rep.res_gap < GAP
 
 
-@pytest.mark.parametrize("nproc,decomp,extra", [(3, "rows", {}), (4, "2x2", {"PE_OVERLAP": "1"})])
+@pytest.mark.parametrize("nproc,decomp,extra", [(3, "rows", {"PE_HALO": "push"}), (4, "2x2", {"PE_OVERLAP": "1"})])
 def test_drift_fault_restarts_multi_rank(gpu, tmp_path, nproc, decomp, extra):
     """the residual replacement across ranks.  Row slabs restart
     with the in-sweep halo push and P2P sums (the replay launch pushes rows
