@@ -19,11 +19,12 @@ ex_us = float(sys.argv[1]) if len(sys.argv) > 1 else 20.0
 ar_us = float(sys.argv[2]) if len(sys.argv) > 2 else 12.0
 graph = os.environ.get("PROBE_GRAPH", "1") == "1"
 configs = [(int(c.split(":")[0]), c.split(":")[1]) for c in os.environ.get("PROBE_CFG", "2:aspect,4:aspect,8:aspect,8:rows").split(",")]
-prob = pe.EllipseProblem(8192, 8192)
+GM, GN = (int(v) for v in os.environ.get("PROBE_GRID", "8192x8192").split("x"))
+prob = pe.EllipseProblem(GM, GN)
 for P, spec in configs:
-    g = D.grid(P, 8192, 8192, spec)
+    g = D.grid(P, GM, GN, spec)
     rank = P // 2
-    blk = nat.decompose(8192, 8192, g, rank)
+    blk = nat.decompose(GM, GN, g, rank)
     for delays in [(0.0, 0.0), (ex_us, ar_us)]:
         for ov in os.environ.get("PROBE_OV", "0,1:8").split(","):
             os.environ["PE_OVERLAP"] = ov.split(":")[0]
