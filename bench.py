@@ -18,9 +18,11 @@ stage4-mpi+cuda/poisson_mpi_cuda2.cu:986-990).
 
 A *step* is one full PCG iteration of the global solve on N GPUs (the
 three-step sweep advances three per launch, its 19 sums summed over ranks
-inside the sweep over xGMI P2P, and the halo rows — row-slab blocks — pushed
-by the same sweep into the neighbours' receive buffers, or exchanged through
-RCCL otherwise; K steps with 3 ∤ K end with a partial sweep).  The
+inside the sweep over xGMI P2P; the halo path — the comm's RCCL exchange,
+the peer-put kernel or the sweep's own push, with or without the
+halo/interior overlap — is the one the solver's construction timed fastest
+on this job's transport, reported as `halo_path` with every candidate's
+time; K steps with 3 ∤ K end with a partial sweep).  The
 timed region runs exactly K steps from the start of a fresh solve (w⁰ = 0, as
 the reference) with the convergence test switched off so every step does full
 work; it is bracketed by a barrier + device synchronise on both sides and the
@@ -75,7 +77,9 @@ def parse_args(argv):
     ap.add_argument("--no-random-solve", action="store_true", help="skip the (untimed) random-init solve")
     ap.add_argument("--seed", type=int, default=1234, help="random-init w0 seed")
     ap.add_argument("--variant", type=int, default=0)
-    ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused", "two-step", "three-step", "four-step"))
+    ap.add_argument("--algo", default="auto", choices=("auto", "classic", "fused", "two-step", "three-step"),
+                    help="sweep kernel (auto: three-step beyond the LDS-resident kernel's blocks); two-step runs "
+                         "whole two-iteration sweeps only, so it needs an even --steps")
     # eager by default: a 20-step window launched eagerly took 5.29-5.41 ms
     # against 5.30-5.85 ms replayed from its chunk graph (the first replay of
     # a window sometimes paid ~0.5 ms more: profiles/r3_window.txt)
@@ -193,7 +197,7 @@ def main(argv=None) -> int:
     opt = nat.SolveOptions()
     opt.check_tol = False  # fixed work per step in the timed region
     opt.variant = a.variant
-    opt.algo = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4, "four-step": 5}[a.algo]
+    opt.algo = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4}[a.algo]
     solver = nat.DeviceSolver(P, blk, comm, opt)
 
     def barrier():
@@ -230,7 +234,8 @@ def main(argv=None) -> int:
           # transport set-up decided and what the sweep finally uses
           "neighbors": {d: int(blk.nbr[i]) for i, d in enumerate(("left", "right", "down", "up")) if blk.nbr[i] >= 0},
           "peer_access": {str(r): int(v) for r, v in enumerate(solver.peer_access)},
-          "p2p_sum_setup": nat.p2p_setup_status(), "halo_push": solver.push_status, "sums": solver.xr_status}
+          "p2p_sum_setup": nat.p2p_setup_status(), "halo_push": solver.push_status, "halo_put": solver.put_status,
+          "sums": solver.xr_status}
     ranks_info = gather(me)
 
     # warmup: first-touch / RCCL connections, then (--launch graph)
@@ -335,11 +340,9 @@ def main(argv=None) -> int:
             "unknowns": (M - 1) * (N - 1),
             "global_batch": 1,
             "seq_len": None,
-            "parallelism": (f"2d-decomp {blk.Px}x{blk.Py} "
-                            + ("(xGMI halo push + P2P sums)" if solver.halo_push else "(RCCL halo)"))
-            if world > 1 else "single-gpu",
+            "parallelism": f"2d-decomp {blk.Px}x{blk.Py} (halo: {solver.halo_path})" if world > 1 else "single-gpu",
             "points_per_s": ips * (M - 1) * (N - 1),
-            "algo": (f"{['', '', 'two', 'three', 'four'][solver.sweep_steps]}-step sweep (1 kernel + 1 reduction per "
+            "algo": (f"{['', '', 'two', 'three'][solver.sweep_steps]}-step sweep (1 kernel + 1 reduction per "
                      f"{solver.sweep_steps} iterations)" if solver.two_step else
                      "single-sweep (1 kernel, 1 allreduce / iter)" if solver.fused else
                      "classic (2 kernels, 2 allreduces / iter)"),
@@ -349,12 +352,19 @@ def main(argv=None) -> int:
             "distinct_gpus": len(pcis),
             "ranks": ranks_info,
             "allreduce": ("in-sweep P2P over xGMI" if solver.xr else "launch per iteration") if world > 1 else "none",
-            "halo": ("in-sweep xGMI push" + (" (graph-captured)" if use_graph else "") if solver.halo_push else
+            "halo": ("in-sweep xGMI push" + (" (graph-captured)" if use_graph and solver.graphs_usable else "")
+                     if solver.halo_push else
+                     "peer put over xGMI (kPut)" + (" (graph-captured)" if use_graph and solver.graphs_usable else "")
+                     if solver.halo_put else
                      ("exchange: " + comm.name)) if world > 1 else "none",
             "overlap": bool(solver.overlap),
+            # the construction's halo-path choice: every candidate's us per sweep (max over ranks; the two
+            # fastest timed twice) and the pick
+            "halo_path": solver.halo_path,
+            "halo_candidates_us_per_sweep": [[n, round(us, 2)] for n, us in solver.halo_candidates],
             "exchange_us_measured": round(solver.exchange_us, 2),
             "item_order": "dynamic per-XCD queue" if solver.order == 3 else f"static {solver.layout_name} layout",
-            "rows_per_item": "segments (one per wave)" if solver.segment_layout else solver.ti,
+            "rows_per_item": solver.ti,
             # (a negative entry: another static layout tried at that height)
             "rows_per_item_candidates": list(solver.ti_tuning_rows),
             "rows_per_item_tuning_ms": [round(x, 4) for x in solver.ti_tuning_ms],

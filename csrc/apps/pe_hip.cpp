@@ -2,7 +2,7 @@
 // MI355X: one process per GPU, RCCL over xGMI, device-resident PCG.
 //
 //   pe_hip [--tol 1e-6] [--max-iter K] [--decomp device|aspect|reference|rows|cols|PxxPy]
-//          [--init zero|random] [--seed S] [--variant 0|1] [--algo auto|classic|fused|two-step|three-step|four-step] [--chunk K]
+//          [--init zero|random] [--seed S] [--variant 0|1] [--algo auto|classic|fused|two-step|three-step] [--chunk K]
 //          [--graph] [--timing] [--vranks P] [--json] [M N]
 //
 // Multi-GPU: `pe_launch -n 8 bin/pe_hip 8192 8192` (or torchrun-style env
@@ -74,7 +74,7 @@ int main(int argc, char** argv) {
   opt.variant = int(args.geti("variant", 0));
   {
     const std::string a = args.get("algo", "auto");
-    opt.algo = a == "classic" ? 1 : a == "fused" ? 2 : a == "two-step" ? 3 : a == "three-step" ? 4 : a == "four-step" ? 5 : 0;
+    opt.algo = a == "classic" ? 1 : a == "fused" ? 2 : a == "two-step" ? 3 : a == "three-step" ? 4 : 0;
   }
   opt.chunk = int(args.geti("chunk", 0));
   opt.use_graph = args.flag("graph") && !args.flag("no-graph");
@@ -124,8 +124,16 @@ int main(int argc, char** argv) {
     {
       std::string pa;
       for (int v : solver->peer_access()) pa += (pa.empty() ? "" : ", ") + std::to_string(v);
+      std::string hc;
+      for (const auto& c : solver->halo_candidates()) {
+        char b[128];
+        std::snprintf(b, sizeof(b), "%s[\"%s\", %.2f]", hc.empty() ? "" : ", ", c.first.c_str(), c.second);
+        hc += b;
+      }
       diag = "\"p2p_sum_setup\": \"" + p2p_setup_status() + "\", \"halo_push\": \"" + solver->push_status() +
-             "\", \"sums\": \"" + solver->xr_status() + "\", \"peer_access\": [" + pa + "]";
+             "\", \"halo_put\": \"" + solver->put_status() + "\", \"halo_path\": \"" + solver->halo_path() +
+             "\", \"halo_candidates_us_per_sweep\": [" + hc + "], \"sums\": \"" + solver->xr_status() +
+             "\", \"peer_access\": [" + pa + "]";
     }
     r = solver->solve();
     const auto t_free = std::chrono::steady_clock::now();

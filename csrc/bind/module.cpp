@@ -449,7 +449,6 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("fused", &DeviceSolver::fused)
       .def_property_readonly("two_step", &DeviceSolver::two_step, "several iterations per sweep (fused2.hip / fused3.hip)")
       .def_property_readonly("sweep_steps", &DeviceSolver::sweep_steps, "iterations per sweep launch (1, 2, 3)")
-      .def_property_readonly("segment_layout", &DeviceSolver::segment_layout)
       .def_property_readonly("resident", &DeviceSolver::resident)
       .def_property_readonly("resident_fallback", &DeviceSolver::resident_fallback)
       .def_property_readonly("layout_cuts", &DeviceSolver::layout_cuts)
@@ -475,6 +474,14 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("overlap", &DeviceSolver::overlap)
       .def_property_readonly("halo_push", &DeviceSolver::halo_push,
                              "halo rows pushed by the sweep over xGMI (no exchange call; graph-capturable)")
+      .def_property_readonly("halo_put", &DeviceSolver::halo_put,
+                             "halo phases exchanged by the peer-put kernel (p2p.hip kPut) instead of the comm")
+      .def_property_readonly("halo_path", &DeviceSolver::halo_path,
+                             "the multi-rank halo path chosen at construction (exchange / put / push [+overlap])")
+      .def_property_readonly("halo_candidates", &DeviceSolver::halo_candidates,
+                             "[(path, µs per sweep)] as timed by the construction's halo-path choice (max over ranks)")
+      .def_property_readonly("graphs_usable", &DeviceSolver::graphs_usable)
+      .def_property_readonly("put_status", &DeviceSolver::put_status, "peer put: available / off: why / fallback: why")
       .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))
       .def_property_readonly("fields_address", &DeviceSolver::fields_address)

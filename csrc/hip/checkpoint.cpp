@@ -108,11 +108,12 @@ void DeviceSolver::load_checkpoint(const std::string& path) {
     // the usual mismatch: a checkpoint of another sweep layout (e.g. one
     // written before the default became the three-step sweep)
     static const char* algo[4] = {"classic", "fused", "two-step", "three-step"};
+    auto name = [](int v) -> std::string { return v >= 0 && v < 4 ? algo[v] : "unknown (steps=" + std::to_string(v) + ")"; };
     const int hf = int(h.fused);
     std::fclose(f);
-    throw std::runtime_error("resume: " + path + " has the " + (hf >= 0 && hf < 4 ? algo[hf] : "?") +
-                             " layout (steps=" + std::to_string(hf) + "), this solver runs " + algo[mine] +
-                             " (steps=" + std::to_string(mine) + "); pass --algo " + (hf >= 0 && hf < 4 ? algo[hf] : "?"));
+    throw std::runtime_error("resume: " + path + " has the " + name(hf) + " layout (steps=" + std::to_string(hf) +
+                             "), this solver runs " + name(mine) + " (steps=" + std::to_string(mine) + "); pass --algo " +
+                             name(hf));
   }
   if (!ok) {
     std::fclose(f);

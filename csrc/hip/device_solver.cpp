@@ -70,6 +70,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     self_ = std::make_unique<SelfDeviceComm>();
     comm_ = self_.get();
   }
+  if (opt_.algo < 0 || opt_.algo > 4)
+    throw std::invalid_argument("algo: 0 auto, 1 classic, 2 fused, 3 two-step, 4 three-step (got " +
+                                std::to_string(opt_.algo) + ")");
   const bool can_fuse = opt_.variant == 0 && fused_possible(prob_, blk_);
   if (opt_.algo >= 2 && !can_fuse)
     throw std::invalid_argument("single-sweep algorithm needs variant 0 and >= 2 rows/columns per split block");
@@ -99,16 +102,11 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     };
     const bool two_ok = fused_ && (single(8) || slabs(8));
     const bool three_ok = fused_ && (single(8) || slabs(12) || grid2d(12) || vgroup(12));
-    // four-step (fused4.hip): an 8-deep halo — 16 rows / columns per block
-    const bool four_ok = fused_ && (single(16) || slabs(16) || grid2d(16) || vgroup(16));
     if (opt_.algo == 3 && !two_ok)
       throw std::invalid_argument("two-step sweep: single-rank blocks of >= 8 x 8 nodes or row slabs of >= 8 rows");
     if (opt_.algo == 4 && !three_ok)
       throw std::invalid_argument(
           "three-step sweep: single-rank blocks of >= 8 x 8 nodes, row slabs of >= 12 rows or 2-D blocks of >= 12 x 12");
-    if (opt_.algo == 5 && !four_ok)
-      throw std::invalid_argument(
-          "four-step sweep: single-rank blocks of >= 16 x 16 nodes, row slabs of >= 16 rows or 2-D blocks of >= 16 x 16");
     // auto: every single-rank block the LDS-resident kernel cannot hold
     // (1x MI355X, fresh processes, T_solver two-step vs single sweep:
     // 1600×2400 0.110 vs 0.127 s, 2048² 0.113 vs 0.133, 4096² 0.378 vs 0.584,
@@ -130,13 +128,12 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     bool auto_ms = slabs(8) || grid2d(12) || vgroup(12) || !resident_likely;
     if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
     int want = 3;
-    if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(4, std::atoi(e)));
+    if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
     steps_ = 1;
     if (opt_.algo == 3) steps_ = 2;
     else if (opt_.algo == 4) steps_ = 3;
-    else if (opt_.algo == 5) steps_ = 4;
     else if (opt_.algo == 0 && auto_ms)
-      steps_ = (want >= 4 && four_ok) ? 4 : (want >= 3 && three_ok) ? 3 : (want >= 2 && two_ok) ? 2 : 1;
+      steps_ = (want >= 3 && three_ok) ? 3 : (want >= 2 && two_ok) ? 2 : 1;
     sstep_ = steps_ > 1;
   }
 
@@ -231,14 +228,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     k.pitch = 2 * plane_;
     k.wpitch = plane_;
     k.poff = plane_;
-    // Plain allocations: shuffling the physical 2-256 MB chunks of the
-    // fields (PE_MALLOC=2) made a fresh process's first allocation fast on
-    // one box and slow on the next (profiles/r2_placement.txt) — the
-    // placement search below is what makes the speed robust.
-    alloc_mode_ = 0;
-    fields_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_, alloc_mode_));
-    xalt_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_, alloc_mode_));
-    walt_ = static_cast<double*>(field_alloc(sizeof(double) * wsize_, alloc_mode_));
+    fields_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_));
+    xalt_ = static_cast<double*>(field_alloc(sizeof(double) * xsize_));
+    walt_ = static_cast<double*>(field_alloc(sizeof(double) * wsize_));
     mark("field allocs");
     set_fused_fields(fields_, xalt_, walt_);
     hsize_ = std::max<int64_t>(1, nx) * 2 * hdep_;  // y strips: hdep columns of r and p per owned row
@@ -507,7 +499,9 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   mark("buffers");
   build_tables(rows_hi, cols_hi);
   mark("tables");
+  if (const char* e = std::getenv("PE_P2P_TIMEOUT_S")) put_timeout_s_ = std::max(0.1, std::atof(e));
   setup_halo_push();
+  setup_halo_put();
   // The placement search times the item layout the solve will run (after
   // setup_items): its best class then reaches the early-stop rate (8192²
   // static layout 0.536-0.545 ms vs 0.564-0.567 for the plain walk), so it
@@ -516,7 +510,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // PE_PLACEMENT_LISTED=0: search with the plain walk, before the layout.
   const bool listed_search = !(std::getenv("PE_PLACEMENT_LISTED") && std::atoi(std::getenv("PE_PLACEMENT_LISTED")) == 0);
   if (fused_ && !listed_search) choose_placement();
-  if (comm_->size() > 1 && !push_) measure_exchange();
+  if (comm_->size() > 1) measure_exchange();  // (diagnostic: the comm's exchange, bench JSON)
   setup_items();
   mark("items");
   if (fused_ && listed_search) choose_placement();
@@ -535,11 +529,6 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // (8-rank 8192² block at 10 rows: busy fraction 0.74-0.78, tools/stamp_probe.py)
     // (candidates: ti_cands above)
     std::vector<int> cands = ti_cands;
-    // (two-step sweep, PE_TI_SEGMENTS=1: also one tall segment per wave — its
-    // 8 pipeline-fill rows re-read once per segment; it lost to the LPT items
-    // on the 2/4/8-rank 8192² slabs, 128 vs 110 µs per sweep at 8 ranks:
-    // profiles/r3_block_probe.txt)
-    if (sstep_ && std::getenv("PE_TI_SEGMENTS") && std::atoi(std::getenv("PE_TI_SEGMENTS")) == 1) cands.push_back(0);
     float best_ms = 0.f;
     int best = ti;
     // one candidate: S_0 + 1 + kTimed local sweeps on real data, the last
@@ -558,9 +547,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       return ms;
     };
     for (int cand : cands) {
-      seg_layout_ = cand == 0;
       const auto tl = clk::now();
-      set_items(cand == 0 ? ti : cand);
+      set_items(cand);
       setup_items();
       const auto tg = clk::now();
       const float ms = time_layout();
@@ -574,7 +562,6 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
         best = cand;
       }
     }
-    seg_layout_ = best == 0;
     // three-step: the other static layouts at the best height
     std::string keep = lay_name_;
     struct Tried {
@@ -584,7 +571,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     };
     std::vector<Tried> tried;
     for (size_t i = 0; i < ti_rows_.size(); ++i) tried.push_back(Tried{ti_rows_[i], lay_name_, ti_ms_[i] * float(kTimed)});
-    if (steps_ >= 3 && best != 0 && !std::getenv("PE_LAYOUT")) {
+    if (steps_ >= 3 && !std::getenv("PE_LAYOUT")) {
       const std::string base = lay_name_;
       for (const char* alt : {"equal", "fill", "lpt"}) {
         if (base == alt) continue;
@@ -606,7 +593,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // candidates were timed slow, and two within ≈2 % swapped places from one
     // process to the next (2400×3200: equal layout at 80 rows or filling at
     // 96, T_iterate 0.099 vs 0.095 s, profiles/r5_prio.txt).  Three-step only.
-    if (steps_ >= 3 && best != 0 && tried.size() >= 2) {
+    if (steps_ >= 3 && tried.size() >= 2) {
       std::stable_sort(tried.begin(), tried.end(), [](const Tried& a, const Tried& b) { return a.ms < b.ms; });
       for (int f = 0; f < 2; ++f) {
         Tried& t = tried[size_t(f)];
@@ -623,7 +610,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       keep = w.lay;
     }
     lay_name_ = keep;
-    set_items(best == 0 ? ti : best);
+    set_items(best);
     setup_items();
   }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
@@ -647,28 +634,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     }
   }
   if (fused_ && comm_->size() > 1 && !comm_->peer_sum()) xr_status_ += "; P2P set-up " + p2p_setup_status();
-  // In-kernel item-sum fold for dynamic sweeps, opt-in (PE_FOLD=1): it saves
-  // the reduction kernel (≈10 µs + a launch gap per iteration at 8192²) but
-  // its per-item publication (drained write-through stores + a returning
-  // counter add) stalls every wave at every item boundary: 1762 / 1734 it/s
-  // vs 1796 / 1752 with kRed, same boxes (profiles/r2_fold.txt).  Counters
-  // are zeroed by enqueue_init.
-  if (fused_ && k.order == 3 && std::getenv("PE_FOLD") && std::atoi(std::getenv("PE_FOLD")) == 1) {
-    const int ng = (nslot_cap_ + dev::kFoldGroup - 1) / dev::kFoldGroup;
-    // [shard exit counters, one 64-B line each, + the shards-done line][group
-    // counters] → 64-B aligned [group sums, 8 doubles each]
-    fold_bytes_ = ((sizeof(unsigned) * (16 * 9 + size_t(ng)) + 63) / 64) * 64;
-    PE_HIP_CHECK(hipMalloc(&fold_buf_, fold_bytes_ + sizeof(double) * 8 * size_t(ng)));
-    PE_HIP_CHECK(hipMemsetAsync(fold_buf_, 0, fold_bytes_, stream_));
-    PE_HIP_CHECK(hipDeviceSynchronize());
-    k.xcnt = static_cast<unsigned*>(fold_buf_);
-    k.gcnt = k.xcnt + 16 * 9;
-    k.gsum = reinterpret_cast<double*>(static_cast<char*>(fold_buf_) + fold_bytes_);
-    k.fold = 1;
-  }
-  // The halo push goes live with the in-sweep sum (its flags are the push's
-  // delivery signal); the local sweeps above ran without either.
-  if (push_) {
+  // The push's pointers (its kernel variant runs when choose_halo_path picks
+  // it: the push is delivered by the in-sweep sum's flags, so the local
+  // sweeps above ran without either).
+  if (push_ok_) {
     const int64_t side = int64_t(hdep_) * k.pitch;
     double* lo = static_cast<double*>(hpeers_[size_t(blk_.nbr[LEFT] >= 0 ? blk_.nbr[LEFT] : blk_.rank)]);
     double* hi = static_cast<double*>(hpeers_[size_t(blk_.nbr[RIGHT] >= 0 ? blk_.nbr[RIGHT] : blk_.rank)]);
@@ -679,8 +648,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       k.hpush_hi[b] = blk_.has(RIGHT) ? hi + (2 * b + 0) * side : nullptr;
     }
     k.hrecv = hrecv_;
-    k.push = 1;
   }
+  k.push = 0;
+  choose_halo_path();
+  mark("halo path");
 
   // Iterations per host check: aim for ~0.5 ms of device work per chunk.
   const double pts = double(nx) * double(ny);
@@ -719,16 +690,20 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
 // there (no import copy) — no exchange launch, no RCCL call, and the iteration
 // becomes graph-capturable.  Every input of the decision is global (grid,
 // process grid, environment, transport type), so every rank reaches
-// map_peer_buffers (collective) or none does.  PE_HALO=exchange opts out.
+// map_peer_buffers (collective) or none does.  This only maps and self-tests
+// the buffers (push_ok_): whether the job pushes is choose_halo_path's
+// decision (PE_HALO=exchange / put: never).
 void DeviceSolver::setup_halo_push() {
-  push_ = false;
+  push_ = push_ok_ = false;
+  const char* hm = std::getenv("PE_HALO");
+  const bool allowed = !hm || std::string(hm) == "push";
   // PE_PUSH_LOOPBACK=1 (diagnostic, tools/block_probe.py on one GPU): the
   // push kernel's work without peers — every push lands in this rank's own
   // receive buffer and the halo rows are read back from it (wrong values,
   // the real stores and loads), so a row slab's per-rank time includes what
   // the 8-GPU job's push kernel does
-  if (const char* e = std::getenv("PE_PUSH_LOOPBACK");
-      e && std::atoi(e) == 1 && comm_->size() > 1 && fused_ && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= 2 * hdep_) {
+  if (const char* e = std::getenv("PE_PUSH_LOOPBACK"); allowed && e && std::atoi(e) == 1 && comm_->size() > 1 &&
+                                                       fused_ && blk_.Py == 1 && (prob_.M - 1) / blk_.Px >= 2 * hdep_) {
     const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);
     void* buf = nullptr;
     PE_HIP_CHECK(hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained));
@@ -736,26 +711,20 @@ void DeviceSolver::setup_halo_push() {
     PE_HIP_CHECK(hipDeviceSynchronize());
     hrecv_ = static_cast<double*>(buf);
     hpeers_.assign(size_t(comm_->size()), buf);
-    push_ = true;
+    push_ok_ = push_loop_ = true;
     push_status_ = "loopback (diagnostic)";
     return;
   }
   push_status_ = comm_->size() < 2 ? "off: one rank" : !fused_ ? "off: classic path" : !comm_->peer_sum()
-                 ? "off: no P2P transport (" + p2p_setup_status() + ")" : blk_.Py != 1 ? "off: 2-D blocks (RCCL exchange)"
+                 ? "off: no P2P transport (" + p2p_setup_status() + ")" : blk_.Py != 1 ? "off: 2-D blocks"
                  : "";
   if (!push_status_.empty()) return;
   push_status_ = "off: slabs thinner than 2 halo depths";
   if ((prob_.M - 1) / blk_.Px < 2 * hdep_) return;  // edge rows 1..h and nx-h+1..nx distinct
   push_status_ = "off: PE_XR=0";
   if (const char* e = std::getenv("PE_XR"); e && std::atoi(e) == 0) return;
-  // Opt-in since round 5 (PE_HALO=push): timed on one GPU (PE_PUSH_LOOPBACK)
-  // the push kernel's per-rank iteration is 58 µs at the 8-rank slab of 8192²
-  // and 109 at 4 ranks, against 45-47 / 79-81 for the plain sweep with the
-  // exchange at 15 / 8 µs exchange / sum delays per sweep (overlapped or not;
-  // profiles/r5_push_release.txt): the push kernel's register pressure and
-  // uncached halo traffic cost more than the exchange it saves
-  push_status_ = "off: exchange (PE_HALO=push pushes from the sweep)";
-  if (const char* e = std::getenv("PE_HALO"); !(e && std::string(e) == "push")) return;
+  push_status_ = std::string("off: PE_HALO=") + (hm ? hm : "");
+  if (!allowed) return;
   push_status_ = "fallback: the receive buffers could not be mapped on every rank";
   const size_t bytes = sizeof(double) * 4 * size_t(hdep_) * size_t(kp_->pitch);  // [parity][side][hdep rows]
   void* buf = nullptr;
@@ -774,8 +743,8 @@ void DeviceSolver::setup_halo_push() {
     return;
   }
   hrecv_ = static_cast<double*>(buf);
-  push_ = true;
-  push_status_ = "on";
+  push_ok_ = true;
+  push_status_ = "available";
   // Collective self-test of the path, in its own store / load forms: every
   // rank fills its neighbours' receive buffers with rank-coded values, the
   // ranks synchronise, every rank checks what arrived; all ranks keep the
@@ -823,21 +792,294 @@ void DeviceSolver::setup_halo_push() {
       hpeers_.clear();
       PE_HIP_CHECK(hipFree(buf));
       hrecv_ = nullptr;
-      push_ = false;
+      push_ok_ = false;
     }
   }
+}
+
+// Halo exchange by peer put (p2p.hip kPut): every rank maps its neighbours'
+// fine-grained inboxes and one kernel per halo phase stores this rank's
+// message straight into them over xGMI, flags it, waits for the neighbours'
+// messages in its own inbox and copies them into place — no RCCL launch, no
+// proxy thread, and the same pack / unpack kernels and halo plan as the
+// comm's exchange.  Set-up is collective and fail-safe like the push's: map
+// (every rank or none), self-test with rank-coded messages, agree.
+// PE_PUT_LOOPBACK=1 (one GPU: probes, tests): the rank is its own peer on
+// every side — each message lands in its own receive buffer, as with the
+// loopback delay transport — so the kernel's real stores, flags and copies run
+// on one device.  PE_HALO=exchange / push: off.
+void DeviceSolver::setup_halo_put() {
+  put_ = put_ok_ = false;
+  const char* hm = std::getenv("PE_HALO");
+  const bool allowed = !hm || std::string(hm) == "put";
+  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
+  const char* lb = std::getenv("PE_PUT_LOOPBACK");
+  put_loop_ = lb && std::atoi(lb) == 1;
+  put_status_ = comm_->size() < 2 ? "off: one rank" : !fused_ ? "off: classic path" : !allowed
+                ? std::string("off: PE_HALO=") + hm : (!put_loop_ && !comm_->peer_sum())
+                ? "off: no P2P transport (" + p2p_setup_status() + ")" : "";
+  if (!put_status_.empty()) return;
+  // inbox slot: the largest message of a phase — y strips (2·hdep values per
+  // owned row) or hdep whole interleaved rows
+  const std::vector<HaloPhase> ph = halo_phases(0);
+  int64_t cmax = 1;
+  for (const HaloPhase& p : ph)
+    for (const Exchange& e : p.ex) cmax = std::max(cmax, e.count);
+  // (every rank takes part in the collectives below, a rank without
+  // neighbours too: its buffer simply stays unused)
+  cmax = std::max<int64_t>({cmax, 2 * int64_t(hdep_) * blk_.nx, int64_t(hdep_) * kp_->pitch});
+  put_stride_ = (cmax + 31) / 32 * 32;
+  const size_t flag_bytes = sizeof(unsigned long long) * 4 * dev::kPutParts * dev::kPutFlagStride;
+  const size_t bytes = flag_bytes + sizeof(double) * 4 * 2 * size_t(put_stride_);
+  void* buf = nullptr;
+  if (hipExtMallocWithFlags(&buf, bytes, hipDeviceMallocFinegrained) != hipSuccess) {
+    buf = nullptr;
+    (void)hipGetLastError();
+  } else {
+    PE_HIP_CHECK(hipMemsetAsync(buf, 0, bytes, stream_));
+  }
+  PE_HIP_CHECK(hipMalloc(&put_cnt_, sizeof(unsigned) * 8));
+  PE_HIP_CHECK(hipMemsetAsync(put_cnt_, 0, sizeof(unsigned) * 8, stream_));
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+  if (put_loop_) {
+    if (!buf) PE_HIP_CHECK(hipErrorOutOfMemory);
+    put_peers_.assign(size_t(comm_->size()), buf);
+  } else {
+    put_peers_ = comm_->map_peer_buffers(buf);
+  }
+  put_status_ = "fallback: the inboxes could not be mapped on every rank";
+  if (put_peers_.empty()) {
+    if (buf) PE_HIP_CHECK(hipFree(buf));
+    return;
+  }
+  put_buf_ = buf;
+  // Self-test: one exchange of every halo phase's messages (at most 4096
+  // values each) with rank-coded data, checked on arrival; every rank keeps
+  // the comm's exchange if any check failed anywhere.
+  {
+    const int64_t n = std::min<int64_t>(4096, put_stride_);
+    double *sbuf = nullptr, *rbuf = nullptr, *codes = nullptr;
+    int* bad = nullptr;
+    PE_HIP_CHECK(hipMalloc(&sbuf, sizeof(double) * 4 * n));
+    PE_HIP_CHECK(hipMalloc(&rbuf, sizeof(double) * 4 * n));
+    PE_HIP_CHECK(hipMalloc(&codes, sizeof(double) * 4));
+    PE_HIP_CHECK(hipMalloc(&bad, sizeof(int)));
+    std::vector<double> hs(size_t(4 * n));
+    const double me = double(blk_.rank + 1);
+    for (int64_t i = 0; i < 4 * n; ++i) hs[size_t(i)] = me + double((i % n) % 7);
+    upload(sbuf, hs.data(), sizeof(double) * hs.size());
+    PE_HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), stream_));
+    int hbad = 0;
+    for (const HaloPhase& p : ph) {
+      std::vector<Exchange> ex;
+      double hc[4] = {0, 0, 0, 0};
+      for (const Exchange& e : p.ex) {
+        const int m = int(ex.size());
+        ex.push_back(Exchange{e.dir, e.peer, sbuf + m * n, rbuf + m * n, n});
+        hc[m] = put_loop_ ? me : double(e.peer + 1);
+      }
+      if (ex.empty()) continue;
+      upload(codes, hc, sizeof(hc));
+      const double keep = put_timeout_s_;
+      put_timeout_s_ = std::min(keep, 5.0);
+      put_ = true;
+      xfer(ex, stream_);
+      put_ = false;
+      put_timeout_s_ = keep;
+      dev::PutArgs a{};
+      a.nmsg = int(ex.size());
+      for (size_t m = 0; m < ex.size(); ++m) {
+        a.m[m].dst = ex[m].recv;
+        a.m[m].n = n;
+      }
+      dev::launch_put_check(a, codes, bad, stream_);
+      PE_HIP_CHECK(hipGetLastError());
+      PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    }
+    PE_HIP_CHECK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, stream_));
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    PE_HIP_CHECK(hipFree(sbuf));
+    PE_HIP_CHECK(hipFree(rbuf));
+    PE_HIP_CHECK(hipFree(codes));
+    PE_HIP_CHECK(hipFree(bad));
+    // PE_FAULT_INJECT=puttest@rank:R — rank R's check fails (fallback test)
+    if (const char* e = std::getenv("PE_FAULT_INJECT"); e && std::string(e).rfind("puttest@rank:", 0) == 0 &&
+                                                        std::atoi(e + 13) == blk_.rank)
+      hbad = 1;
+    if (hbad) std::fprintf(stderr, "[pe] rank %d: halo-put self-test: %d wrong values received\n", blk_.rank, hbad);
+    double fail[1] = {hbad != 0 ? 1.0 : 0.0};
+    comm_->host_max(fail, 1, stream_);
+    if (fail[0] != 0.0) {
+      if (blk_.rank == 0) std::fprintf(stderr, "[pe] halo put unavailable on this job (self-test), using the exchange\n");
+      put_status_ = hbad ? "fallback: self-test failed on this rank" : "fallback: self-test failed on a peer";
+      if (!put_loop_) comm_->unmap_peer_buffers(put_peers_);
+      put_peers_.clear();
+      PE_HIP_CHECK(hipFree(put_buf_));
+      put_buf_ = nullptr;
+      return;
+    }
+  }
+  (void)nb;
+  put_ok_ = true;
+  put_status_ = put_loop_ ? "loopback (diagnostic)" : "available";
+}
+
+void DeviceSolver::xfer(const std::vector<Exchange>& ex, hipStream_t s) {
+  if (!put_) {
+    comm_->exchange(ex, s);
+    return;
+  }
+  if (ex.empty()) return;
+  if (ex.size() > 4) throw std::logic_error("put: at most 4 messages per halo phase");
+  const size_t flag_words = size_t(4) * dev::kPutParts * dev::kPutFlagStride;
+  auto flags = [&](void* buf, int d) {
+    return static_cast<unsigned long long*>(buf) + size_t(d) * dev::kPutParts * dev::kPutFlagStride;
+  };
+  auto box = [&](void* buf, int d) {
+    return reinterpret_cast<double*>(static_cast<unsigned long long*>(buf) + flag_words) + size_t(d) * 2 * put_stride_;
+  };
+  dev::PutArgs a{};
+  a.nmsg = int(ex.size());
+  a.stride = put_stride_;
+  a.cnt = put_cnt_;
+  a.timeout_ticks = (long long)(put_timeout_s_ * 1e8);
+  for (size_t m = 0; m < ex.size(); ++m) {
+    const Exchange& e = ex[m];
+    if (e.count > put_stride_) throw std::logic_error("put: message larger than the inbox");
+    void* peer = put_peers_[size_t(put_loop_ ? blk_.rank : e.peer)];
+    // the peer files this rank's message under the direction it sees us in;
+    // a loopback rank under the message's own direction (send → own receive)
+    const int rd = put_loop_ ? e.dir : opposite(e.dir);
+    a.m[m] = dev::PutMsg{e.send, box(peer, rd), flags(peer, rd), box(put_buf_, e.dir), flags(put_buf_, e.dir),
+                         e.recv, (long long)e.count, e.dir};
+  }
+  dev::launch_put(a, s);
+  PE_HIP_CHECK(hipGetLastError());
+}
+
+void DeviceSolver::apply_halo_path(const std::string& path, bool overlap) {
+  push_ = path == "push" && push_ok_;
+  put_ = path == "put" && put_ok_;
+  kp_->push = push_ ? 1 : 0;
+  const bool relay = overlap != want_overlap_;
+  want_overlap_ = overlap;
+  for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured on the old path
+  graphs_.clear();
+  // the overlap's boundary-first list, or the plain one (the exchange, the put
+  // and the push share the plain layout: no re-layout between them)
+  if (relay || overlap_ != (overlap && !push_)) setup_items();
+}
+
+// The multi-rank halo path, chosen on the job's own transport.  Candidates:
+// the comm's exchange (RCCL grouped send / receive: pack, exchange, unpack
+// after the sweep), the same through the peer-put kernel (setup_halo_put), each
+// with and without the halo/interior overlap (the exchange on the halo stream
+// under the interior items), and — row slabs with in-sweep P2P sums — the
+// sweep's own halo push.  Each runs 2 + kTimed sweeps of the real iteration
+// (cross-rank sums included, the stop test off) from the initial state; the
+// two fastest are timed once more (min of the two); every time is the max over
+// ranks, so every rank keeps the same path.  Until round 5 the choice was a
+// fixed rule (exchange; overlap when a measured exchange exceeded 12 µs) set
+// from one-GPU probes with simulated 15 / 8 µs delays; the first cross-device
+// run must not rest on a simulation.  PE_HALO=exchange / put / push and
+// PE_OVERLAP=0 / 1 restrict the candidates; PE_HALO_TUNE=0 takes the first one
+// left (exchange, no overlap, when allowed) without timing.
+void DeviceSolver::choose_halo_path() {
+  halo_cands_.clear();
+  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
+  if (comm_->size() < 2 || !fused_ || resident_) {
+    halo_path_ = comm_->size() < 2 ? "none: one rank" : !fused_ ? "exchange (classic path)" : "none: resident";
+    apply_halo_path("exchange", false);
+    return;
+  }
+  const char* hm = std::getenv("PE_HALO");
+  const char* ov = std::getenv("PE_OVERLAP");
+  // (the two-step sweep has no boundary-item signal; every rank decides this
+  // from global inputs — a rank without neighbours still takes part, its
+  // overlap is simply off in setup_items)
+  const bool ov_able = !sstep_ || steps_ >= 3;
+  struct Cand {
+    std::string path;
+    bool ov;
+    double ms;
+  };
+  std::vector<Cand> cands;
+  auto add = [&](const char* path, bool o) {
+    if (o && !ov_able) return;
+    if (ov && (std::atoi(ov) != 0) != o) return;
+    cands.push_back(Cand{path, o, 0.0});
+  };
+  // (the plain-layout candidates first, then the overlapped ones: one re-layout)
+  const bool ex_ok = !hm || std::string(hm) == "exchange";
+  if (ex_ok) add("exchange", false);
+  if (put_ok_) add("put", false);
+  if (push_ok_ && !(ov && std::atoi(ov) != 0)) cands.push_back(Cand{"push", false, 0.0});
+  if (ex_ok) add("exchange", true);
+  if (put_ok_) add("put", true);
+  if (cands.empty()) cands.push_back(Cand{"exchange", ov && std::atoi(ov) != 0 && ov_able, 0.0});
+  auto name = [](const Cand& c) { return c.path + (c.ov ? "+overlap" : ""); };
+  const bool tune = !(std::getenv("PE_HALO_TUNE") && std::atoi(std::getenv("PE_HALO_TUNE")) == 0);
+  if (cands.size() == 1 || !tune) {
+    apply_halo_path(cands[0].path, cands[0].ov);
+    halo_path_ = name(cands[0]) + (cands.size() == 1 ? " (only candidate)" : " (PE_HALO_TUNE=0)");
+    (void)nb;
+    return;
+  }
+  Range range("pe.choose_halo_path");
+  const int keep_tol = kp_->check_tol;
+  kp_->check_tol = 0;
+  constexpr int kTimed = 4;
+  auto time_path = [&](const Cand& c) {
+    apply_halo_path(c.path, c.ov);
+    reset();
+    run_iterations(2 * steps_, false);
+    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+    run_iterations(int64_t(kTimed) * steps_, false);
+    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+    wait_event(t1_);
+    float ms = 0.f;
+    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+    double v[1] = {double(ms) / kTimed};
+    comm_->host_max(v, 1, stream_);
+    return v[0];
+  };
+  for (Cand& c : cands) {
+    c.ms = time_path(c);
+    halo_cands_.emplace_back(name(c), 1e3 * c.ms);
+  }
+  // finalists: the two fastest once more (the clock ramps during construction)
+  std::vector<size_t> order(cands.size());
+  for (size_t i = 0; i < order.size(); ++i) order[i] = i;
+  std::stable_sort(order.begin(), order.end(), [&](size_t a, size_t b) { return cands[a].ms < cands[b].ms; });
+  for (size_t f = 0; f < 2 && f < order.size(); ++f) {
+    Cand& c = cands[order[f]];
+    const double ms = time_path(c);
+    halo_cands_.emplace_back(name(c) + " (again)", 1e3 * ms);
+    c.ms = std::min(c.ms, ms);
+  }
+  size_t best = 0;
+  for (size_t i = 1; i < cands.size(); ++i)
+    if (cands[i].ms < cands[best].ms) best = i;
+  apply_halo_path(cands[best].path, cands[best].ov);
+  halo_path_ = name(cands[best]);
+  kp_->check_tol = keep_tol;
+  if (std::getenv("PE_CTOR_TRACE") && blk_.rank == 0) {
+    for (const auto& c : halo_cands_) std::fprintf(stderr, "[pe] halo path %-24s %8.2f us/sweep\n", c.first.c_str(), c.second);
+    std::fprintf(stderr, "[pe] halo path chosen: %s\n", halo_path_.c_str());
+  }
+  (void)nb;
 }
 
 void DeviceSolver::relayout(int ti, int order) {
   if (!fused_ || resident_) return;
   ti = std::max(2, std::min(ti, steps_ >= 3 ? dev::kTImax3 : 64));
   const int ord = (order == 0 || order == 3) ? order : kp_->order;  // static LPT list / dynamic per-XCD queue
-  // the item-sum slots of the dynamic order and the fold buffer were sized at
+  // the item-sum slots of the dynamic order were sized at
   // construction: a layout that needs more is refused before anything
   // changes (the static layout sums per block, not per item: any height)
   const int64_t nitems = int64_t(kp_->nstrips) * ((blk_.nx + ti - 1) / ti);
   const int64_t need = ord == 0 ? 0 : 2 * nitems + 64;
-  if (need > nslot_cap_ || (kp_->fold && ord != 3))
+  if (need > nslot_cap_)
     throw std::invalid_argument("relayout: " + std::to_string(ti) + " rows per item (order " + std::to_string(ord) +
                                 ") needs " + std::to_string(need) + " item-sum slots, " + std::to_string(nslot_cap_) +
                                 " allocated");
@@ -927,10 +1169,12 @@ DeviceSolver::~DeviceSolver() {
   (void)hipFree(tables_);
   (void)hipFree(rowcls_);
   (void)hipFree(halo_);
-  if (push_) comm_->unmap_peer_buffers(hpeers_);
+  if (!hpeers_.empty() && !push_loop_) comm_->unmap_peer_buffers(hpeers_);
   if (hrecv_) (void)hipFree(hrecv_);
+  if (!put_peers_.empty() && !put_loop_) comm_->unmap_peer_buffers(put_peers_);
+  if (put_buf_) (void)hipFree(put_buf_);
+  if (put_cnt_) (void)hipFree(put_cnt_);
   if (stage_) (void)hipHostFree(stage_);
-  if (fold_buf_) (void)hipFree(fold_buf_);
   (void)hipFree(partial_);
   if (hist_) (void)hipFree(hist_);
   if (stamps_) (void)hipFree(stamps_);
@@ -1035,7 +1279,7 @@ void DeviceSolver::enqueue_exchange(int buf, bool after_sweep) {
   if (push_ && after_sweep) return;
   if (sstep_ && after_sweep) dev::launch_pack(*kp_, buf, stream_);  // (no-op without a y neighbour)
   for (const HaloPhase& ph : halo_phases(buf)) {
-    comm_->exchange(ph.ex, stream_);
+    xfer(ph.ex, stream_);
     if (ph.unpack) dev::launch_unpack(*kp_, buf, stream_);
   }
   // initial state through the comm: its halo rows into the receive buffer
@@ -1066,7 +1310,6 @@ void DeviceSolver::enqueue_init() {
   }
   PE_HIP_CHECK(hipMemsetAsync(halo_, 0, sizeof(double) * hsize_ * 4, stream_));
   PE_HIP_CHECK(hipMemsetAsync(st_, 0, sizeof(DevState), stream_));
-  if (fold_buf_) PE_HIP_CHECK(hipMemsetAsync(fold_buf_, 0, fold_bytes_, stream_));
   ov_epoch_ = 0;
   dev::launch_init(*kp_, opt_.init == Init::Random ? 1 : 0, opt_.seed, opt_.init_amp, opt_.variant, stream_);
   PE_HIP_CHECK(hipGetLastError());
@@ -1141,7 +1384,7 @@ void DeviceSolver::enqueue_iteration(int par, int mlimit) {
     mark_begin(kPhSweep, stream_);
     dev::launch_S(ko, par, stream_, false);  // boundary items first in every shard
     mark_end(stream_);
-    if (ko.order == 3 && !ko.fold) {
+    if (ko.order == 3) {
       mark_begin(kPhDot, stream_);
       dev::launch_red(ko, par, stream_);
       mark_end(stream_);
@@ -1156,7 +1399,7 @@ void DeviceSolver::enqueue_iteration(int par, int mlimit) {
       mark_begin(kPhHalo, hs_);
       if (sstep_) dev::launch_pack(*kp_, par, hs_);  // (multi-step: y strips packed after the boundary items)
       for (const HaloPhase& ph : halo_phases(par)) {
-        comm_->exchange(ph.ex, hs_);
+        xfer(ph.ex, hs_);
         if (ph.unpack) dev::launch_unpack(*kp_, par, hs_);
       }
       mark_end(hs_);
@@ -1178,7 +1421,7 @@ void DeviceSolver::enqueue_iteration(int par, int mlimit) {
       dev::launch_S(*kp_, par, stream_, false);
     }
     mark_end(stream_);
-    if (kp_->order == 3 && !kp_->fold) {
+    if (kp_->order == 3) {
       mark_begin(kPhDot, stream_);
       dev::launch_red(*kp_, par, stream_);
       mark_end(stream_);
@@ -1241,7 +1484,11 @@ hipGraphExec_t DeviceSolver::graph_for(int iters) {
 
 // (overlap: a graph may serialise the two streams' branches in any order,
 // and the halo branch waits on the sweep — always eager)
-bool DeviceSolver::graphs_usable() const { return (comm_->capturable() || push_) && !overlap_ && !resident_; }
+// (no comm call in the iteration: the sweep's push or the put kernel for the
+// halo, the in-sweep P2P sums for the scalars)
+bool DeviceSolver::graphs_usable() const {
+  return (comm_->capturable() || push_ || (put_ && kp_->xr.peers)) && !overlap_ && !resident_;
+}
 
 void DeviceSolver::enqueue_chunk(int iters, int sample_iters) {
   // The captured graph starts at parity 0 and has an even length; iterations
@@ -1402,7 +1649,7 @@ SolveResult DeviceSolver::solve() {
   const auto t_start = clk::now();
   SolveResult res;
   res.backend = "hip";
-  res.algo = resident_ ? "resident" : steps_ == 4 ? "four-step" : steps_ == 3 ? "three-step" : steps_ == 2 ? "two-step" : fused_ ? "fused" : "classic";
+  res.algo = resident_ ? "resident" : steps_ == 3 ? "three-step" : steps_ == 2 ? "two-step" : fused_ ? "fused" : "classic";
   res.Px = blk_.Px;
   res.Py = blk_.Py;
   // T_solver spans construction (allocation, tables, placement search) like
@@ -1545,7 +1792,7 @@ SolveResult DeviceSolver::solve() {
     // fix-up (the solve stopped inside the last sweep), the replay launch
     // first recomputes that iterate's r into x[wpar], so w and r belong to the
     // same iterate.
-    const bool three = fused_ && steps_ >= 3;  // (three- or four-step: the moment recurrence)
+    const bool three = fused_ && steps_ >= 3;  // (three-step: the moment recurrence)
     enqueue_wflush();
     // (the check below is timed on its own: res.t.check, outside T_iterate / T_solver)
     PE_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -1662,7 +1909,7 @@ SolveResult DeviceSolver::solve() {
     // in-sweep cross-rank sum: the final blocks' wait for the peers' flags
     // (ticks of the 100 MHz s_memrealtime clock)
     res.t.wait = double(hs.xr_wait) * 1e-8;
-    res.t.dot_fused = !(fused_ && kp_->order == 3 && !kp_->fold);
+    res.t.dot_fused = !(fused_ && kp_->order == 3);
     if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
   }
   res.t.solver = construct + secs(t_start, clk::now()) - check_s;
@@ -1882,7 +2129,7 @@ SolveResult device_solve_group(const Problem& P, const ProcessGrid& pg, const So
   PE_HIP_CHECK(hipFree(dp));
   for (auto& e : ev) PE_HIP_CHECK(hipEventDestroy(e));
   res.backend = "hip-group";
-  res.algo = steps == 4 ? "four-step" : steps == 3 ? "three-step" : steps == 2 ? "two-step" : fused ? "fused" : "classic";
+  res.algo = steps == 3 ? "three-step" : steps == 2 ? "two-step" : fused ? "fused" : "classic";
   res.Px = pg.Px;
   res.Py = pg.Py;
   res.t.solver = secs(t_start, clk::now());

@@ -283,112 +283,11 @@ __device__ __forceinline__ void finalize_block(const KParams& k, DevState* st, i
   if (threadIdx.x == 0) sweep_finalize<WM>(k, st, par, sc, t);
 }
 
-// Wave-level form of finalize_block (the item-sum fold ends in one wave).
-template <int WM>
-__device__ __forceinline__ void finalize_wave(const KParams& k, DevState* st, int par, const Scal& sc,
-                                              double (&t)[7]) {
-  if (k.xr.peers) {
-    slow_inject(k);
-    peer_sum_wave(k.xr, t, 7);
-  }
-  if ((threadIdx.x & 63) == 0) sweep_finalize<WM>(k, st, par, sc, t);
-}
-
 __device__ __forceinline__ void wave_sum7(double (&v)[7]) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1)
 #pragma unroll
     for (int n = 0; n < 7; ++n) v[n] += __shfl_xor(v[n], o, 64);
-}
-
-// In-kernel item-sum fold (KParams::fold), per item: publish the item's 7
-// sums (write-through, drained), count it in its group; the wave that counts
-// a group's last item sums the group's slots in lane order (deterministic,
-// whoever computed which item) and publishes the group sum.
-__device__ __forceinline__ void fold_item(const KParams& k, int64_t slot, const double (&v)[7]) {
-  const int lane = int(threadIdx.x & 63);
-  const int g = int(slot / kFoldGroup);
-  const int gn = min(kFoldGroup, k.nslots - g * kFoldGroup);
-  unsigned t = 0;
-  if (lane == 0) {
-    double* dst = k.itemsum + 8 * slot;
-#pragma unroll
-    for (int n = 0; n < 7; ++n) __hip_atomic_store(dst + n, v[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    t = __hip_atomic_fetch_add(k.gcnt + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  t = unsigned(__builtin_amdgcn_readfirstlane(int(t)));
-  if (int(t) != gn - 1) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const bool in = lane < gn;
-  const int64_t q = int64_t(g) * kFoldGroup + (in ? lane : 0);
-  const double4 a = *reinterpret_cast<const double4*>(k.itemsum + 8 * q);
-  const double4 b = *reinterpret_cast<const double4*>(k.itemsum + 8 * q + 4);
-  double sm[7] = {in ? a.x : 0.0, in ? a.y : 0.0, in ? a.z : 0.0, in ? a.w : 0.0,
-                  in ? b.x : 0.0, in ? b.y : 0.0, in ? b.z : 0.0};
-  wave_sum7(sm);
-  if (lane == 0) {
-    __hip_atomic_store(k.gcnt + g, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // next sweep
-    double* gd = k.gsum + 8 * int64_t(g);
-#pragma unroll
-    for (int n = 0; n < 7; ++n) __hip_atomic_store(gd + n, sm[n], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-}
-
-// ... at wave exit (live sweeps only, every wave of the grid): count the wave
-// in its XCD shard, the shard's last wave counts the shard; the last wave of
-// the grid sums the group sums in order (batched loads) and updates the
-// state.  Every wave has read the sweep's state long before it exits, so the
-// state update races no reader (nor a queue pull: the heads are reset here).
-template <int WM>
-__device__ __forceinline__ void fold_exit(const KParams& k, DevState* st, int par, const Scal& sc) {
-  const int lane = int(threadIdx.x & 63);
-  const int nsh = min(8, int(gridDim.x));
-  const int xs = int(blockIdx.x) % nsh;
-  const int waves_x = ((int(gridDim.x) - xs + nsh - 1) / nsh) * kWPB;
-  unsigned t = 0;
-  if (lane == 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    t = __hip_atomic_fetch_add(k.xcnt + 16 * xs, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  t = unsigned(__builtin_amdgcn_readfirstlane(int(t)));
-  if (int(t) != waves_x - 1) return;
-  unsigned t2 = 0;
-  if (lane == 0) {
-    __hip_atomic_store(k.xcnt + 16 * xs, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    t2 = __hip_atomic_fetch_add(k.xcnt + 16 * 8, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  t2 = unsigned(__builtin_amdgcn_readfirstlane(int(t2)));
-  if (int(t2) != nsh - 1) return;
-  if (lane == 0) __hip_atomic_store(k.xcnt + 16 * 8, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  const int ng = (k.nslots + kFoldGroup - 1) / kFoldGroup;
-  double tot[7] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-  constexpr int RU = 8;  // group sums per lane in flight (+0.0 past the end: order and bits unchanged)
-  for (int g0 = lane; g0 < ng + 63; g0 += RU * 64) {
-    double4 a[RU], b[RU];
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const int gi = min(g0 + u * 64, ng - 1);
-      a[u] = *reinterpret_cast<const double4*>(k.gsum + 8 * int64_t(gi));
-      b[u] = *reinterpret_cast<const double4*>(k.gsum + 8 * int64_t(gi) + 4);
-    }
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int u = 0; u < RU; ++u) {
-      const bool in = g0 + u * 64 < ng;
-      tot[0] += in ? a[u].x : 0.0;
-      tot[1] += in ? a[u].y : 0.0;
-      tot[2] += in ? a[u].z : 0.0;
-      tot[3] += in ? a[u].w : 0.0;
-      tot[4] += in ? b[u].x : 0.0;
-      tot[5] += in ? b[u].y : 0.0;
-      tot[6] += in ? b[u].z : 0.0;
-    }
-  }
-  wave_sum7(tot);
-  finalize_wave<WM>(k, st, par, sc, tot);
 }
 
 // OCC > 0 caps registers for OCC waves per SIMD (amdgpu_waves_per_eu); PF =
@@ -417,8 +316,7 @@ __device__ __forceinline__ unsigned long long rtc() {
 // also stored into the x-neighbours' fine-grained receive buffers over xGMI
 // (system-scope write-through stores, drained and released before the item
 // ends, so they are delivered before this rank's cross-rank-sum flags).
-// FOLD — in-kernel item-sum fold (KParams::fold, dynamic sweeps, opt-in).
-template <int OCC, int PF, bool NT, int WM, bool STAMP = false, bool PUSH = false, bool FOLD = false>
+template <int OCC, int PF, bool NT, int WM, bool STAMP = false, bool PUSH = false>
 __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OCC : 1))) void kS(KParams k, int par) {
   DevState* st = k.st;
   const unsigned long long t_entry = STAMP ? rtc() : 0ull;
@@ -566,7 +464,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       // A wave reaches this point after its first item's prologue or after
       // an empty walk — different program points within one workgroup — so
       // the hand-off counts waves (no workgroup barrier on this path).
-      if ((!persum || FOLD) && arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
+      if (!persum && arrive_last_wave(&st->ticket[4], gridDim.x * kWPB) && lane == 0) {
         sweep_terminal(k, st, sc, tm);
         __hip_atomic_store(&st->ticket[4], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       }
@@ -922,9 +820,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
       // wave pulled which item
       double v[7] = {sg, sd, se, sps, szz, szp, spp};
       wave_sum7(v);
-      if constexpr (FOLD) {
-        fold_item(k, slot, v);
-      } else if (lane == 0) {
+      if (lane == 0) {
         double* dst = k.itemsum + 8 * slot;
 #pragma unroll
         for (int n = 0; n < 7; ++n) dst[n] = v[n];
@@ -955,10 +851,7 @@ __global__ __launch_bounds__(TJ) __attribute__((amdgpu_waves_per_eu(OCC > 0 ? OC
     if (lane == 0) k.stamps[4 * int64_t(k.nslots) + 2 * gwave + 1] = rtc();
   }
   if (!state_ok && leave()) return;
-  if (persum) {  // kRed reduces the item sums and finalizes — or the fold, here
-    if constexpr (FOLD) fold_exit<WM>(k, st, par, sc);
-    return;
-  }
+  if (persum) return;  // kRed reduces the item sums and finalizes
 
   double v[7] = {sg, sd, se, sps, szz, szp, spp};
   if (publish_last_nm<7>(k.partial, v, &st->ticket[0], &sflag, sm)) {  // (kcommon.hpp: n-major partials)
@@ -1280,8 +1173,7 @@ static int s_cfg() {
 template <int WM, class F>
 static auto with_kS(const KParams& k, F&& f) {
   if (k.stamps) return f(kS<2, 4, true, WM, true>);
-  if (k.push) return k.fold ? f(kS<2, 4, true, WM, false, true, true>) : f(kS<2, 4, true, WM, false, true>);
-  if (k.fold) return f(kS<2, 4, true, WM, false, false, true>);
+  if (k.push) return f(kS<2, 4, true, WM, false, true>);
   switch (s_cfg()) {
     case 1: return f(kS<2, 4, false, WM>);
     default: return f(kS<2, 4, true, WM>);
@@ -1289,10 +1181,6 @@ static auto with_kS(const KParams& k, F&& f) {
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
-  if (k.steps == 4) {  // four iterations per sweep (fused4.hip)
-    launch_S4(k, par, s);
-    return;
-  }
   if (k.steps == 3) {  // three iterations per sweep (fused3.hip)
     launch_S3(k, par, s);
     return;
@@ -1312,7 +1200,7 @@ void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
   // odd iterations (par 0) defer their w term, even ones (par 1) apply both
   if (par == 0) with_kS<0>(k, go);
   else with_kS<2>(k, go);
-  if (k.order == 3 && with_red && !k.fold) launch_red(k, par, s);
+  if (k.order == 3 && with_red) launch_red(k, par, s);
 }
 
 void launch_red(const KParams& k, int par, hipStream_t s) {
@@ -1350,7 +1238,6 @@ void launch_wflush(const KParams& k, hipStream_t s) {
 }
 
 int resident_blocks_S(const KParams& k, int wm) {
-  if (k.steps == 4) return resident_blocks_S4();
   if (k.steps == 3) return resident_blocks_S3();
   if (k.steps == 2) return resident_blocks_S2();
   auto occ = [](auto kern) {

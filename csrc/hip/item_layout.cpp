@@ -68,26 +68,12 @@ void DeviceSolver::set_items(int ti) {
 void DeviceSolver::setup_items() {
   KParams& k = *kp_;
   const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
-  // Overlap only pays when the exchange costs more than what the overlap
-  // itself costs the sweep (boundary-first item order, blocks kept free for
-  // the halo stream: +9-11 µs per iteration on 2-8 ranks with a zero-latency
-  // transport, profiles/r1_overlap_probe_device_decomp.txt).  Auto: measure
-  // the real exchange here (max over ranks, so every rank decides the same)
-  // and overlap when it exceeds PE_OVERLAP_MIN_US (default 12).
-  // PE_OVERLAP=1 / 0 forces it on / off.
-  const char* e = std::getenv("PE_OVERLAP");
-  overlap_ = false;
-  // (the two-step sweep runs without the overlap; the three-step sweep's
-  // boundary items count themselves in its kSignal variant, fused3.hip)
-  if (fused_ && (!sstep_ || steps_ >= 3) && comm_->size() > 1 && nb && !push_) {
-    if (e) {
-      overlap_ = std::atoi(e) != 0;
-    } else {
-      double min_us = 12.0;
-      if (const char* m = std::getenv("PE_OVERLAP_MIN_US")) min_us = std::atof(m);
-      overlap_ = exchange_us_ > min_us;
-    }
-  }
+  // Halo/interior overlap: the construction's choice (choose_halo_path times
+  // the exchange with and without it on the job's transport; PE_OVERLAP=1 / 0
+  // restricts the choice).  Only where the sweep can signal its boundary items
+  // (single sweep; the three-step sweep's kSignal variant, fused3.hip — not
+  // the two-step sweep) and the halo is exchanged, not pushed.
+  overlap_ = want_overlap_ && fused_ && (!sstep_ || steps_ >= 3) && comm_->size() > 1 && nb && !push_;
   // Lists: dynamic sweeps (order 3), static chunk-major sweeps (order 0:
   // heavy items split, below) and the overlap; orders 1 / 2 are plain
   // tuning walks.
@@ -132,7 +118,7 @@ void DeviceSolver::setup_items() {
   // columns?  (The kernel's has_gen on the same row-class table.)
   const int H = hdep_;  // halo rows an item re-reads per side (2 single sweep, 4 two-step, 6 three-step)
   const int HL = xorg_ + 1;  // a strip's left halo columns (three-step: 8, for aligned loads and stores)
-  const int64_t Wc = steps_ >= 3 ? 64 : 128;  // columns a wave strip loads (three-/four-step: one per lane)
+  const int64_t Wc = steps_ >= 3 ? 64 : 128;  // columns a wave strip loads (three-step: one per lane)
   auto row_gen_x = [&](int64_t q, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t t = q - tab_lo_;  // table index of local row q
@@ -182,7 +168,6 @@ void DeviceSolver::setup_items() {
     const int* m = &pmix_[size_t(s) * size_t(R + 1)];
     return m[b - q0 + 1] - m[a - q0];
   };
-  auto row_gen = [&](int64_t q, int s) { return q >= q0 && q < q0 + R ? ngen(q, q, s) > 0 : row_gen_x(q, s); };
   auto rows_cost = [&](int64_t ib, int64_t ie, int s) {
     const int64_t n = ie - ib + 1 + 2 * H, ng = ngen(ib - H, ie + H, s);
     return double(n - ng) + double(ng) * gen_cost;
@@ -269,65 +254,6 @@ void DeviceSolver::setup_items() {
           pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
         }
       }
-    // Segment layout (PE_SEGMENTS=1, or chosen by the two-step sweep's
-    // rows-per-item tuner, seg_layout_): one tall item per wave
-    const char* sg = std::getenv("PE_SEGMENTS");
-    if (seg_layout_ || (sg && std::atoi(sg) == 1)) {
-      // Segment layout: one tall item per wave.  Each strip's rows are cut
-      // into segments of equal estimated cost, and the strips' segment
-      // counts are dealt (largest remaining segment cost first) so that the
-      // heaviest segment is as light as possible.  An item re-reads its 4
-      // halo rows; at 24 rows that is +17 % row reads, ≈ the +21 % excess
-      // DRAM reads the counters show (profiles/r2_head_profile.txt), and a
-      // segment of a few hundred rows re-reads them once.
-      pcs.clear();
-      const int64_t nx = blk_.nx;
-      const int ns = k.nstrips;
-      const int Wt = std::max(dev::kWPB, (waves_avail / dev::kWPB) * dev::kWPB);
-      std::vector<std::vector<double>> pre(static_cast<size_t>(ns));  // cost prefix over rows 1..q
-      std::vector<double> C(static_cast<size_t>(ns));
-      double sumC = 0.0;
-      for (int s = 0; s < ns; ++s) {
-        auto& p = pre[size_t(s)];
-        p.assign(size_t(nx) + 1, 0.0);
-        for (int64_t q = 1; q <= nx; ++q) p[size_t(q)] = p[size_t(q - 1)] + (row_gen(q, s) ? gen_cost : 1.0);
-        C[size_t(s)] = p[size_t(nx)];
-        sumC += C[size_t(s)];
-      }
-      // at most 1500 rows (the list entry's row field), at least 4 per segment
-      const int n_min = int((nx + 1499) / 1500), n_max = std::max<int>(1, int(nx / 4));
-      std::vector<int> n(static_cast<size_t>(ns));
-      int tot = 0;
-      using CS = std::pair<double, int>;
-      std::priority_queue<CS> h;
-      for (int s = 0; s < ns; ++s) {
-        n[size_t(s)] = std::min(n_max, std::max(n_min, int(std::floor(C[size_t(s)] * Wt / sumC))));
-        tot += n[size_t(s)];
-        h.push(CS{C[size_t(s)] / n[size_t(s)], s});
-      }
-      while (tot < Wt && !h.empty()) {
-        const int s = h.top().second;
-        h.pop();
-        if (n[size_t(s)] >= n_max) continue;
-        ++n[size_t(s)];
-        ++tot;
-        h.push(CS{C[size_t(s)] / n[size_t(s)], s});
-      }
-      for (int s = 0; s < ns; ++s) {
-        const auto& p = pre[size_t(s)];
-        int64_t a0 = 1;
-        for (int q = 1; q <= n[size_t(s)]; ++q) {
-          int64_t a1 = nx + 1;
-          if (q < n[size_t(s)]) {
-            const double target = C[size_t(s)] * q / n[size_t(s)];
-            a1 = int64_t(std::lower_bound(p.begin() + 1, p.end(), target) - p.begin()) + 1;
-            a1 = std::min<int64_t>(std::max<int64_t>(a1, a0 + 4), nx + 1 - 4 * (n[size_t(s)] - q));
-          }
-          pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, is_boundary(a0, a1 - 1, s)});
-          a0 = a1;
-        }
-      }
-    }
     // Three-step sweep: a filling layout instead.  The sweep's time per row
     // step depends on the item's kind — a boundary-band item ≈2.2×, a mixed
     // one ≈1.3× a uniform one (tools/stamp_probe.py, profiles/r4_stamps.txt)
@@ -352,7 +278,7 @@ void DeviceSolver::setup_items() {
     // several rounds; the filling layout cost the 2×2 block 18 % there —
     // 108 vs 90.9 µs at zero delay, profiles/r5_overlap.txt)
     if (overlap_ && !std::getenv("PE_LAYOUT") && double(blk_.nx) * double(blk_.ny) < 1.2e7) lay = "fill";
-    const bool s3lay = steps_ >= 3 && !seg_layout_ && !(sg && std::atoi(sg) == 1);
+    const bool s3lay = steps_ >= 3;
     if (!s3lay) lay = "lpt";
     const bool equal = s3lay && lay == "equal";
     const bool fill = s3lay && lay == "fill";
@@ -370,26 +296,11 @@ void DeviceSolver::setup_items() {
     // profiles/r5_costband.txt; the slab's band row step runs ≈3.0× a uniform
     // one, 8192²'s 2.25×)
     double fband = 2.8, fmixed = 1.3;
-    // Tie-break among equally loaded waves: one wave per workgroup in turn
-    // (wave slot 0 of workgroups 0, 1, 2, …, then slot 1, …), so the pieces
-    // dealt first — the heaviest, band pieces — land on different CUs.  In
-    // wave order they stacked on the waves of a few CUs: the three-step LPT
-    // costed by kind put 8192²'s 505 band items on waves 0..504 (63 CUs, 8
-    // band waves each, two per SIMD) and each ran 456 µs instead of 222
-    // (profiles/r5_stamps_concentrated.txt).  Workgroups are dealt round-robin
-    // over the XCDs, so consecutive ones are on different CUs.
-    // PE_SPREAD=1 (opt-in); default: ties in wave order (the round-4 layouts).
-    // (PE_SPREAD=1 measured neutral to 1 % slower on the 8192² splits and the
-    // round-4 layouts it was made for are the defaults again: off by default)
-    const bool spread = std::getenv("PE_SPREAD") && std::atoi(std::getenv("PE_SPREAD")) == 1;
-    auto wfrom = [&](int r, int Wn) {  // the wave of tie-break rank r
-      const int nbw = std::max(1, Wn / dev::kWPB);
-      return spread ? (r % nbw) * dev::kWPB + r / nbw : r;
-    };
-    auto wrank = [&](int w, int Wn) {
-      const int nbw = std::max(1, Wn / dev::kWPB);
-      return spread ? (w % dev::kWPB) * nbw + w / dev::kWPB : w;
-    };
+    // (ties among equally loaded waves go in wave order; one wave per
+    // workgroup in turn measured neutral to 1 % slower on the 8192² splits,
+    // round 5 — removed in round 6)
+    auto wfrom = [](int r, int) { return r; };
+    auto wrank = [](int w, int) { return w; };
     // Wave capacity: workgroup b < cus_ is the first one dispatched to its CU,
     // b ≥ cus_ the second; the SIMDs' age-ordered issue runs the first
     // workgroup's waves ≈12 % faster per row step at the 8-rank slab of
@@ -699,7 +610,7 @@ void DeviceSolver::setup_items() {
       }
       lay_cuts_ = cuts;
     } else {
-    // Three-/four-step LPT.  A band item runs EVERY row step on the band path
+    // Three-step LPT.  A band item runs EVERY row step on the band path
     // (≈2.25× a uniform one at 8192²: 221.8 vs 98.6 µs per 112-row item,
     // profiles/r4_stamps48.txt), but costed by its band rows alone it looks
     // barely heavier than a uniform one, so waves that take one still get as
@@ -707,25 +618,17 @@ void DeviceSolver::setup_items() {
     // (6945-7169) starting 607-631 µs into a 722 µs span (a 33-40 µs tail).
     // Both ways of costing items by kind measured slower, on one box against
     // the round-4 build (profiles/r5_ab_kernel.txt, profiles/r5_ab_layout.txt):
-    // PE_LPT_KIND=1 — dealt in the band-row order (≈ chunk-major) but every
-    // wave's LOAD counts an item by its kind (rows + 2H fill steps × the kind's
-    // factor): 3632-3644 vs 3985-4005 it/s (the last rows' items then went to
-    // whichever waves were least loaded, a 110-123 µs tail); PE_LPT_KIND=2 —
-    // also ORDERED by kind cost: every band item in the first round, all over
+    // wave LOADS counted by kind (rows + 2H fill steps × the kind's factor):
+    // 3632-3644 vs 3985-4005 it/s (the last rows' items then went to
+    // whichever waves were least loaded, a 110-123 µs tail); items also
+    // ORDERED by kind cost: every band item in the first round, all over
     // the grid, 3519-3606 (the first round lost its row window; band items ran
     // 4.1 µs per row step instead of 1.8).  The round-4 tail (late items of the
     // last rows) is made of UNIFORM items whose waves ran slow — the wave-time
     // spread the static costs do not predict (r4 stamps: correlation -0.1).
-    // Default 0: band-row costs only.
-    const int lpt_kind = std::getenv("PE_LPT_KIND") ? std::atoi(std::getenv("PE_LPT_KIND")) : 0;
+    // Band-row costs only (the kind-cost knob was removed in round 6).
     std::vector<double> kcost(pcs.size());
-    for (size_t i = 0; i < pcs.size(); ++i) {
-      Piece& p = pcs[i];
-      const int2 e = entry(p.ib, p.rows, p.s);
-      const double f = (e.x & dev::kBandBit) ? fband : (e.x & dev::kUniBit) ? 1.0 : fmixed;
-      kcost[i] = steps_ >= 3 && lpt_kind > 0 ? double(p.rows + 2 * H) * f + overhead : p.cost;
-      if (steps_ >= 3 && lpt_kind == 2) p.cost = kcost[i];
-    }
+    for (size_t i = 0; i < pcs.size(); ++i) kcost[i] = pcs[i].cost;
     per.assign(size_t(W), {});
     load.assign(size_t(W), 0.0);
     std::vector<int> order;
@@ -764,39 +667,19 @@ void DeviceSolver::setup_items() {
       lay_mean_ += l / W;
     }
     lay_items_ = int(rounds);
-    // XCD-aware placement of the lists: the persistent grid's workgroup b runs
-    // on XCD b mod 8 (round-robin dispatch), and each XCD has its own L2.
-    // Consecutive lists hold neighbouring strips of the same rows (chunk-major
-    // LPT order), whose halo columns overlap: list w goes to a physical wave
-    // of XCD ⌊8w/W⌋, so each XCD marches a contiguous run of strips and the
-    // overlapped lines are fetched once into its L2 instead of once per XCD.
-    // Measured SLOWER (three-step 8192²: 3759 / 3778 it/s vs 4023 / 4031 with
-    // list w on physical wave w, alternating runs on one box —
-    // profiles/r3_three_ti.txt): opt-in PE_XCD_MAP=1.
+    // List w runs on physical wave w (the persistent grid's workgroup b runs
+    // on XCD b mod 8).  XCD-aware maps — each XCD marching a contiguous run of
+    // strips so shared halo lines are fetched once into its L2 — read 3-7 %
+    // fewer DRAM bytes but ran 0-12 % slower (profiles/r3_three_ti.txt,
+    // profiles/r5_dram_layout.txt); removed in round 6.
     std::vector<int> phys(static_cast<size_t>(W));
     {
-      const bool xmap = std::getenv("PE_XCD_MAP") && std::atoi(std::getenv("PE_XCD_MAP")) == 1;
       const int nb = W / dev::kWPB;
-      // PE_XCD_GROUP=g (opt-in): runs of g consecutive lists' workgroups on one
-      // XCD (g = 1: the default round-robin; PE_XCD_MAP=1 ≈ nb / 8)
-      const int xg = std::getenv("PE_XCD_GROUP") ? std::max(1, std::atoi(std::getenv("PE_XCD_GROUP"))) : 1;
-      size_t i = 0;
-      if (!xmap && xg > 1 && nb % (8 * xg) == 0) {
-        for (int lb = 0; lb < nb; ++lb) {
-          const int G = lb / xg, x = G % 8, slot = (G / 8) * xg + lb % xg;
-          for (int l = 0; l < dev::kWPB; ++l) phys[i++] = (slot * 8 + x) * dev::kWPB + l;
-        }
-      } else if (xmap) {
-        for (int x = 0; x < 8; ++x)
-          for (int b = x; b < nb; b += 8)
-            for (int l = 0; l < dev::kWPB; ++l) phys[i++] = b * dev::kWPB + l;
-      } else {
-        for (int w = 0; w < W; ++w) phys[i++] = w;
-      }
+      for (int w = 0; w < W; ++w) phys[size_t(w)] = w;
       // PE_WPERM (diagnostic: does a slow item stay slow on another wave?):
       // 1 lists on the workgroups in reverse order, 2 rotated by a quarter of
       // the grid (other co-resident workgroup pairs)
-      if (const char* e = std::getenv("PE_WPERM"); e && !xmap) {
+      if (const char* e = std::getenv("PE_WPERM")) {
         const int m = std::atoi(e);
         for (int w = 0; w < W; ++w) {
           const int b = w / dev::kWPB, l = w % dev::kWPB;

@@ -88,7 +88,7 @@ struct DevState {
 // peers[r] = rank r's buffer (2 × P slots of kP2PSlot doubles: n ≤ kP2PSlot-1
 // values + a sequence flag) mapped into this process, seq = this rank's
 // reduction counter (device), timeout in s_memrealtime ticks (100 MHz).
-constexpr int kP2PSlot = 32;  // ≥ 26 sums of the four-step sweep + the flag
+constexpr int kP2PSlot = 32;  // ≥ 19 sums of the three-step sweep + the flag
 struct PeerSum {
   double* const* peers;
   unsigned long long* seq;
@@ -98,6 +98,42 @@ struct PeerSum {
   // (and one count at wait_acc[1]) — DevState::xr_wait of the solver
   unsigned long long* wait_acc;
 };
+
+// Halo exchange by peer put over xGMI (p2p.hip kPut; DeviceSolver's "put"
+// halo path).  Every rank owns one fine-grained buffer, IPC-mapped into its
+// neighbours: per direction d (as seen by the owner) kPutParts flags, then
+// an inbox of 2 parities × `stride` doubles.  Message m (direction d) of one
+// launch: block part b copies its 1/kPutParts of `src` into the peer's inbox
+// slot for this rank (parity c & 1, c = the exchanges done towards d so far),
+// releases it (system scope) with flag = c + 1, waits for this rank's own
+// flag of that part (the peer's matching store), and copies the inbox part
+// into `dst`.  One launch per halo phase, no host involvement, no RCCL call;
+// a peer that never arrives poisons `dst` with NaN (the sweep then stops with
+// a non-finite status) instead of hanging.
+constexpr int kPutParts = 16;  // blocks per message; each waits only on its own part's flag
+constexpr int kPutFlagStride = 16;  // u64 words per part flag (one 128-B line each)
+struct PutMsg {
+  const double* src;                  // local send buffer
+  double* rbox;                       // the peer's inbox slot for this message (parity 0)
+  unsigned long long* rflag;          // the peer's flags of that slot (kPutParts × kPutFlagStride)
+  const double* lbox;                 // this rank's inbox slot of direction dir (parity 0)
+  const unsigned long long* lflag;    // this rank's flags of that slot
+  double* dst;                        // local receive buffer
+  long long n;                        // doubles
+  int dir;
+};
+struct PutArgs {
+  PutMsg m[4];
+  int nmsg;
+  long long stride;        // doubles between an inbox slot's two parities
+  unsigned* cnt;           // [0..3] exchanges done per direction, [4..7] part tickets (device, local)
+  long long timeout_ticks; // s_memrealtime ticks (100 MHz)
+};
+void launch_put(const PutArgs& a, hipStream_t s);
+// Set-up self-test of the put path: rank-coded values through the same
+// protocol (kPut with src = a device buffer of `code`), then *bad counts the
+// received values differing from each peer's code (codes[m] = the peer of m).
+void launch_put_check(const PutArgs& a, const double* codes, int* bad, hipStream_t s);
 
 // Per-block launch description.  Local indexing: (li, lj), li ∈ [0, nx+1],
 // lj ∈ [0, ny+1], element = base + li*pitch + lj.
@@ -181,17 +217,6 @@ struct KParams {
   double* hpush_hi[2];
   const double* hrecv;
   int push;
-  // In-kernel item-sum fold (dynamic sweeps, fold = 1): the wave that counts
-  // the last item of a group of kFoldGroup consecutive slots sums that group
-  // (fixed lane order) into gsum[g]; the last wave to leave the sweep — every
-  // wave has read the state by then — sums the groups in order and updates
-  // the state, so no separate reduction kernel runs.  Counters: gcnt[g] per
-  // group, xcnt[16·x] per XCD shard of exiting waves, xcnt[16·8] shards done;
-  // each is reset by the wave that completes it.
-  int fold;
-  unsigned* gcnt;
-  unsigned* xcnt;
-  double* gsum;
   // PE_FAULT_INJECT=slow@rank:R,us:X — this rank's final reduction block
   // idles X µs (in ticks) before the cross-rank sum (T_MPI test hook)
   long long slow_ticks;
@@ -217,7 +242,6 @@ struct KParams {
   // kernel entry (fused3.hip stage_first3; PE_STAGE=0: off)
   int stage;
 };
-constexpr int kFoldGroup = 64;
 // KParams::mlimit of the three-step replay launch (DevState::fixj)
 constexpr int kReplay3 = -2;
 
@@ -351,13 +375,7 @@ int resident_blocks_S2();
 // launch_S dispatches here when k.steps == 3.
 void launch_S3(const KParams& k, int par, hipStream_t s);
 int resident_blocks_S3();
-// Four-step sweep (fused4.hip): the same protocol for iterations K+1..K+4
-// (8-deep halo, 26 sums; state layout sc3 = {zc[4], α[4], β[4], g[4]});
-// launch_S dispatches here when k.steps == 4.
-void launch_S4(const KParams& k, int par, hipStream_t s);
-int resident_blocks_S4();
-constexpr int kNS4 = 26;         // four-step sweep: sums per sweep
-constexpr int sweep_sums(int steps) { return steps >= 3 ? 7 * steps - 2 : steps == 2 ? kNS2 : 7; }
+constexpr int sweep_sums(int steps) { return steps >= 3 ? kNS3 : steps == 2 ? kNS2 : 7; }
 // (k.ti / k.order select the kernel variant: set them first)
 int resident_blocks_classic(int variant);
 

@@ -27,7 +27,79 @@ __global__ void kP2PSum(double* d, int n, PeerSum ps) {
   if (int(threadIdx.x) < n) d[threadIdx.x] = v[threadIdx.x];
 }
 
+// Halo exchange by peer put (protocol: kernels.hpp PutArgs).  Block
+// (part b, message m): b = blockIdx / nmsg, so every message's part 0 is
+// dispatched before any part 1 — each block waits only for the SAME part of
+// its peer's message, and the in-order dispatch on both GPUs then guarantees
+// progress with as few as nmsg resident blocks (the overlap keeps 8 free).
+__global__ __launch_bounds__(256) void kPut(PutArgs a) {
+  const int m = int(blockIdx.x) % a.nmsg, b = int(blockIdx.x) / a.nmsg;
+  const PutMsg g = a.m[m];
+  __shared__ unsigned long long sc;
+  __shared__ int sok;
+  if (threadIdx.x == 0) {
+    sc = __hip_atomic_load(a.cnt + g.dir, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    sok = 1;
+  }
+  __syncthreads();
+  const unsigned long long c = sc;
+  const long long par = (long long)(c & 1ull) * a.stride;
+  const long long lo = g.n * b / kPutParts, hi = g.n * (b + 1) / kPutParts;
+  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) g.rbox[par + i] = g.src[i];
+  // every wave's remote stores complete before the flag (a system-scope
+  // release only waits for the releasing wave's own stores)
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __hip_atomic_store(g.rflag + size_t(b) * kPutFlagStride, c + 1, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    const unsigned long long* f = g.lflag + size_t(b) * kPutFlagStride;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) < c + 1) {
+      __builtin_amdgcn_s_sleep(1);
+      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > a.timeout_ticks) {
+        sok = 0;  // the peer never arrived: poison instead of hanging
+        break;
+      }
+    }
+  }
+  __syncthreads();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
+  const bool ok = sok != 0;
+  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x)
+    g.dst[i] = ok ? __hip_atomic_load(g.lbox + par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
+                  : __builtin_nan("");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    // the message's last part advances the direction's count (every part read
+    // it above, before its ticket)
+    const unsigned t = __hip_atomic_fetch_add(a.cnt + 4 + g.dir, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t == unsigned(kPutParts - 1)) {
+      __hip_atomic_store(a.cnt + 4 + g.dir, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(a.cnt + g.dir, unsigned(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void kPutCheck(PutArgs a, const double* codes, int* bad) {
+  const int m = int(blockIdx.x);
+  if (m >= a.nmsg) return;
+  const PutMsg g = a.m[m];
+  int nb = 0;
+  for (long long i = threadIdx.x; i < g.n; i += blockDim.x) nb += g.dst[i] != codes[m] + double(i % 7);
+  if (nb) atomicAdd(bad, nb);
+}
+
 }  // namespace
+
+void launch_put(const PutArgs& a, hipStream_t s) {
+  if (a.nmsg <= 0) return;
+  hipLaunchKernelGGL(kPut, dim3(unsigned(a.nmsg * kPutParts)), dim3(256), 0, s, a);
+}
+
+void launch_put_check(const PutArgs& a, const double* codes, int* bad, hipStream_t s) {
+  if (a.nmsg <= 0) return;
+  hipLaunchKernelGGL(kPutCheck, dim3(unsigned(a.nmsg)), dim3(256), 0, s, a, codes, bad);
+}
 
 void launch_p2p_sum(double* d, int n, const PeerSum& ps, hipStream_t s) {
   hipLaunchKernelGGL(kP2PSum, dim3(1), dim3(64), 0, s, d, n, ps);

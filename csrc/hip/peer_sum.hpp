@@ -72,53 +72,6 @@ __device__ __forceinline__ void peer_sum_block(const PeerSum& ps, double* v, int
   __syncthreads();
 }
 
-// The same protocol run by ONE wave (lane r talks to rank r; P ≤ 64): the
-// sweep's in-kernel item-sum fold ends in a single wave while the other waves
-// of its workgroup have already left, so no workgroup barrier is available.
-// v[0..n) is wave-uniform on entry and on exit.
-__device__ __forceinline__ void peer_sum_wave(const PeerSum& ps, double* v, int n) {
-  const int lane = int(threadIdx.x & 63);
-  unsigned long long q = 0;
-  if (lane == 0) {
-    q = *ps.seq + 1;
-    *ps.seq = q;
-  }
-  q = (unsigned long long)__builtin_amdgcn_readfirstlane(int(q & 0xffffffffu)) |
-      ((unsigned long long)__builtin_amdgcn_readfirstlane(int(q >> 32)) << 32);
-  const size_t set = size_t(q & 1);
-  int ok = 1;
-  const unsigned long long tw = __builtin_amdgcn_s_memrealtime();
-  if (lane < ps.P) {
-    double* dst = ps.peers[lane] + (set * size_t(ps.P) + size_t(ps.me)) * kP2PSlot;
-    for (int i = 0; i < n; ++i) dst[i] = v[i];
-    __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst + kP2PSlot - 1), q, __ATOMIC_RELEASE,
-                       __HIP_MEMORY_SCOPE_SYSTEM);
-    const unsigned long long* flag = reinterpret_cast<const unsigned long long*>(
-        ps.peers[ps.me] + (set * size_t(ps.P) + size_t(lane)) * kP2PSlot + kP2PSlot - 1);
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != q) {
-      __builtin_amdgcn_s_sleep(1);
-      if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ps.timeout_ticks) {
-        ok = 0;  // a peer never arrived: poison instead of hanging
-        break;
-      }
-    }
-  }
-  const bool all_ok = __ballot(ok == 0) == 0ull;
-  if (lane == 0 && ps.wait_acc) {
-    ps.wait_acc[0] += __builtin_amdgcn_s_memrealtime() - tw;
-    ps.wait_acc[1] += 1;
-  }
-  double s = 0.0;
-  if (lane < n)
-    for (int r = 0; r < ps.P; ++r)
-      s += __hip_atomic_load(ps.peers[ps.me] + (set * size_t(ps.P) + size_t(r)) * kP2PSlot + lane, __ATOMIC_RELAXED,
-                             __HIP_MEMORY_SCOPE_SYSTEM);
-  for (int i = 0; i < n; ++i) {
-    const double si = __shfl(s, i, 64);
-    v[i] = all_ok ? si : __builtin_nan("");
-  }
-}
 
 }  // namespace dev
 }  // namespace pe

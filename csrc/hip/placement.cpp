@@ -1,7 +1,6 @@
-// Memory placement of the solver fields: the allocation modes (plain,
-// physically contiguous, shuffled physical chunks) and the placement
-// search that picks, among a few candidate allocations, the one the sweep
-// streams fastest from (DeviceSolver::choose_placement / carve_placement).
+// Memory placement of the solver fields: the placement search that picks,
+// among a few candidate allocations, the one the sweep streams fastest from
+// (DeviceSolver::choose_placement).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
@@ -25,104 +24,29 @@
 namespace pe {
 
 namespace detail {
-// Field allocation.  PE_MALLOC=1 requests physically contiguous memory
-// (hipDeviceMallocContiguous); PE_MALLOC=2 builds the range from
-// PE_VMM_CHUNK_MB-sized physical chunks (default 2) mapped into one virtual
-// range in a shuffled order (virtual memory API) — experiments on the
-// allocation-dependent speed of the streaming sweep (docs/PERFORMANCE.md).
-namespace {
-struct VmmRange {
-  size_t size;
-  std::vector<hipMemGenericAllocationHandle_t> h;
-};
-std::mutex g_vmm_mu;
-std::map<void*, VmmRange> g_vmm;
-
-void* vmm_alloc_shuffled(size_t bytes) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  hipMemAllocationProp prop{};
-  prop.type = hipMemAllocationTypePinned;
-  prop.location.type = hipMemLocationTypeDevice;
-  prop.location.id = dev;
-  size_t gran = 0;
-  if (hipMemGetAllocationGranularity(&gran, &prop, hipMemAllocationGranularityMinimum) != hipSuccess || gran == 0)
-    return nullptr;
-  size_t chunk = size_t(2) << 20;
-  if (const char* e = std::getenv("PE_VMM_CHUNK_MB")) chunk = size_t(std::max(1, std::atoi(e))) << 20;
-  chunk = (chunk + gran - 1) / gran * gran;
-  const size_t n = (bytes + chunk - 1) / chunk, size = n * chunk;
-  void* va = nullptr;
-  if (hipMemAddressReserve(&va, size, chunk, nullptr, 0) != hipSuccess) return nullptr;
-  VmmRange r{size, std::vector<hipMemGenericAllocationHandle_t>(n)};
-  for (size_t i = 0; i < n; ++i)
-    if (hipMemCreate(&r.h[i], chunk, &prop, 0) != hipSuccess) {
-      for (size_t j = 0; j < i; ++j) (void)hipMemRelease(r.h[j]);
-      (void)hipMemAddressFree(va, size);
-      return nullptr;
-    }
-  // chunk i of the range ← physical chunk perm[i] (fixed-seed shuffle)
-  std::vector<size_t> perm(n);
-  for (size_t i = 0; i < n; ++i) perm[i] = i;
-  unsigned long long x = 0x9E3779B97F4A7C15ull;
-  for (size_t i = n; i > 1; --i) {
-    x ^= x << 13;
-    x ^= x >> 7;
-    x ^= x << 17;
-    std::swap(perm[i - 1], perm[size_t(x % i)]);
-  }
-  for (size_t i = 0; i < n; ++i)
-    PE_HIP_CHECK(hipMemMap(static_cast<char*>(va) + i * chunk, chunk, 0, r.h[perm[i]], 0));
-  hipMemAccessDesc acc{};
-  acc.location.type = hipMemLocationTypeDevice;
-  acc.location.id = dev;
-  acc.flags = hipMemAccessFlagsProtReadWrite;
-  PE_HIP_CHECK(hipMemSetAccess(va, size, &acc, 1));
-  std::lock_guard<std::mutex> g(g_vmm_mu);
-  g_vmm.emplace(va, std::move(r));
-  return va;
-}
-}  // namespace
-
-// mode: 0 hipMalloc, 1 physically contiguous, 2 shuffled physical chunks;
-// PE_MALLOC overrides.  nullptr when the device is out of memory.
-void* field_try_alloc(size_t bytes, int mode) {
+// Field allocation: plain hipMalloc.  (Physically contiguous memory and
+// shuffled physical chunks mapped through the virtual memory API were
+// measured as placement experiments in round 2 — contiguous slowest, chunks
+// fast on one box and slow on the next, profiles/r2_placement.txt — and
+// removed in round 6; the placement search below is what makes the speed
+// robust.)  nullptr when the device is out of memory.
+void* field_try_alloc(size_t bytes) {
   void* p = nullptr;
-  if (const char* e = std::getenv("PE_MALLOC")) mode = std::atoi(e);
-  if (mode == 2) {
-    if (void* v = vmm_alloc_shuffled(bytes)) return v;
-    (void)hipGetLastError();
-    mode = 0;  // no virtual memory API: plain allocation
-  }
-  const hipError_t r = mode == 1 ? hipExtMallocWithFlags(&p, bytes, hipDeviceMallocContiguous) : hipMalloc(&p, bytes);
-  if (r != hipSuccess) {
+  if (hipMalloc(&p, bytes) != hipSuccess) {
     (void)hipGetLastError();
     return nullptr;
   }
   return p;
 }
 
-void* field_alloc(size_t bytes, int mode) {
-  void* p = field_try_alloc(bytes, mode);
+void* field_alloc(size_t bytes) {
+  void* p = field_try_alloc(bytes);
   if (!p) PE_HIP_CHECK(hipErrorOutOfMemory);
   return p;
 }
 
 void field_free(void* p) {
-  if (!p) return;
-  {
-    std::lock_guard<std::mutex> g(g_vmm_mu);
-    auto it = g_vmm.find(p);
-    if (it != g_vmm.end()) {
-      (void)hipDeviceSynchronize();
-      (void)hipMemUnmap(p, it->second.size);
-      for (auto h : it->second.h) (void)hipMemRelease(h);
-      (void)hipMemAddressFree(p, it->second.size);
-      g_vmm.erase(it);
-      return;
-    }
-  }
-  (void)hipFree(p);
+  if (p) (void)hipFree(p);
 }
 }  // namespace detail
 
@@ -217,10 +141,6 @@ bool DeviceSolver::placement_search(bool retry) {
     }
   }
   if (tries <= 1) return true;
-  if (const char* e = std::getenv("PE_PLACEMENT"); e && std::string(e) == "carve") {
-    carve_placement();
-    return true;
-  }
   struct Cand {
     double *x0, *x1, *w;
     float ms;
@@ -243,14 +163,14 @@ bool DeviceSolver::placement_search(bool retry) {
       void* sp = nullptr;
       if (skip_gb > 0 && hipMalloc(&sp, size_t(skip_gb * double(1ull << 30))) != hipSuccess) break;
       if (sp) spacers.push_back(sp);
-      void* a = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
+      void* a = field_try_alloc(sizeof(double) * xsize_);
       if (!a) break;
-      void* b = field_try_alloc(sizeof(double) * xsize_, alloc_mode_);
+      void* b = field_try_alloc(sizeof(double) * xsize_);
       if (!b) {
         field_free(a);
         break;
       }
-      void* w = field_try_alloc(sizeof(double) * wsize_, alloc_mode_);
+      void* w = field_try_alloc(sizeof(double) * wsize_);
       if (!w) {
         field_free(a);
         field_free(b);
@@ -304,46 +224,6 @@ bool DeviceSolver::placement_search(bool retry) {
   placement_best_ = int(placement_ms_.size() + best);
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
   return fast || (sstep_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
-}
-
-// Placement experiment (PE_PLACEMENT=carve): the three arrays carved from ONE
-// allocation at x0 = base, x1 = base + X + d, w = base + 2X + 2d for a set of
-// offsets d, each timed like a search candidate — does the sweep's speed
-// depend on the arrays' relative offsets within the same physical memory?
-void DeviceSolver::carve_placement() {
-  static const size_t kD[] = {0, 4096, 65536, 262144, 1 << 20, 2 << 20, 3 << 20, 5 << 20, 7 << 20, 11 << 20, 13 << 20};
-  const size_t X = sizeof(double) * size_t(xsize_), W = sizeof(double) * size_t(wsize_);
-  const size_t dmax = size_t(16) << 20;
-  char* base = nullptr;
-  PE_HIP_CHECK(hipMalloc(&base, 2 * X + W + 2 * dmax + 4096));
-  double *o0 = fields_, *o1 = xalt_, *ow = walt_;
-  placement_ms_.clear();
-  float best = 0.f;
-  size_t bi = 0;
-  for (size_t i = 0; i < sizeof(kD) / sizeof(kD[0]); ++i) {
-    const size_t d = kD[i];
-    set_fused_fields(reinterpret_cast<double*>(base), reinterpret_cast<double*>(base + X + d),
-                     reinterpret_cast<double*>(base + 2 * X + 2 * d));
-    enqueue_init();
-    dev::launch_S(*kp_, 1, stream_);
-    for (int it = 0; it < 2; ++it) dev::launch_S(*kp_, it & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-    for (int it = 0; it < 6; ++it) dev::launch_S(*kp_, it & 1, stream_);
-    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-    PE_HIP_CHECK(hipEventSynchronize(t1_));
-    float ms = 0.f;
-    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-    placement_ms_.push_back(ms / 6.0f);
-    if (i == 0 || ms < best) {
-      best = ms;
-      bi = i;
-    }
-  }
-  // keep the separate allocations of the constructor (the carve block is an
-  // experiment); report the best offset's index
-  PE_HIP_CHECK(hipFree(base));
-  set_fused_fields(o0, o1, ow);
-  placement_best_ = int(bi);
 }
 
 }  // namespace pe

@@ -18,12 +18,10 @@ struct Range {
 using clk = std::chrono::steady_clock;
 inline double secs(clk::time_point a, clk::time_point b) { return std::chrono::duration<double>(b - a).count(); }
 
-// Field allocation (placement.cpp).  mode: 0 hipMalloc, 1 physically
-// contiguous, 2 shuffled physical chunks; PE_MALLOC overrides.
-// field_try_alloc returns nullptr when the device is out of memory,
-// field_alloc aborts with the HIP error instead.
-void* field_try_alloc(size_t bytes, int mode = 0);
-void* field_alloc(size_t bytes, int mode = 0);
+// Field allocation (placement.cpp): hipMalloc; field_try_alloc returns
+// nullptr when the device is out of memory, field_alloc throws.
+void* field_try_alloc(size_t bytes);
+void* field_alloc(size_t bytes);
 void field_free(void* p);
 }  // namespace detail
 }  // namespace pe

@@ -294,7 +294,7 @@ __device__ __forceinline__ double apply_row1(const KParams& k, const RowCtx& rx,
   return lap(k, in0 ? 1.0 : k.inv_eps, um, u0, un, ul, ur);
 }
 
-// Row scalars of a uniform row (fused3.hip / fused4.hip uniform items):
+// Row scalars of a uniform row (fused3.hip uniform items):
 // 1/h1², 1/h2² times the row's face coefficient, and 1/D (0 outside the
 // global interior rows).
 struct URow {

@@ -175,7 +175,6 @@ class DeviceSolver {
   // two iterations per sweep (fused2.hip)
   bool two_step() const { return sstep_; }     // a multi-iteration sweep (two- or three-step)
   int sweep_steps() const { return steps_; }   // iterations per sweep launch: 1, 2 or 3
-  bool segment_layout() const { return seg_layout_; }  // static layout of one tall segment per wave
   // LDS-resident single sweep (resident.hip): small single-rank blocks run
   // each chunk of iterations as one launch.  PE_RESIDENT=0 disables.
   bool resident() const { return resident_; }
@@ -184,6 +183,20 @@ class DeviceSolver {
   // Halo rows pushed by the sweep itself over xGMI (row slabs + in-sweep P2P
   // sums): no exchange call in the iteration, which is then graph-capturable.
   bool halo_push() const { return push_; }
+  // Halo exchange by the solver's own peer-put kernel (p2p.hip kPut) instead
+  // of the comm's exchange (RCCL grouped send / receive).
+  bool halo_put() const { return put_; }
+  // The iteration replays from captured hipGraphs (run_iterations(.., true)):
+  // no comm call inside it and no two-stream overlap
+  bool graphs_usable() const;
+  // Multi-rank halo path chosen at construction by timing the candidates on
+  // the job's own transport (max over ranks): "exchange", "put" or "push",
+  // "+overlap" when the exchange runs on the halo stream under the interior
+  // items; halo_candidates() = {path, µs per sweep} as timed ("forced: …" /
+  // "none: …" when there was nothing to choose).
+  const std::string& halo_path() const { return halo_path_; }
+  const std::vector<std::pair<std::string, double>>& halo_candidates() const { return halo_cands_; }
+  const std::string& put_status() const { return put_status_; }
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   int placement_choice() const { return placement_best_; }       // index into placement_ms()
@@ -245,7 +258,6 @@ class DeviceSolver {
   void create_halo_stream();
   void choose_placement();   // local search, then (multi-rank) the coordinated retry round
   bool placement_search(bool retry);  // local; true when the kept candidate is in the best class
-  void carve_placement();  // PE_PLACEMENT=carve experiment (relative offsets within one allocation)
   void measure_exchange();  // sets exchange_us_ (collective)
   void setup_resident();    // tile geometry, band-table size, buffers (single rank, small blocks)
   void set_items(int ti);   // item counts and persistent grids for `ti` rows per item
@@ -254,7 +266,14 @@ class DeviceSolver {
   // after_sweep: the halo of `buf` was produced by a sweep (with the halo
   // push: import it); false for the initial state (the comm's exchange).
   void enqueue_exchange(int buf, bool after_sweep = true);
-  void setup_halo_push();  // collective: decides push_ identically on every rank
+  void setup_halo_push();  // collective: maps the push's receive buffers (push_ok_) identically on every rank
+  void setup_halo_put();   // collective: maps the put's inboxes + self-test (put_ok_) identically on every rank
+  // collective: time the available halo paths (exchange / put / push, with and
+  // without the overlap) for a few sweeps each and keep the fastest (max over ranks)
+  void choose_halo_path();
+  void apply_halo_path(const std::string& path, bool overlap);  // switch path + re-lay the items
+  // one halo phase through the put kernel (put_) or the comm
+  void xfer(const std::vector<Exchange>& ex, hipStream_t s);
   void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
   // End-of-solve true residual (single-sweep layouts): w → the p-plane of
   // x[0], the sweep's halo exchange, then kResid into DevState::res
@@ -282,7 +301,6 @@ class DeviceSolver {
   void mark_end(hipStream_t s);
   void harvest(size_t n);  // read the first n records (their events have completed)
   hipGraphExec_t graph_for(int iters);
-  bool graphs_usable() const;
 
   Problem prob_;
   Block blk_;
@@ -297,7 +315,6 @@ class DeviceSolver {
   int hdep_ = 2;          // halo depth of the single-sweep layouts (2 / 4 / 6)
   int xorg_ = 1;          // columns stored left of column 0 (KParams::xorg)
   int64_t tab_lo_ = -1;   // first local index of the chord tables / row classes
-  bool seg_layout_ = false;  // static layout of tall equal-cost segments, one per wave (setup_items)
   double* fields_ = nullptr;  // classic: r, w, p0, p1 (alloc each); single-sweep: x0, x1, w
   double* xalt_ = nullptr;    // single-sweep: x1 (separate allocation)
   double* walt_ = nullptr;    // single-sweep: w
@@ -372,13 +389,24 @@ class DeviceSolver {
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials
   unsigned* res_ctr_ = nullptr;
-  void* fold_buf_ = nullptr;        // item-sum fold: counters, then group sums (KParams::gcnt/xcnt/gsum)
-  size_t fold_bytes_ = 0;           // its counter part (zeroed per solve)
   bool state_memcpy_ = false;       // PE_STATE_COPY=memcpy: per-chunk state read by hipMemcpyAsync
   void* stage_ = nullptr;           // pinned staging buffer of upload()
   size_t stage_bytes_ = 0;
-  int alloc_mode_ = 0;              // field allocation: 0 hipMalloc, 2 shuffled physical chunks (large blocks)
   bool push_ = false;               // in-sweep halo push (KParams::push)
+  bool push_ok_ = false;            // push set up on every rank: a halo-path candidate
+  bool push_loop_ = false;          // PE_PUSH_LOOPBACK diagnostic (own receive buffer)
+  bool put_ = false;                // halo phases through kPut (peer put) instead of comm_->exchange
+  bool put_ok_ = false;             // put set up and self-tested on every rank: a halo-path candidate
+  bool put_loop_ = false;           // PE_PUT_LOOPBACK: this rank is its own peer (one-GPU probes / tests)
+  bool want_overlap_ = false;       // the chosen path's overlap (setup_items)
+  void* put_buf_ = nullptr;         // fine-grained: [4 dirs][kPutParts] flags, then [4 dirs][2][put_stride_] inbox
+  std::vector<void*> put_peers_;    // every rank's put_buf_ mapped here
+  unsigned* put_cnt_ = nullptr;     // PutArgs::cnt (device)
+  int64_t put_stride_ = 0;          // doubles per inbox parity
+  double put_timeout_s_ = 120.0;    // a peer that never arrives poisons the halo after this long (PE_P2P_TIMEOUT_S)
+  std::string put_status_ = "off";
+  std::string halo_path_ = "none: one rank";
+  std::vector<std::pair<std::string, double>> halo_cands_;
   double* hrecv_ = nullptr;         // its fine-grained receive buffer [2][2][2 × pitch]
   std::vector<void*> hpeers_;       // every rank's receive buffer mapped here (comm_->map_peer_buffers)
   double exchange_us_ = 0;  // measured halo exchange (max over ranks), multi-rank only  // the first solve() carries the construction time

@@ -41,7 +41,7 @@ def build_parser():
     ap.add_argument("--max-iter", type=int, default=-1)
     ap.add_argument("--norm", choices=("weighted", "unweighted"), default="weighted")
     ap.add_argument("--variant", type=int, default=0, help="device arithmetic: 0 fast (default), 1 reference-exact")
-    ap.add_argument("--algo", choices=("auto", "classic", "fused", "two-step", "three-step", "four-step"), default="auto",
+    ap.add_argument("--algo", choices=("auto", "classic", "fused", "two-step", "three-step"), default="auto",
                     help="device iteration: fused single-sweep (1 kernel, 1 reduction), two-step / three-step (2 / 3 "
                          "iterations per sweep, 1 reduction per sweep) or classic (2 + 2)")
     ap.add_argument("--timing", action="store_true", help="per-phase device event timers")

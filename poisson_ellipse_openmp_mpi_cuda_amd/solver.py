@@ -62,6 +62,12 @@ class SolveReport:
     # the halo push's ("on" / "off: why" / "fallback: why"), the per-sweep sums' transport, and
     # hipDeviceCanAccessPeer toward every rank's device (1 / 0, -1 same device)
     overlap: bool = False  # the halo exchange runs on a second stream while the sweep's interior items run
+    halo_put: bool = False  # the halo phases go through the peer-put kernel (p2p.hip kPut), not the comm
+    # the halo path chosen at construction ("exchange" / "put" / "push" [+overlap]) and the candidates' timings
+    # ([path, us per sweep], max over ranks), the peer put's set-up status
+    halo_path: str = ""
+    halo_candidates: Optional[list] = None
+    put_status: str = ""
     p2p_sum_setup: str = ""
     push_status: str = ""
     sums: str = ""
@@ -88,7 +94,7 @@ class SolveReport:
         return d
 
 
-ALGOS = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4, "four-step": 5}
+ALGOS = {"auto": 0, "classic": 1, "fused": 2, "two-step": 3, "three-step": 4}
 
 
 def _options(init="zero", seed=1234, threads=1, chunk=0, graph=False, timing=False, check_tol=True, variant=0,
@@ -220,6 +226,10 @@ def solve(prob: EllipseProblem, backend: str = "hip", ranks: int = 1, threads: i
     rep.xr = bool(solver.xr)
     rep.halo_push = bool(solver.halo_push)
     rep.overlap = bool(solver.overlap)
+    rep.halo_put = bool(solver.halo_put)
+    rep.halo_path = str(solver.halo_path)
+    rep.halo_candidates = [[str(n), round(float(us), 2)] for n, us in solver.halo_candidates]
+    rep.put_status = str(solver.put_status)
     rep.p2p_sum_setup = str(nat.p2p_setup_status())
     rep.push_status = str(solver.push_status)
     rep.sums = str(solver.xr_status)

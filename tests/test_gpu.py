@@ -154,26 +154,6 @@ def test_fused_item_orders_deterministic(gpu, order, monkeypatch):
     np.testing.assert_allclose(a.w, c.w, rtol=0, atol=1e-10)
 
 
-@pytest.mark.parametrize("M,N", [(800, 1200), (2048, 2048)])
-def test_item_sum_fold_matches_reduction_kernel(gpu, M, N, monkeypatch):
-    """PE_FOLD=1: dynamic sweeps fold their per-item sums inside the sweep
-    (groups of 64 slots summed by the wave that completes the group, the
-    groups by the last wave to leave) instead of launching kRed: same
-    iteration count, w equal to rounding, bitwise reproducible run to run."""
-    monkeypatch.setenv("PE_ORDER", "3")
-    monkeypatch.setenv("PE_RESIDENT", "0")
-    monkeypatch.setenv("PE_FOLD", "1")
-    prob = EllipseProblem(M, N)
-    a = solve(prob, backend="hip", return_w=True, algo="fused")
-    b = solve(prob, backend="hip", return_w=True, algo="fused")
-    monkeypatch.setenv("PE_FOLD", "0")
-    c = solve(prob, backend="hip", return_w=True, algo="fused")
-    assert a.iters == b.iters and abs(a.iters - c.iters) <= 1
-    assert a.iters == {(800, 1200): 989, (2048, 2048): 1730}[(M, N)]
-    assert np.array_equal(a.w, b.w)
-    np.testing.assert_allclose(a.w, c.w, rtol=0, atol=1e-10)
-
-
 def test_virtual_ranks_golden_grid(gpu):
     rep = solve(EllipseProblem(1600, 2400), backend="hip-group", ranks=4)
     assert rep.iters == GOLDEN_ITERS[(1600, 2400, "weighted")]
@@ -326,36 +306,38 @@ def test_two_process_device_path_host_staged(gpu):
     assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
 
 
-@pytest.mark.parametrize("nproc,decomp,overlap,allreduce", [(4, "aspect", "1", "rccl"), (3, "aspect", "1", "rccl"),
-                                                        (4, "aspect", "0", "rccl"), (4, "aspect", "1", "p2p"),
-                                                        (2, "aspect", "0", "p2p"), (4, "aspect", "1", "p2p-kernel"),
-                                                        (3, "rows", "0", "p2p"), (4, "rows", "0", "p2p"),
-                                                        (3, "rows", "0", "p2p-exchange"), (3, "rows", "0", "p2p-dyn"),
-                                                        (4, "aspect", "0", "p2p-dyn")])
-def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
-    """4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
-    rows through the x phase of the single-sweep halo) — and 3×1 — match the
-    single-process solution (gathered w); with and without the boundary /
-    interior overlap on two streams; with the per-iteration sums through the
-    host-staged transport, through the P2P transport (IPC-mapped buffers of
-    the other processes) summed inside the sweep's final reduction block
-    ("p2p"), or through the standalone one-shot P2P kernel ("p2p-kernel",
-    PE_XR=0).  Row slabs with the in-sweep sums push their halo rows from the
-    sweep into the neighbours' receive buffers (no exchange call);
-    "p2p-exchange" (PE_HALO=exchange) keeps the exchange; "p2p-dyn" runs the
-    dynamic item queue (PE_ORDER=3) with the in-sweep fold of its item sums
-    (PE_FOLD=1), whose cross-rank sum is then done by one wave."""
+@pytest.mark.parametrize("nproc,decomp,allreduce,env", [
+    # the default path (no PE_HALO / PE_OVERLAP): chosen at construction by timing
+    (4, "aspect", "p2p", {}), (3, "rows", "p2p", {}), (4, "rows", "p2p", {}), (2, "aspect", "p2p", {}),
+    (4, "aspect", "rccl", {}),
+    # each path forced: the comm's exchange with the overlap on the default slabs
+    # (kSignal on a row slab, the multi-GPU default since round 5), the peer put
+    # (IPC-mapped inboxes of the other processes), the sweep's push
+    (3, "rows", "p2p", {"PE_HALO": "exchange", "PE_OVERLAP": "1"}),
+    (4, "rows", "p2p", {"PE_HALO": "put", "PE_OVERLAP": "1"}), (4, "aspect", "p2p", {"PE_HALO": "put"}),
+    (3, "rows", "p2p", {"PE_HALO": "push"}),
+    (3, "aspect", "rccl", {"PE_OVERLAP": "1"}), (4, "aspect", "p2p-kernel", {"PE_OVERLAP": "1"}),
+    # the single sweep and its overlap
+    (4, "aspect", "rccl", {"PE_OVERLAP": "1", "PE_STEPS": "1"}),
+])
+def test_multi_process_2d_host_staged(gpu, nproc, decomp, allreduce, env):
+    """3-4 processes on the one GPU, 2×2 blocks (y-strip phase, unpack, corner
+    rows through the x phase) and 3×1 / 4×1 row slabs, match the
+    single-process solution (gathered w).  The halo path is the construction's
+    choice — timed on this job's transport — or forced: the host-staged
+    transport's exchange (with the boundary / interior overlap on two
+    streams), the peer-put kernel through the other processes' IPC-mapped
+    inboxes, or the sweep's own push.  The per-iteration sums go through the
+    host-staged transport ("rccl"), the P2P transport summed inside the
+    sweep's final reduction block ("p2p"), or the standalone one-shot P2P
+    kernel ("p2p-kernel", PE_XR=0)."""
     from conftest import free_port
 
-    env = dict(os.environ, PE_COMM="host", PE_OVERLAP=overlap, PE_ALLREDUCE=allreduce.split("-")[0],
-               PE_P2P_TIMEOUT_S="60", PE_XR="0" if allreduce == "p2p-kernel" else "1",
-               PE_HALO="exchange" if allreduce == "p2p-exchange" else "push")
-    if overlap == "1":  # the boundary / interior overlap is a single-sweep feature
-        env["PE_STEPS"] = "1"
-    if allreduce == "p2p-dyn":
-        env["PE_ORDER"] = "3"
-        env["PE_FOLD"] = "1"
-    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{overlap}_{allreduce}.npy")
+    tag = "_".join(f"{k}{v}" for k, v in sorted(env.items()))
+    base = {k: v for k, v in os.environ.items() if k not in ("PE_HALO", "PE_OVERLAP", "PE_STEPS")}
+    env = dict(base, PE_COMM="host", PE_ALLREDUCE=allreduce.split("-")[0], PE_P2P_TIMEOUT_S="60",
+               PE_XR="0" if allreduce == "p2p-kernel" else "1", **env)
+    outp = os.path.join(ROOT, "gpurun_out", f"mp_w_{nproc}_{decomp}_{allreduce}_{tag}.npy")
     os.makedirs(os.path.dirname(outp), exist_ok=True)
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
@@ -365,12 +347,20 @@ def test_multi_process_2d_host_staged(gpu, nproc, decomp, overlap, allreduce):
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
     assert d["comm"] == ("p2p-allreduce+host-staged" if allreduce.startswith("p2p") else "host-staged")
-    assert d["xr"] == (allreduce in ("p2p", "p2p-exchange", "p2p-dyn"))
-    assert d["halo_push"] == (d["Py"] == 1 and allreduce in ("p2p", "p2p-dyn"))
-    # every split runs the three-step sweep (6-deep halo: pushed by the sweep on
-    # row slabs, else exchanged — 2-D blocks pack their y strips after the
-    # sweep); PE_STEPS=1 keeps the single sweep and its overlap
-    assert d["algo"] == ("fused" if overlap == "1" else "three-step"), d["algo"]
+    assert d["xr"] == (allreduce == "p2p")
+    path = d["halo_path"]
+    assert d["halo_push"] == path.startswith("push") and d["halo_put"] == path.startswith("put"), d
+    assert d["overlap"] == ("+overlap" in path), path
+    if "PE_HALO" in env:
+        assert path.startswith(env["PE_HALO"]), path
+    if "PE_OVERLAP" in env:
+        assert d["overlap"] == (env["PE_OVERLAP"] == "1"), path
+    if not allreduce.startswith("p2p"):  # no IPC-mapped transport: the exchange only
+        assert path.startswith("exchange"), path
+    elif "PE_HALO" not in env and "PE_OVERLAP" not in env:
+        names = [n for n, _ in d["halo_candidates"]]
+        assert "put" in names and "exchange" in names and ("push" in names) == (d["Py"] == 1 and d["xr"]), names
+    assert d["algo"] == ("fused" if env.get("PE_STEPS") == "1" else "three-step"), d["algo"]
     one = solve(EllipseProblem(300, 420), backend="hip", return_w=True)
     assert abs(d["iters"] - one.iters) <= 1
     w = np.load(outp)
@@ -430,6 +420,56 @@ def test_halo_push_selftest_failure_falls_back(gpu):
     assert d["sums"] == "in-sweep P2P over xGMI"
 
 
+def test_halo_put_selftest_failure_falls_back(gpu):
+    """A failed peer-put self-test on ONE rank (PE_FAULT_INJECT=puttest@rank:1)
+    takes the put out of every rank's candidates; the job solves correctly on
+    the path chosen among the rest."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60",
+               PE_FAULT_INJECT="puttest@rank:1")
+    env.pop("PE_HALO", None)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+           "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+           "--quiet", "--decomp", "rows", "400", "600"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert "halo put unavailable" in out.stderr
+    assert d["put_status"] == "fallback: self-test failed on a peer" and not d["halo_put"]
+    names = [n for n, _ in d["halo_candidates"]]
+    assert not any(n.startswith("put") for n in names) and "push" in names, names
+    assert d["iters"] == 546
+
+
+def test_halo_put_checkpoint_resume_bitwise(gpu, tmp_path):
+    """Row slabs exchanging through the peer put (3 processes, IPC-mapped
+    inboxes): a checkpointed and resumed job ends bitwise where the
+    uninterrupted one does (the put keeps no halo state of its own: its
+    counters restart with the new solvers on every rank)."""
+    from conftest import free_port
+
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="put")
+    ck = str(tmp_path / "ck")
+
+    def run(*extra):
+        outp = str(tmp_path / f"w{len(extra)}.npy")
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "3", "--master-addr",
+               "127.0.0.1", "--master-port", str(free_port()), "-m", "poisson_ellipse_openmp_mpi_cuda_amd", "--json",
+               "--quiet", "--decomp", "rows", "--dump", outp, *extra, "400", "600"]
+        out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stderr[-3000:]
+        d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+        assert d["halo_put"] and d["halo_path"].startswith("put"), d["halo_path"]
+        return d, np.load(outp)
+
+    full, wf = run("--checkpoint", ck, "--checkpoint-every", "200")
+    assert full["iters"] == 546 and os.path.exists(ck + ".r2")
+    res, wr = run("--resume", ck)
+    assert res["iters"] == full["iters"]
+    assert np.array_equal(wr, wf)
+
+
 def test_p2p_selftest_failure_falls_back(gpu):
     """A failed P2P-sum self-test on ONE rank (PE_FAULT_INJECT=p2ptest@rank:1):
     every rank keeps the base transport for the sums (so no in-sweep sum and
@@ -447,6 +487,7 @@ def test_p2p_selftest_failure_falls_back(gpu):
     assert d["ranks"] == 3 and not d["xr"] and not d["halo_push"] and d["comm"] == "host-staged"
     assert d["p2p_sum_setup"] == "fallback: self-test sum wrong on a peer"
     assert d["push_status"].startswith("off: no P2P transport") and d["sums"].startswith("allreduce launch")
+    assert d["put_status"].startswith("off: no P2P transport") and d["halo_path"].startswith("exchange")
     assert d["peer_access"] == [-1, -1, -1]  # one GPU shared by the ranks
     assert d["iters"] == 546
 
@@ -479,19 +520,20 @@ def test_halo_push_checkpoint_resume_bitwise(gpu, tmp_path):
     assert np.array_equal(wr, wf)
 
 
-@pytest.mark.parametrize("nproc", [2, 4])
-def test_bench_halo_push_graphs(gpu, nproc):
+@pytest.mark.parametrize("nproc,halo", [(2, "push"), (4, "push"), (3, "put")])
+def test_bench_halo_push_graphs(gpu, nproc, halo):
     """bench.py on row slabs over the P2P transport (processes sharing the
     one GPU, host-staged base transport for set-up only): the sweep pushes its
-    edge rows into the neighbours' IPC-mapped receive buffers, the in-sweep
-    sum's flags deliver them, and the iterations run as captured hipGraphs —
-    the timed steps are valid and the full solve converges in the
-    single-GPU iteration count."""
+    edge rows into the neighbours' IPC-mapped receive buffers (the in-sweep
+    sum's flags deliver them), or the peer-put kernel exchanges them through
+    the neighbours' inboxes — no comm call in the iteration either way, so the
+    iterations run as captured hipGraphs: the timed steps are valid and the
+    full solve converges in the single-GPU iteration count."""
     from conftest import free_port
 
     M = N = 1024
     one = solve(EllipseProblem(M, N), backend="hip")
-    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO="push")
+    env = dict(os.environ, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_HALO=halo, PE_OVERLAP="0")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
            "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.join(ROOT, "bench.py"),
            "--gpus", str(nproc), "--steps", "40", "--warmup", "4", "--grid", str(M), str(N), "--decomp", "rows",
@@ -501,7 +543,8 @@ def test_bench_halo_push_graphs(gpu, nproc):
     d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
     c = d["config"]
     assert c["decomposition"]["Px"] == nproc and c["decomposition"]["Py"] == 1
-    assert c["halo"] == "in-sweep xGMI push (graph-captured)", c
+    assert c["halo"] == ("in-sweep xGMI push" if halo == "push" else "peer put over xGMI (kPut)") + " (graph-captured)", c
+    assert c["halo_path"].startswith(halo)
     assert c["allreduce"] == "in-sweep P2P over xGMI"
     assert c["algo"].startswith("three-step")
     assert d["valid"] and d["converged"] and abs(d["iters_converged"] - one.iters) <= 1
@@ -901,18 +944,22 @@ def test_fast_coefficients_vs_assembly(gpu, nat, M, N, kw):
     assert rel.max() <= (inv_eps + 4.0) * np.spacing(1.0)
 
 
-@pytest.mark.parametrize("spec,P", [("4x2", 8), ("2x2", 4)])
+@pytest.mark.parametrize("spec,P", [("4x2", 8), ("2x2", 4), ("8x1", 8), ("4x1", 4)])
 def test_overlap_async_loopback_transport_bitwise(gpu, monkeypatch, spec, P):
-    """the halo/interior overlap through an ASYNCHRONOUS
-    transport that moves data.  The loopback delay transport waits 150 µs on
-    the stream (longer than a sweep of this block), then copies every send
-    buffer into its receive buffer with a stream-ordered device copy — no host
-    synchronisation anywhere, as with RCCL.  The same layout and kernel
-    (kSignal) run once with the exchange serialised on the solver stream
-    (PE_OV_DEBUG=2) and once on the halo stream (kWaitSig → pack → exchange →
-    unpack → event → next sweep): any ordering hole — the pack before the
-    boundary items' stores, the next sweep before the unpack — changes the
-    data, so the two must agree bitwise."""
+    """the halo/interior overlap through an
+    ASYNCHRONOUS transport that moves data, on 2-D blocks AND on the row slabs
+    that the multi-GPU default runs (kSignal on slabs: one phase).  The
+    loopback delay transport waits 150 µs on the stream (longer than a sweep
+    of this block), then copies every send buffer into its receive buffer with
+    a stream-ordered device copy — no host synchronisation anywhere, as with
+    RCCL.  The peer-put kernel in loopback (PE_PUT_LOOPBACK=1: the rank is its
+    own peer, each message lands in its own receive buffer through the inbox,
+    flags and all) moves the same data.  Every arm — exchange or put,
+    serialised on the solver stream (PE_OV_DEBUG=2), overlapped (kWaitSig →
+    pack → exchange → unpack on the halo stream → event → next sweep), or with
+    no overlap at all — must end bitwise where the serialised exchange does:
+    any ordering hole (the pack before the boundary items' stores, the next
+    sweep before the unpack, a put read before its flag) changes the data."""
     from poisson_ellipse_openmp_mpi_cuda_amd._loader import native
     from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
 
@@ -922,20 +969,78 @@ def test_overlap_async_loopback_transport_bitwise(gpu, monkeypatch, spec, P):
     g = D.grid(P, M, N, spec)
     blk = nat.decompose(M, N, g, P // 2)
     out = {}
-    for dbg in ("2", "0"):
-        monkeypatch.setenv("PE_OVERLAP", "1")
-        monkeypatch.setenv("PE_OV_DEBUG", dbg)
+    for halo in ("exchange", "put"):
+        for ov, dbg in (("1", "2"), ("1", "0"), ("0", "0")):
+            monkeypatch.setenv("PE_HALO", halo)
+            monkeypatch.setenv("PE_PUT_LOOPBACK", "1" if halo == "put" else "0")
+            monkeypatch.setenv("PE_OVERLAP", ov)
+            monkeypatch.setenv("PE_OV_DEBUG", dbg)
+            opt = nat.SolveOptions()
+            opt.check_tol = False
+            comm = nat.make_delay_comm(P, 150.0, 3.0, True)
+            s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
+            assert s.overlap == (ov == "1") and s.sweep_steps == 3
+            assert s.halo_put == (halo == "put"), (s.halo_path, s.put_status)
+            assert s.halo_path.startswith(halo + ("+overlap" if ov == "1" else "")), s.halo_path
+            s.reset()
+            s.run_iterations(45, False)
+            s.synchronize()
+            out[(halo, ov, dbg)] = (s.state(), s.w())
+            del s, comm
+    st0, w0 = out[("exchange", "1", "2")]
+    for key, (st1, w1) in out.items():
+        assert st0["iter"] == st1["iter"] and st0["status"] == st1["status"], key
+        assert st0["fs2"] == st1["fs2"], key
+        np.testing.assert_array_equal(w0, w1, err_msg=str(key))
+
+
+def test_halo_path_choice_follows_the_transport(gpu, monkeypatch):
+    """the multi-rank halo path is chosen at construction by
+    timing the candidates on the job's transport (here one rank's block of an
+    8-rank row-slab split of 4096², the loopback forms of the put and the push
+    on one GPU, the delay transport as the exchange).  The pick is the fastest
+    candidate as timed; with a 3 ms exchange every exchange arm loses to the
+    put / push; PE_HALO=exchange with a 400 µs exchange (several sweeps of this
+    block) picks the overlap, which hides part of it under the interior items;
+    PE_HALO_TUNE=0 times nothing."""
+    from poisson_ellipse_openmp_mpi_cuda_amd._loader import native
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+    nat = native()
+    M = N = 4096
+    prob = EllipseProblem(M, N)
+    blk = nat.decompose(M, N, D.grid(8, M, N, "8x1"), 3)
+    monkeypatch.delenv("PE_OVERLAP", raising=False)
+    monkeypatch.delenv("PE_HALO", raising=False)
+    monkeypatch.setenv("PE_PUT_LOOPBACK", "1")
+    monkeypatch.setenv("PE_PUSH_LOOPBACK", "1")
+
+    def build(ex_us):
         opt = nat.SolveOptions()
-        opt.check_tol = False
-        comm = nat.make_delay_comm(P, 150.0, 3.0, True)
-        s = nat.DeviceSolver(prob.to_native(), blk, comm, opt)
-        assert s.overlap and s.sweep_steps == 3
-        s.reset()
-        s.run_iterations(45, False)
-        s.synchronize()
-        out[dbg] = (s.state(), s.w())
-        del s, comm
-    (st0, w0), (st1, w1) = out["2"], out["0"]
-    assert st0["iter"] == st1["iter"] and st0["status"] == st1["status"]
-    assert st0["fs2"] == st1["fs2"]
-    np.testing.assert_array_equal(w0, w1)
+        comm = nat.make_delay_comm(8, ex_us, 0.0, True)
+        return nat.DeviceSolver(prob.to_native(), blk, comm, opt), comm
+
+    s, c = build(0.0)
+    cands = s.halo_candidates
+    names = [n for n, _ in cands]
+    for want in ("exchange", "exchange+overlap", "put", "put+overlap", "push"):
+        assert want in names, names
+    final = {}
+    for n, us in cands:  # a finalist's time is the min of its two timings
+        base = n.replace(" (again)", "")
+        final[base] = min(final.get(base, us), us)
+    assert s.halo_path == min(final, key=final.get), (s.halo_path, cands)
+    del s, c
+    s, c = build(3000.0)
+    assert s.halo_path in ("put", "put+overlap", "push"), (s.halo_path, s.halo_candidates)
+    ex = [us for n, us in s.halo_candidates if n.startswith("exchange")]
+    assert min(ex) > 3000.0
+    del s, c
+    monkeypatch.setenv("PE_HALO", "exchange")
+    s, c = build(400.0)
+    assert sorted(n for n, _ in s.halo_candidates[:2]) == ["exchange", "exchange+overlap"]
+    assert s.halo_path == "exchange+overlap" and s.overlap, s.halo_candidates
+    del s, c
+    monkeypatch.setenv("PE_HALO_TUNE", "0")
+    s, c = build(400.0)
+    assert s.halo_candidates == [] and s.halo_path == "exchange (PE_HALO_TUNE=0)" and not s.overlap

@@ -3,9 +3,11 @@
 The reference's stage 4 runs N MPI ranks on N GPUs with halo traffic and
 per-iteration allreduces between them (stage4-mpi+cuda/poisson_mpi_cuda2.cu:
 331-500, :842-925) and publishes 2-GPU rows (Этап_4_1213.pdf p.11-12).  These
-tests launch that path for N ∈ {2, 4, 8} with the default transport (RCCL
-send/recv for halos; the in-sweep P2P sum or ncclAllReduce for the scalars;
-the boundary-first halo/interior overlap on or off) and compare the gathered
+tests launch that path for N ∈ {2, 4, 8} with the default transport (the
+halo path the construction times fastest — RCCL send/recv, the peer-put
+kernel or the sweep's push, overlapped with the interior items or not — and
+each path forced; the in-sweep P2P sum or ncclAllReduce for the scalars) and
+compare the gathered
 solution and the iteration count with the single-GPU solve.  Each case is
 skipped unless the box has at least N GPUs (the gpurun boxes of this project
 have one: the same code paths run there through the host-staged transport in
@@ -58,20 +60,26 @@ def single():
 
 
 @pytest.mark.parametrize("nproc,decomp,allreduce,overlap,halo", [
-    (2, "device", "p2p", "1", "push"), (2, "2x1", "rccl", "0", "push"), (2, "1x2", "p2p", "1", "push"),
-    (4, "2x2", "p2p", "1", "push"), (4, "device", "rccl", "1", "push"), (4, "2x2", "rccl", "0", "push"),
-    (8, "device", "p2p", "1", "push"), (8, "device", "p2p", "0", "push"), (8, "4x2", "p2p", "1", "push"),
-    (8, "4x2", "rccl", "0", "push"),
-    # row slabs with the in-sweep P2P sums: halo rows pushed by the sweep over xGMI (or exchanged: PE_HALO)
-    (2, "rows", "p2p", "0", "push"), (4, "rows", "p2p", "0", "push"), (8, "rows", "p2p", "0", "push"),
-    (8, "rows", "p2p", "0", "exchange"),
+    # the DEFAULT path (no PE_HALO / PE_OVERLAP): the construction times the
+    # candidates on the real transport and keeps the fastest
+    (2, "device", "p2p", None, None), (2, "2x1", "rccl", None, None), (2, "1x2", "p2p", None, None),
+    (4, "2x2", "p2p", None, None), (4, "device", "rccl", None, None), (4, "2x2", "rccl", "0", None),
+    (8, "device", "p2p", None, None), (8, "4x2", "p2p", None, None), (8, "4x2", "rccl", None, None),
+    (8, "rows", "p2p", None, None),
+    # each path forced: the sweep's push, the peer put, the comm's exchange
+    (2, "rows", "p2p", "0", "push"), (8, "rows", "p2p", "0", "push"),
+    (4, "rows", "p2p", None, "put"), (8, "4x2", "p2p", "1", "put"),
+    (8, "rows", "p2p", "1", "exchange"),
 ])
 def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, overlap, halo, tmp_path):
     _need(nproc)
     from conftest import free_port
 
-    env = dict(os.environ, PE_ALLREDUCE=allreduce, PE_OVERLAP=overlap, PE_P2P_TIMEOUT_S="30",
-               PE_WATCHDOG_S="60", PE_HALO=halo)
+    env = dict(os.environ, PE_ALLREDUCE=allreduce, PE_P2P_TIMEOUT_S="30", PE_WATCHDOG_S="60")
+    for k, v in (("PE_OVERLAP", overlap), ("PE_HALO", halo)):
+        env.pop(k, None)
+        if v is not None:
+            env[k] = v
     env.pop("PE_COMM", None)
     outp = str(tmp_path / "w.npy")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", str(nproc),
@@ -83,17 +91,30 @@ def test_rccl_torchrun_matches_single(gpu, single, nproc, decomp, allreduce, ove
     assert d["ranks"] == nproc and d["Px"] * d["Py"] == nproc
     assert d["comm"].endswith("rccl")
     assert d["comm"].startswith("p2p-allreduce") == (allreduce == "p2p")
-    assert d["halo_push"] == (d["Py"] == 1 and allreduce == "p2p" and halo == "push")
+    # the halo path: forced, or the fastest candidate as timed (every candidate listed)
+    path = d["halo_path"]
+    assert d["halo_push"] == path.startswith("push") and d["halo_put"] == path.startswith("put"), d
+    assert d["overlap"] == ("+overlap" in path)
+    if halo:
+        assert path.startswith(halo), path
+    if overlap is not None:
+        assert d["overlap"] == (overlap == "1"), path
+    if allreduce == "rccl":  # no IPC-mapped P2P transport: neither the put nor the push
+        assert path.startswith("exchange"), path
+    if halo is None and overlap is None:
+        names = [n for n, _ in d["halo_candidates"]]
+        assert "exchange" in names and "exchange+overlap" in names, names
+        if allreduce == "p2p":
+            assert "put" in names and "put+overlap" in names, (names, d["put_status"])
+            assert ("push" in names) == (d["Py"] == 1), names
     # first cross-device run labels (rank 0): distinct GPUs, peer access to each
     # (xGMI), every self-tested set-up passed, and the transports they chose
     assert len(d["peer_access"]) == nproc and d["peer_access"][0] == -1
     assert all(v == 1 for v in d["peer_access"][1:]), d["peer_access"]
     if allreduce == "p2p":
         assert d["p2p_sum_setup"] == "ok" and d["sums"] == "in-sweep P2P over xGMI"
-    assert d["push_status"] == ("on" if d["halo_push"] else d["push_status"]) and (d["halo_push"] or
-                                                                                  d["push_status"].startswith("off"))
+        assert d["put_status"] == "available", d["put_status"]
     # every block of 600×840 keeps >= 12 rows and columns: three-step everywhere
-    # (row slabs push their halos, 2-D blocks exchange them through RCCL)
     assert d["algo"] == "three-step", d["algo"]
     assert abs(d["iters"] - single.iters) <= 1
     np.testing.assert_allclose(np.load(outp), single.w, rtol=0, atol=1e-9)
@@ -132,12 +153,14 @@ def test_bench_multi_gpu_contract(gpu, nproc):
     assert c["decomposition"]["Px"] * c["decomposition"]["Py"] == nproc
     assert "rccl" in c["transport"]
     # 2047 rows: slabs while every rank keeps >= 32 rows (decomp.cpp: every N here); the
-    # halo is exchanged (the sweep pushes it only with PE_HALO=push, round 5)
-    assert c["halo"].startswith("exchange")
+    # halo path is the construction's fastest candidate on the real transport
+    names = [n for n, _ in c["halo_candidates_us_per_sweep"]]
+    assert c["halo_path"] in names and "exchange" in names and "put" in names, c["halo_path"]
+    assert ("push" in names) == (c["decomposition"]["Py"] == 1), names
     for r in c["ranks"]:  # per-rank diagnostics of the first cross-device run
         assert r["p2p_sum_setup"] == "ok" and r["sums"] == "in-sweep P2P over xGMI"
-        assert r["halo_push"] == ("off: exchange (PE_HALO=push pushes from the sweep)" if c["decomposition"]["Py"] == 1
-                                  else "off: 2-D blocks (RCCL exchange)")
+        assert r["halo_put"] == "available"
+        assert r["halo_push"] == ("available" if c["decomposition"]["Py"] == 1 else "off: 2-D blocks")
         assert all(v == 1 for k, v in r["peer_access"].items() if int(k) != r["rank"])
 
 

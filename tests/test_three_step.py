@@ -158,6 +158,14 @@ def test_three_step_checkpoint_resume_bitwise(gpu, tmp_path):
     assert np.array_equal(res.w, full.w)
     with pytest.raises(RuntimeError, match="has the three-step layout.*pass --algo three-step"):  # not resumable here
         solve(prob, backend="hip", algo="two-step", resume=ck)
+    # a layout code this build does not know (header field `fused`, byte 32):
+    # a readable error, never an out-of-range table lookup
+    raw = bytearray(open(ck + ".r0", "rb").read())
+    raw[32:36] = (9).to_bytes(4, "little", signed=True)
+    bad = str(tmp_path / "bad")
+    open(bad + ".r0", "wb").write(bytes(raw))
+    with pytest.raises(RuntimeError, match=r"has the unknown \(steps=9\) layout.*runs three-step"):
+        solve(prob, backend="hip", algo=THREE, resume=bad)
 
 
 def test_three_step_breakdown_and_nonfinite(gpu, monkeypatch):
