@@ -55,10 +55,13 @@ ProcessGrid process_grid_from_spec(const std::string& spec, int P, int M, int N)
   if (spec == "cols") return choose_process_grid(P, M, N, DecompMode::Cols);
   // "device": the GPU solver's preference — P×1 row slabs while every rank
   // keeps >= 32 rows, else the aspect rule.  Both run the three-step sweep
-  // (three iterations per pass): slabs push their 6-row halo from the sweep
-  // itself over xGMI (one contiguous message per side, no strided strips), 2-D
-  // blocks exchange theirs through RCCL after (or, overlapped, during) each
-  // sweep; the single sweep remains only for blocks under 12 rows / columns.
+  // (three iterations per pass); a slab's 6-row halo is one contiguous
+  // message per side (no strided strips), a 2-D block adds the packed y
+  // strips.  How it travels — the comm's RCCL exchange, the peer-put kernel
+  // or (slabs) the sweep's own push, overlapped with the interior items or not
+  // — the solver's construction decides by timing them on the job's transport
+  // (DeviceSolver::choose_halo_path); the single sweep remains only for blocks
+  // under 12 rows / columns.
   // Per rank block, zero-latency transport, measured with the two-step sweep
   // (profiles/r3_block_probe.txt): 4096² on 8 ranks 28.3 µs/iter as 8×1 vs
   // 39.8 as 4×2, on 4 ranks 41.2 vs 59.7 (4×1 / 2×2); 2048² on 8: 23.4 vs

@@ -26,6 +26,8 @@
 #include <limits>
 #include <thread>
 
+#include <unistd.h>
+
 #include <rocprofiler-sdk-roctx/roctx.h>
 
 #include "../hip/kernels.hpp"
@@ -148,52 +150,65 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // gathered 64 ranks per collective (the comms' host scratch size); a failure
   // leaves the diagnostics empty and never aborts construction.
   if (comm_->size() > 1) {
-    try {
-      const int P = comm_->size();
-      auto pci_key = [](int dv) -> double {
-        int dom = 0, bus = -1, dev = 0;
-        if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dv) != hipSuccess ||
-            hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dv) != hipSuccess ||
-            hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, dv) != hipSuccess) {
-          (void)hipGetLastError();
-          return -1.0;
-        }
-        return double((int64_t(dom) << 16) | (int64_t(bus) << 8) | int64_t(dev));
-      };
-      int mydev = 0, ndev = 0;
-      PE_HIP_CHECK(hipGetDevice(&mydev));
-      PE_HIP_CHECK(hipGetDeviceCount(&ndev));
-      const double mykey = pci_key(mydev);
-      std::vector<double> keys(size_t(P), -1.0);
-      for (int c0 = 0; c0 < P; c0 += 64) {
-        const int n = std::min(64, P - c0);
-        double chunk[64];
-        for (int i = 0; i < n; ++i) chunk[i] = c0 + i == comm_->rank() ? mykey : -1.0;
-        comm_->host_max(chunk, n, stream_);
-        for (int i = 0; i < n; ++i) keys[size_t(c0 + i)] = chunk[i];
+    // key = (host hash << 32) | PCI domain / bus / device: exact in a double
+    // (52 bits), so GPUs of different nodes never compare equal.  Every rank
+    // runs every collective round whatever failed locally (a failure only
+    // turns its own contribution into -1).
+    const int P = comm_->size();
+    auto host_hash = []() -> int64_t {
+      char name[256] = {0};
+      if (gethostname(name, sizeof(name) - 1) != 0) return 0;
+      uint64_t h = 1469598103934665603ull;  // FNV-1a
+      for (const char* c = name; *c; ++c) h = (h ^ uint64_t(uint8_t(*c))) * 1099511628211ull;
+      return int64_t((h ^ (h >> 20) ^ (h >> 40)) & 0xFFFFF);
+    };
+    const int64_t hh = host_hash();
+    auto pci_key = [hh](int dv) -> double {
+      int dom = 0, bus = -1, dev = 0;
+      if (hipDeviceGetAttribute(&dom, hipDeviceAttributePciDomainID, dv) != hipSuccess ||
+          hipDeviceGetAttribute(&bus, hipDeviceAttributePciBusId, dv) != hipSuccess ||
+          hipDeviceGetAttribute(&dev, hipDeviceAttributePciDeviceId, dv) != hipSuccess) {
+        (void)hipGetLastError();
+        return -1.0;
       }
-      std::vector<int> pa(size_t(P), -1);
-      for (int r = 0; r < P; ++r) {
-        const double key = keys[size_t(r)];
-        if (key < 0 || key == mykey) continue;
-        int d = -1;
-        for (int i = 0; i < ndev && d < 0; ++i)
-          if (pci_key(i) == key) d = i;
-        if (d < 0) {
-          pa[size_t(r)] = -2;
-          continue;
-        }
-        int can = 0;
-        if (hipDeviceCanAccessPeer(&can, mydev, d) != hipSuccess) {
-          (void)hipGetLastError();
-          can = 0;
-        }
-        pa[size_t(r)] = can;
-      }
-      peer_access_ = std::move(pa);
-    } catch (const std::exception&) {
-      peer_access_.clear();
+      return double((hh << 32) | (int64_t(dom & 0xFFFF) << 16) | (int64_t(bus & 0xFF) << 8) | int64_t(dev & 0xFF));
+    };
+    int mydev = -1, ndev = 0;
+    if (hipGetDevice(&mydev) != hipSuccess || hipGetDeviceCount(&ndev) != hipSuccess) {
+      (void)hipGetLastError();
+      mydev = -1;
+      ndev = 0;
     }
+    const double mykey = mydev >= 0 ? pci_key(mydev) : -1.0;
+    std::vector<double> keys(size_t(P), -1.0);
+    for (int c0 = 0; c0 < P; c0 += 64) {
+      const int n = std::min(64, P - c0);
+      double chunk[64];
+      for (int i = 0; i < n; ++i) chunk[i] = c0 + i == comm_->rank() ? mykey : -1.0;
+      comm_->host_max(chunk, n, stream_);
+      for (int i = 0; i < n; ++i) keys[size_t(c0 + i)] = chunk[i];
+    }
+    for (int r = 0; r < P; ++r)
+      if (r != comm_->rank() && mykey >= 0 && keys[size_t(r)] == mykey) shared_dev_ = true;
+    std::vector<int> pa(size_t(P), -1);
+    for (int r = 0; r < P && mykey >= 0; ++r) {
+      const double key = keys[size_t(r)];
+      if (key < 0 || key == mykey) continue;
+      int d = -1;
+      for (int i = 0; i < ndev && d < 0; ++i)
+        if (pci_key(i) == key) d = i;
+      if (d < 0) {
+        pa[size_t(r)] = -2;
+        continue;
+      }
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, mydev, d) != hipSuccess) {
+        (void)hipGetLastError();
+        can = 0;
+      }
+      pa[size_t(r)] = can;
+    }
+    peer_access_ = std::move(pa);
   }
   KParams& k = *kp_;
   std::memset(&k, 0, sizeof(KParams));
@@ -943,6 +958,10 @@ void DeviceSolver::xfer(const std::vector<Exchange>& ex, hipStream_t s) {
   a.stride = put_stride_;
   a.cnt = put_cnt_;
   a.timeout_ticks = (long long)(put_timeout_s_ * 1e8);
+  // 64 blocks per message alone on the GPU (8x1 block of 8192², one GPU,
+  // loopback: 134 vs 141 µs per sweep at 16); 8 under the overlap, whose
+  // halo stream gets the 8 blocks the sweep leaves free (64: 164 vs 140)
+  a.parts = want_overlap_ ? 8 : dev::kPutParts;
   for (size_t m = 0; m < ex.size(); ++m) {
     const Exchange& e = ex[m];
     if (e.count > put_stride_) throw std::logic_error("put: message larger than the inbox");
@@ -1015,7 +1034,11 @@ void DeviceSolver::choose_halo_path() {
   if (put_ok_) add("put", false);
   if (push_ok_ && !(ov && std::atoi(ov) != 0)) cands.push_back(Cand{"push", false, 0.0});
   if (ex_ok) add("exchange", true);
-  if (put_ok_) add("put", true);
+  // (not when ranks share a GPU — test jobs: put blocks spinning on the halo
+  // stream under another process's persistent sweep can starve it of CUs; a
+  // 6-process 2×3 job on one GPU stalled past 3 minutes, round 6)
+  const bool put_ov_forced = hm && std::string(hm) == "put" && ov && std::atoi(ov) != 0;
+  if (put_ok_ && (!shared_dev_ || put_ov_forced)) add("put", true);
   if (cands.empty()) cands.push_back(Cand{"exchange", ov && std::atoi(ov) != 0 && ov_able, 0.0});
   auto name = [](const Cand& c) { return c.path + (c.ov ? "+overlap" : ""); };
   const bool tune = !(std::getenv("PE_HALO_TUNE") && std::atoi(std::getenv("PE_HALO_TUNE")) == 0);
@@ -1794,7 +1817,7 @@ SolveResult DeviceSolver::solve() {
     // same iterate.
     const bool three = fused_ && steps_ >= 3;  // (three-step: the moment recurrence)
     enqueue_wflush();
-    // (the check below is timed on its own: res.t.check, outside T_iterate / T_solver)
+    // (the check below is timed on its own: res.t.check, outside T_iterate, inside T_solver)
     PE_HIP_CHECK(hipStreamSynchronize(stream_));
     const auto t_chk = clk::now();
     if (three) {  // (after a fix-up: x[wpar] ← the r of the returned w)
@@ -1912,7 +1935,11 @@ SolveResult DeviceSolver::solve() {
     res.t.dot_fused = !(fused_ && kp_->order == 3);
     if (nit == 0) res.t.gpu = ms * 1e-3;  // sampling off: the loop's device span
   }
-  res.t.solver = construct + secs(t_start, clk::now()) - check_s;
+  // T_solver spans the whole solve, the end-of-solve residual check included
+  // (it drives the residual-replacement restart: part of the solve, as the
+  // reference's time_solver spans its whole gradient_solver_mpi call); t_check
+  // reports it separately and T_iterate excludes it
+  res.t.solver = construct + secs(t_start, clk::now());
   // Timers: max over ranks (reference MPI_Reduce(MAX), :962-966).
   double tv[11] = {res.t.gpu, res.t.copy, res.t.halo, res.t.reduce, res.t.setup, res.t.solver, res.t.iterate,
                    res.t.dot, res.t.construct, res.t.wait, res.t.check};

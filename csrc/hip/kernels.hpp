@@ -110,7 +110,7 @@ struct PeerSum {
 // into `dst`.  One launch per halo phase, no host involvement, no RCCL call;
 // a peer that never arrives poisons `dst` with NaN (the sweep then stops with
 // a non-finite status) instead of hanging.
-constexpr int kPutParts = 16;  // blocks per message; each waits only on its own part's flag
+constexpr int kPutParts = 64;  // most blocks per message (PutArgs::parts); each waits only on its own part's flag
 constexpr int kPutFlagStride = 16;  // u64 words per part flag (one 128-B line each)
 struct PutMsg {
   const double* src;                  // local send buffer
@@ -127,6 +127,7 @@ struct PutArgs {
   int nmsg;
   long long stride;        // doubles between an inbox slot's two parities
   unsigned* cnt;           // [0..3] exchanges done per direction, [4..7] part tickets (device, local)
+  int parts;               // blocks per message (≤ kPutParts; the same on every rank)
   long long timeout_ticks; // s_memrealtime ticks (100 MHz)
 };
 void launch_put(const PutArgs& a, hipStream_t s);

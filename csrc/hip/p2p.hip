@@ -44,8 +44,19 @@ __global__ __launch_bounds__(256) void kPut(PutArgs a) {
   __syncthreads();
   const unsigned long long c = sc;
   const long long par = (long long)(c & 1ull) * a.stride;
-  const long long lo = g.n * b / kPutParts, hi = g.n * (b + 1) / kPutParts;
-  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x) g.rbox[par + i] = g.src[i];
+  const long long lo = g.n * b / a.parts, hi = g.n * (b + 1) / a.parts;
+  // 4 loads in flight per lane before their stores (the remote stores are
+  // write-through: the copy is bound by how many are outstanding)
+  const int T = int(blockDim.x);
+  long long i = lo + threadIdx.x;
+  for (; i + 3 * T < hi; i += 4 * T) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = g.src[i + u * T];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g.rbox[par + i + u * T] = v[u];
+  }
+  for (; i < hi; i += T) g.rbox[par + i] = g.src[i];
   // every wave's remote stores complete before the flag (a system-scope
   // release only waits for the releasing wave's own stores)
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
@@ -65,15 +76,22 @@ __global__ __launch_bounds__(256) void kPut(PutArgs a) {
   __syncthreads();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   const bool ok = sok != 0;
-  for (long long i = lo + threadIdx.x; i < hi; i += blockDim.x)
-    g.dst[i] = ok ? __hip_atomic_load(g.lbox + par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM)
-                  : __builtin_nan("");
+  i = lo + threadIdx.x;
+  for (; i + 3 * T < hi; i += 4 * T) {
+    double v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = __hip_atomic_load(g.lbox + par + i + u * T, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) g.dst[i + u * T] = ok ? v[u] : __builtin_nan("");
+  }
+  for (; i < hi; i += T)
+    g.dst[i] = ok ? __hip_atomic_load(g.lbox + par + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) : __builtin_nan("");
   __syncthreads();
   if (threadIdx.x == 0) {
     // the message's last part advances the direction's count (every part read
     // it above, before its ticket)
     const unsigned t = __hip_atomic_fetch_add(a.cnt + 4 + g.dir, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t == unsigned(kPutParts - 1)) {
+    if (t == unsigned(a.parts - 1)) {
       __hip_atomic_store(a.cnt + 4 + g.dir, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       __hip_atomic_store(a.cnt + g.dir, unsigned(c + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
@@ -93,7 +111,7 @@ __global__ __launch_bounds__(256) void kPutCheck(PutArgs a, const double* codes,
 
 void launch_put(const PutArgs& a, hipStream_t s) {
   if (a.nmsg <= 0) return;
-  hipLaunchKernelGGL(kPut, dim3(unsigned(a.nmsg * kPutParts)), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(kPut, dim3(unsigned(a.nmsg * a.parts)), dim3(256), 0, s, a);
 }
 
 void launch_put_check(const PutArgs& a, const double* codes, int* bad, hipStream_t s) {

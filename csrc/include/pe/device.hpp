@@ -399,6 +399,7 @@ class DeviceSolver {
   bool put_ok_ = false;             // put set up and self-tested on every rank: a halo-path candidate
   bool put_loop_ = false;           // PE_PUT_LOOPBACK: this rank is its own peer (one-GPU probes / tests)
   bool want_overlap_ = false;       // the chosen path's overlap (setup_items)
+  bool shared_dev_ = false;         // another rank of the job runs on this rank's GPU (test jobs)
   void* put_buf_ = nullptr;         // fine-grained: [4 dirs][kPutParts] flags, then [4 dirs][2][put_stride_] inbox
   std::vector<void*> put_peers_;    // every rank's put_buf_ mapped here
   unsigned* put_cnt_ = nullptr;     // PutArgs::cnt (device)

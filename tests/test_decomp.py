@@ -100,7 +100,7 @@ def test_thread_ranks_explicit_grid_matches_serial(spec):
 
 
 def test_device_spec_falls_back_to_aspect_for_thin_slabs():
-    # row slabs (the two-step sweep's halo push) while every rank keeps >= 32
+    # row slabs (one contiguous halo message per side) while every rank keeps >= 32
     # rows: 8192² on 8 ranks → 8×1, 4096² on 16 → 16×1; 128 ranks on 2048²
     # would leave 15 rows → the aspect rule
     assert D.process_grid(8, 8192, 8192, "device") == (8, 1)

@@ -1,0 +1,16 @@
+# Round 6, fourth GPU call: the remaining new tests, the halo probe on the
+# 8192^2 splits (each path forced, delays 0/0, 15/8, 60/8 us), the 1-GPU bench,
+# then the whole GPU suite.
+set -o pipefail
+R=$GRAFT_REPO_ROOT; O=$R/gpurun_out/r6fourth; mkdir -p $O
+cd $R
+timeout -k 10 600 python -u -m pytest -x -v --timeout 300 --timeout-method thread tests/test_gpu.py \
+  -k "loopback_transport_bitwise or halo_path_choice" > $O/new_tests.txt 2>&1 || { tail -40 $O/new_tests.txt; exit 1; }
+grep -E "passed|failed" $O/new_tests.txt | tail -3
+PROBE_EACH=1 PROBE_ITERS=300 timeout -k 10 400 python -u tools/halo_probe.py 0 0 15 8 60 8 > $O/halo_probe.txt 2>&1 || { tail -20 $O/halo_probe.txt; exit 1; }
+cat $O/halo_probe.txt
+timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 > $O/bench.txt 2>&1 || { tail -20 $O/bench.txt; exit 1; }
+tail -1 $O/bench.txt | cut -c1-300
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > $O/gpu_tests.txt 2>&1 || { tail -30 $O/gpu_tests.txt; exit 1; }
+tail -3 $O/gpu_tests.txt
+echo EXIT 0
