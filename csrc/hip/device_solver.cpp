@@ -84,7 +84,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // transport of ≥ 4s rows per rank (the 2s-deep halo comes from one
   // neighbour and the pushed edge rows are distinct).  Every input is global: every rank
   // decides the same.  algo 3 / 4 force two / three steps; auto takes three
-  // where it can (PE_STEPS=1/2/3 overrides; PE_TWO=0 keeps one).
+  // where it can (PE_STEPS=1/2/3 caps the iterations per sweep).
   {
     auto single = [&](int64_t m) { return comm_->size() == 1 && blk_.Px * blk_.Py == 1 && blk_.nx >= m && blk_.ny >= m; };
     auto slabs = [&](int64_t m) {
@@ -128,7 +128,6 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       }
     }
     bool auto_ms = slabs(8) || grid2d(12) || vgroup(12) || !resident_likely;
-    if (const char* e = std::getenv("PE_TWO")) auto_ms = std::atoi(e) != 0;
     int want = 3;
     if (const char* e = std::getenv("PE_STEPS")) want = std::max(1, std::min(3, std::atoi(e)));
     steps_ = 1;
@@ -236,7 +235,6 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // 64 loaded straddled 64-B segments: partial writes from two strips, and
     // 5 lines touched for 4 lines of data).
     if (steps_ >= 3) plane_ = ((xorg_ + fsw_ * (strips - 1) + 64 - dev::kHL3 + 1 + 15) / 16) * 16;
-    if (const char* e = std::getenv("PE_PAD")) plane_ += 8 * ((std::max(0, std::atoi(e)) + 7) / 8);
     const int64_t rows = nx + 2 * hdep_ + 2;
     xsize_ = ((rows * 2 * plane_ + 64 + 31) / 32) * 32;
     wsize_ = ((rows * plane_ + 64 + 31) / 32) * 32;
@@ -287,8 +285,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   k.fused = fused_ ? 1 : 0;
   k.steps = steps_;
   k.hdep = hdep_;
-  k.pre_load = !(std::getenv("PE_PRE") && std::atoi(std::getenv("PE_PRE")) == 0);
-  k.dring = !(std::getenv("PE_DRING") && std::atoi(std::getenv("PE_DRING")) == 0);
+  k.pre_load = 1;  // first item's list entry + row classes loaded at kernel entry (fused3.hip Pre3)
+  k.dring = 1;     // band rows read 1/D from the LDS ring (+0.7 % at 8192², profiles/r5_ab_kernel.txt)
   // SIMD priority turns (fused3.hip prio_turn), opt-in: 1-GPU 2048² and
   // 1600×2400 T_iterate −0.8-1.5 % at PE_PRIO=10, but the 2-rank blocks of
   // 2048² / 1600×2400 +2-7 % (20.2 vs 18.9 µs per iteration), 8192² −4-6 %
@@ -522,13 +520,10 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   // static layout 0.536-0.545 ms vs 0.564-0.567 for the plain walk), so it
   // stops after 2-3 tries instead of 8 — construction 0.10-0.14 vs 0.15-0.25 s,
   // the same iteration speed (profiles/r2_bench_psearch.txt).
-  // PE_PLACEMENT_LISTED=0: search with the plain walk, before the layout.
-  const bool listed_search = !(std::getenv("PE_PLACEMENT_LISTED") && std::atoi(std::getenv("PE_PLACEMENT_LISTED")) == 0);
-  if (fused_ && !listed_search) choose_placement();
   if (comm_->size() > 1) measure_exchange();  // (diagnostic: the comm's exchange, bench JSON)
   setup_items();
   mark("items");
-  if (fused_ && listed_search) choose_placement();
+  if (fused_) choose_placement();
   mark("placement");
   setup_resident();
   mark("resident");
@@ -683,13 +678,13 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     stream_chunk_ = chunk_;
   }
   mark("tuning+rest");
-  // PE_WARM_COPY=1: one small pageable copy at construction.  The runtime
-  // sets up its pageable-copy path lazily at the first such copy of the
-  // process (≈19 ms, profiles/r2_init_probe.txt) — which a graph
-  // instantiation triggers; with graph-replayed solves (--graph) this keeps
-  // that cost out of the iteration loop (4 µs per iteration at 1600×2400
-  // otherwise).  The default eager solve never takes that path.
-  if (std::getenv("PE_WARM_COPY") && std::atoi(std::getenv("PE_WARM_COPY")) == 1) {
+  // Graph-replayed solves (--graph): one small pageable copy at construction.
+  // The runtime sets up its pageable-copy path lazily at the first such copy
+  // of the process (≈19 ms, profiles/r2_init_probe.txt) — which a graph
+  // instantiation triggers; this keeps that cost out of the iteration loop (4
+  // µs per iteration at 1600×2400 otherwise).  The eager solve never takes
+  // that path.
+  if (opt_.use_graph) {
     double h = 0.0;
     PE_HIP_CHECK(hipMemcpy(partial_, &h, sizeof(double), hipMemcpyHostToDevice));
   }
@@ -1696,10 +1691,6 @@ SolveResult DeviceSolver::solve() {
   res.t.construct = construct;
   res.t.setup = construct + secs(t_start, clk::now());
   const int64_t ck_every = opt_.checkpoint_path.empty() ? 0 : opt_.checkpoint_every;
-  // per-chunk state read: a copy kernel into mapped pinned memory (default),
-  // or PE_STATE_COPY=memcpy (hipMemcpyAsync; its first use initialises the
-  // runtime's copy path inside T_solver)
-  state_memcpy_ = std::getenv("PE_STATE_COPY") && std::string(std::getenv("PE_STATE_COPY")) == "memcpy";
 
   // Phase sampling: every `sample_every`-th chunk, its first two iterations
   // (all of them with opt_.timing); no host sync beyond the per-chunk state
@@ -1749,10 +1740,10 @@ SolveResult DeviceSolver::solve() {
         sampling_ = sample;
         sample_iter_ = enq - 1;
         mark_begin(kPhCopy, stream_);
-        if (state_memcpy_)
-          PE_HIP_CHECK(hipMemcpyAsync(&hst_[slot], st_, sizeof(DevState), hipMemcpyDeviceToHost, stream_));
-        else
-          dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);  // pinned, mapped
+        // per-chunk state read: a copy kernel into mapped pinned memory (a
+        // hipMemcpyAsync's first use initialises the runtime's copy path
+        // inside T_solver)
+        dev::launch_copy_words(&hst_[slot], st_, sizeof(DevState), true, stream_);
         mark_end(stream_);
         sampling_ = false;
         PE_HIP_CHECK(hipEventRecord(ev_[slot], stream_));

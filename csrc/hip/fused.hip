@@ -1156,28 +1156,16 @@ void launch_coef_fast(const KParams& k, double* a, double* b, double* dinv, hipS
   hipLaunchKernelGGL(kCoefFast, dim3(g), dim3(256), 0, s, k, a, b, dinv);
 }
 
-// Kernel configuration (PE_SKERNEL, for tuning sweeps): 0 default = 4 rows
-// of loads in flight per wave + non-temporal w/output streams (8192² sweep:
-// 1373 it/s vs 1119 for 2 rows / temporal at 3 waves per SIMD — the sweep is
-// bound by HBM latency per wave, not by occupancy); 1 = temporal streams.
-// (Round 1 also measured 2 / 3 / 5 rows in flight: 4 won, and the plain
-// march's unroll is tied to it.)
-static int s_cfg() {
-  static const int v = [] {
-    const char* e = std::getenv("PE_SKERNEL");
-    return e ? std::atoi(e) : 0;
-  }();
-  return v;
-}
-
+// Kernel configuration: 4 rows of loads in flight per wave + non-temporal
+// w / output streams (8192² sweep: 1373 it/s vs 1119 for 2 rows / temporal
+// streams at 3 waves per SIMD — the sweep is bound by HBM latency per wave,
+// not by occupancy; round 1 also measured 2 / 3 / 5 rows in flight: 4 won,
+// and the plain march's unroll is tied to it).
 template <int WM, class F>
 static auto with_kS(const KParams& k, F&& f) {
   if (k.stamps) return f(kS<2, 4, true, WM, true>);
   if (k.push) return f(kS<2, 4, true, WM, false, true>);
-  switch (s_cfg()) {
-    case 1: return f(kS<2, 4, false, WM>);
-    default: return f(kS<2, 4, true, WM>);
-  }
+  return f(kS<2, 4, true, WM>);
 }
 
 void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
@@ -1204,12 +1192,9 @@ void launch_S(const KParams& k, int par, hipStream_t s, bool with_red) {
 }
 
 void launch_red(const KParams& k, int par, hipStream_t s) {
-  static const int red1_max = [] {
-    const char* e = std::getenv("PE_RED1_MAX");
-    // one workgroup streams ≈1.5 µs per 1000 slots (8192²'s 44 k slots: 71 µs
-    // vs 10 µs for 64 blocks, tools/jobs/red_trace.sh): only tiny lists
-    return e ? std::atoi(e) : 4000;
-  }();
+  // one workgroup streams ≈1.5 µs per 1000 slots (8192²'s 44 k slots: 71 µs
+  // vs 10 µs for 64 blocks, tools/jobs/red_trace.sh): only tiny lists
+  constexpr int red1_max = 4000;
   if (k.nslots <= red1_max) {
     if (par == 0) hipLaunchKernelGGL(kRed1<0>, dim3(1), dim3(kRed1Threads), 0, s, k, par);
     else hipLaunchKernelGGL(kRed1<2>, dim3(1), dim3(kRed1Threads), 0, s, k, par);
@@ -1218,9 +1203,7 @@ void launch_red(const KParams& k, int par, hipStream_t s) {
   {
     // 8192² (44 k slots, 2.8 MB): 4 / 16 / 64 / 128 / 512 blocks = 26.7 / 13.5 /
     // 10.1 / 10.8 / 11.6 µs — load parallelism first, then the ticket fan-in
-    int rb = 64;
-    if (const char* e = std::getenv("PE_REDBLOCKS")) rb = std::max(1, std::atoi(e));
-    rb = std::max(1, std::min(rb, (k.nslots + 255) / 256));
+    const int rb = std::max(1, std::min(64, (k.nslots + 255) / 256));
     if (par == 0) hipLaunchKernelGGL(kRed<0>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
     else hipLaunchKernelGGL(kRed<2>, dim3(unsigned(rb)), dim3(TJ), 0, s, k, par);
   }

@@ -102,16 +102,14 @@ void DeviceSolver::setup_items() {
   // out better at 2 (8-rank 8192² block 84.2-85.1 vs 87.3-87.8 µs per
   // iteration, 4-rank 155 vs 160, 2400×3200 77.9-79.3 vs 79.5-80.3; 1 is
   // worse everywhere); larger blocks see no difference above the placement
-  // noise and keep 3 (profiles/r2_gencost.txt).  PE_GEN_COST overrides.
+  // noise and keep 3 (profiles/r2_gencost.txt).
   double gen_cost = double(blk_.nx) * double(blk_.ny) >= double(1 << 24) ? 3.0 : 2.0;
   // three-step LPT at 2²⁵-2²⁶ nodes (8192², 112-row items): 3.25-4 run ≈1 %
   // faster than 3 on three boxes, 5-8 ≈8 % slower (profiles/r4_ti48.txt)
   if (steps_ >= 3 && double(blk_.nx) * double(blk_.ny) >= double(1 << 25) &&
       double(blk_.nx) * double(blk_.ny) <= double(1 << 26))
     gen_cost = 3.5;
-  if (const char* g = std::getenv("PE_GEN_COST")) gen_cost = std::max(0.0, std::atof(g));
-  const bool sort_heavy = !(std::getenv("PE_HEAVY_FIRST") && std::atoi(std::getenv("PE_HEAVY_FIRST")) == 0);
-  const bool split_heavy = !(std::getenv("PE_HEAVY_SPLIT") && std::atoi(std::getenv("PE_HEAVY_SPLIT")) == 0);
+  const bool sort_heavy = true, split_heavy = true;  // heavy items first (dynamic) / split (static)
   // per-item cost: rows ib-2 .. ie+2, band rows weighted
   const int64_t rows_tab = int64_t(rowcls_host_.size() / 4);
   // Does local row q have a boundary-band node in strip s's loaded
@@ -193,10 +191,10 @@ void DeviceSolver::setup_items() {
   // feed the exchange) and under the halo push (their xGMI stores then
   // overlap the rest of the sweep instead of ending it)
   // The halo push keeps the plain layout: cutting its boundary pieces off and
-  // dealing them first (PE_PUSH_FIRST=1, the earlier default) cost the push
-  // kernel 10 % at the 8-rank slab of 8192² (64.6-65.1 vs 58.2 µs per
-  // iteration) and 4 % at 4 ranks, loopback probe, profiles/r5_push_release.txt
-  const bool push_first = push_ && std::getenv("PE_PUSH_FIRST") && std::atoi(std::getenv("PE_PUSH_FIRST")) == 1;
+  // dealing them first (the pre-round-5 layout) cost the push kernel 10 % at
+  // the 8-rank slab of 8192² (64.6-65.1 vs 58.2 µs per iteration) and 4 % at
+  // 4 ranks, loopback probe, profiles/r5_push_release.txt
+  const bool push_first = false;
   auto is_boundary = [&](int64_t ib, int64_t ie, int s) {
     const int64_t J = -(HL - 1) + int64_t(s) * fsw_;
     const int64_t jlo = std::max<int64_t>(1, J + HL), jhi = std::min<int64_t>(blk_.ny, J + fsw_ + HL - 1);
@@ -320,8 +318,6 @@ void DeviceSolver::setup_items() {
     auto capw = [&](int w, int Wn) {
       return (Wn / dev::kWPB > cus_ && w / dev::kWPB < cus_) ? rho : 1.0;
     };
-    if (const char* e = std::getenv("PE_COST_BAND")) fband = std::atof(e);
-    if (const char* e = std::getenv("PE_COST_MIXED")) fmixed = std::atof(e);
     if (equal) {
       // Three-step sweep: EQUAL-COST PIECES, EXACTLY k PER WAVE.  Whole items
       // cannot balance ~8 items per wave: the waves hold 8 or 9 uniform items,
@@ -737,17 +733,12 @@ void DeviceSolver::setup_items() {
     cut[size_t(x)] = c;
   }
   cut[size_t(nsh)] = nchunks;
-  // Tail split (dynamic sweeps, opt-in): the last PE_TAIL_FRAC of every
-  // shard's light items are cut into PE_TAIL_SPLIT shorter items, so the round
-  // of items running when the queues drain is short.  Off by default since the
-  // per-XCD queues: at one placement every extra item costs more than the
-  // shorter drain saves (8192², 18 rows: 545.5 µs per iteration unsplit vs
-  // 550.6 / 552.1 / 556.1 with 5 / 10 / 30 % split; 2 ranks 297.8 vs 307.5 —
-  // profiles/r2_layout.txt).
-  double tail_frac = 0.0;
-  int tail_split = 2;
-  if (const char* t = std::getenv("PE_TAIL_FRAC")) tail_frac = std::min(1.0, std::max(0.0, std::atof(t)));
-  if (const char* t = std::getenv("PE_TAIL_SPLIT")) tail_split = std::max(1, std::atoi(t));
+  // (no tail split of the last items: at one placement every extra item cost
+  // more than the shorter drain saved — 8192², 18 rows: 545.5 µs per
+  // iteration unsplit vs 550.6 / 552.1 / 556.1 with 5 / 10 / 30 % split; 2
+  // ranks 297.8 vs 307.5, profiles/r2_layout.txt; the knob was removed in round 6)
+  const double tail_frac = 0.0;
+  const int tail_split = 2;
   std::vector<int2> all;
   ov_nb_ = 0;
   ov_lnsh_ = nsh;

@@ -64,7 +64,7 @@ using dev::KParams;
 // row padding, virtual address or TLB misses — the slow placements show ~1.7×
 // the DRAM credit stalls; docs/PERFORMANCE.md).  Try up to
 // PE_PLACEMENT_TRIES (default 8) candidate allocations, each after a
-// PE_PLACEMENT_SKIP_GB (default 8) spacer so it lands in another region;
+// 8 GB spacer so it lands in another region;
 // time a few local sweeps on real data (no communication) and keep the
 // fastest (stop early once one is clearly in the fast class).  Everything else is freed; an allocation failure ends the search.
 //
@@ -116,8 +116,7 @@ bool DeviceSolver::placement_search(bool retry) {
   int tries = pts >= 24.0e6 ? 12 : 1;
   if (retry) tries = std::max(1, tries / 2 + 1);  // the kept candidate + half a round
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
-  double skip_gb = 8.0;
-  if (const char* e = std::getenv("PE_PLACEMENT_SKIP_GB")) skip_gb = std::max(0.0, std::atof(e));
+  const double skip_gb = 8.0;
   // best-class threshold: the single sweep's 40 B/node at ≥ 4.9 TB/s (8192²:
   // ≤ 0.548 ms); the two-step sweep's 48 B/node per sweep at ≥ 4.7 TB/s
   // (8192²: its classes are 0.676-0.69 and 0.83-0.85 ms per sweep); the
@@ -125,15 +124,14 @@ bool DeviceSolver::placement_search(bool retry) {
   // with the aligned strips and 112-row items its classes are 0.709-0.722,
   // 0.74, 0.78-0.79 and 0.83-0.85 ms, the first fast one usually the 5th try —
   // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates)
-  double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
+  const double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9;
+  double max_s = 0.3;
   if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
-  if (const char* e = std::getenv("PE_PLACEMENT_FAST_TBS")) fast_tbs = std::atof(e);
   if (tries <= 1) return true;
   // spacers are transient; never let the search take more than 40 % of the
-  // free memory (several solvers may share the device; PE_PLACEMENT_MEM_FRAC)
+  // free memory (several solvers may share the device)
   {
-    double frac = 0.4;
-    if (const char* e = std::getenv("PE_PLACEMENT_MEM_FRAC")) frac = std::min(0.9, std::max(0.0, std::atof(e)));
+    const double frac = 0.4;
     size_t free_b = 0, total_b = 0;
     if (hipMemGetInfo(&free_b, &total_b) == hipSuccess) {
       const double per_try = skip_gb * double(1ull << 30) + double(sizeof(double) * (2 * xsize_ + wsize_));
@@ -193,7 +191,7 @@ bool DeviceSolver::placement_search(bool retry) {
     // ≈6 ms (spacer, allocation, 9 sweeps), the best class saves ≈3 % of a
     // 3.3 s solve: keep the best of all tries, stopping early only at the
     // best class — the sweep's average 40 B/node streamed at >=
-    // PE_PLACEMENT_FAST_TBS (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
+    // fast_tbs (4.9 TB/s = 0.548 ms at 8192²).  (Earlier stop
     // rules — 5 % / 7 % below the slowest seen, 4.6 / 4.75 TB/s — settled for
     // 0.56-0.60 ms placements when better ones were a try or two further.)
     const double bps = sstep_ ? 48.0 : 40.0;  // streamed bytes per node and sweep

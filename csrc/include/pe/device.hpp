@@ -389,7 +389,6 @@ class DeviceSolver {
   int* res_rowstart_ = nullptr;
   double* res_buf_ = nullptr;  // edges then partials
   unsigned* res_ctr_ = nullptr;
-  bool state_memcpy_ = false;       // PE_STATE_COPY=memcpy: per-chunk state read by hipMemcpyAsync
   void* stage_ = nullptr;           // pinned staging buffer of upload()
   size_t stage_bytes_ = 0;
   bool push_ = false;               // in-sweep halo push (KParams::push)

@@ -14,6 +14,9 @@ stores stay on the device) and the real RCCL latency — the delays model them.
 
     python tools/halo_probe.py [exchange_us allreduce_us ...]
     PROBE_CFG=8:rows,4:rows,8:4x2 PROBE_GRID=8192x8192 PROBE_EACH=1
+    PROBE_HALO=exchange  (the auto run chooses among the exchange arms only:
+                          the projections' model — the loopback put / push pay
+                          no xGMI time, the delayed exchange does)
 """
 import os
 import sys
@@ -62,7 +65,7 @@ for P, spec in configs:
     rank = P // 2
     blk = nat.decompose(GM, GN, g, rank)
     for ex, ar in delays:
-        path, cands, us, ctor = run(P, blk, ex, ar)
+        path, cands, us, ctor = run(P, blk, ex, ar, os.environ.get("PROBE_HALO"))
         cs = ", ".join(f"{n} {t:.1f}" for n, t in cands)
         print(f"P={P} {g.Px}x{g.Py} rank {rank} block {blk.nx}x{blk.ny} delays ex={ex:5.1f} ar={ar:5.1f} us: "
               f"chosen {path}: {us:7.1f} us/iter (construction {ctor * 1e3:.0f} ms) | candidates us/sweep: {cs}",
