@@ -1046,20 +1046,9 @@ void DeviceSolver::choose_halo_path() {
   Range range("pe.choose_halo_path");
   const int keep_tol = kp_->check_tol;
   kp_->check_tol = 0;
-  constexpr int kTimed = 4;
   auto time_path = [&](const Cand& c) {
     apply_halo_path(c.path, c.ov);
-    reset();
-    run_iterations(2 * steps_, false);
-    PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-    run_iterations(int64_t(kTimed) * steps_, false);
-    PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-    wait_event(t1_);
-    float ms = 0.f;
-    PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-    double v[1] = {double(ms) / kTimed};
-    comm_->host_max(v, 1, stream_);
-    return v[0];
+    return time_halo_path(4);
   };
   for (Cand& c : cands) {
     c.ms = time_path(c);
@@ -1086,6 +1075,35 @@ void DeviceSolver::choose_halo_path() {
     std::fprintf(stderr, "[pe] halo path chosen: %s\n", halo_path_.c_str());
   }
   (void)nb;
+}
+
+void DeviceSolver::set_halo_path(const std::string& path, bool overlap) {
+  if ((path == "push" && !push_ok_) || (path == "put" && !put_ok_) ||
+      (path != "push" && path != "put" && path != "exchange"))
+    throw std::invalid_argument("set_halo_path: '" + path + "' is not available (push: " + push_status_ +
+                                ", put: " + put_status_ + ")");
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));
+  apply_halo_path(path, overlap);
+  halo_path_ = path + (overlap_ ? "+overlap" : "") + " (set)";
+}
+
+// 2 + `sweeps` sweeps of the real iteration from the initial state (the stop
+// test off), the last `sweeps` timed; ms per sweep, max over ranks.
+double DeviceSolver::time_halo_path(int sweeps) {
+  const int keep_tol = kp_->check_tol;
+  kp_->check_tol = 0;
+  reset();
+  run_iterations(2 * steps_, false);
+  PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+  run_iterations(int64_t(sweeps) * steps_, false);
+  PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+  wait_event(t1_);
+  kp_->check_tol = keep_tol;
+  float ms = 0.f;
+  PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+  double v[1] = {double(ms) / sweeps};
+  comm_->host_max(v, 1, stream_);
+  return v[0];
 }
 
 void DeviceSolver::relayout(int ti, int order) {
@@ -1161,9 +1179,7 @@ void DeviceSolver::measure_exchange() {
 
 void DeviceSolver::create_halo_stream() {
   if (hs_) return;
-  int least = 0, greatest = 0;
-  PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-  PE_HIP_CHECK(hipStreamCreateWithPriority(&hs_, hipStreamNonBlocking, greatest));
+  hs_ = acquire_halo_stream();  // (pooled: set_device created one next to the solver stream — runtime.cpp)
   PE_HIP_CHECK(hipEventCreateWithFlags(&ev_halo_, hipEventDisableTiming));
 }
 
@@ -1200,7 +1216,10 @@ DeviceSolver::~DeviceSolver() {
   if (res_rowstart_) (void)hipFree(res_rowstart_);
   if (res_buf_) (void)hipFree(res_buf_);
   if (res_ctr_) (void)hipFree(res_ctr_);
-  if (hs_) (void)hipStreamDestroy(hs_);
+  if (hs_) {
+    (void)hipStreamSynchronize(hs_);
+    release_halo_stream(hs_);
+  }
   if (ev_halo_) (void)hipEventDestroy(ev_halo_);
   (void)hipFree(st_);
   (void)hipHostFree(hst_);

@@ -29,35 +29,37 @@ int device_count() {
   return n;
 }
 
-// Per-device pool of idle solver streams.  A new stream costs the runtime a
-// hardware queue: 20-41 ms in a fresh process, the largest part of a small
-// grid's construction (400×600: T_solver 0.035-0.054 s of which the stream
-// 21-41 ms — PE_CTOR_TRACE=1, profiles/r4_cold.txt).  set_device() creates
-// one while binding the process to its GPU (like the RCCL / P2P set-up, before
-// any solver), and a solver returns its stream here when it is destroyed.
+// Per-device pools of idle streams: solver streams and the high-priority
+// halo streams of the overlap.  A new stream costs the runtime a hardware
+// queue: 20-41 ms in a fresh process, the largest part of a small grid's
+// construction (400×600: T_solver 0.035-0.054 s of which the stream 21-41 ms —
+// PE_CTOR_TRACE=1, profiles/r4_cold.txt).  set_device() creates one of each
+// while binding the process to its GPU (like the RCCL / P2P set-up, before any
+// solver), one right after the other: the process has few hardware queues
+// (GPU_MAX_HW_QUEUES, 4 by default) and streams take them in turn, so the
+// pair gets two different queues.  A halo stream created later could land on
+// the solver stream's queue, which serialises the overlap: a fresh solver
+// with the overlap ran the 8-rank slab of 8192² at 52 µs per iteration, the
+// same overlap switched on in a solver whose halo stream had been created
+// early 42.5 (profiles/r6_overlap_steady.txt).  A solver returns its streams
+// here when it is destroyed.
 namespace {
 std::mutex g_stream_mu;
 std::vector<std::pair<int, hipStream_t>> g_idle_streams;  // (device, stream)
-}  // namespace
+std::vector<std::pair<int, hipStream_t>> g_idle_halo;     // (device, high-priority stream)
 
-hipStream_t acquire_stream() {
-  int dev = 0;
-  PE_HIP_CHECK(hipGetDevice(&dev));
-  {
-    std::lock_guard<std::mutex> g(g_stream_mu);
-    for (size_t i = 0; i < g_idle_streams.size(); ++i)
-      if (g_idle_streams[i].first == dev) {
-        const hipStream_t s = g_idle_streams[i].second;
-        g_idle_streams.erase(g_idle_streams.begin() + long(i));
-        return s;
-      }
-  }
-  hipStream_t s = nullptr;
-  PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
-  return s;
+hipStream_t take(std::vector<std::pair<int, hipStream_t>>& pool, int dev) {
+  std::lock_guard<std::mutex> g(g_stream_mu);
+  for (size_t i = 0; i < pool.size(); ++i)
+    if (pool[i].first == dev) {
+      const hipStream_t s = pool[i].second;
+      pool.erase(pool.begin() + long(i));
+      return s;
+    }
+  return nullptr;
 }
 
-void release_stream(hipStream_t s) {
+void give(std::vector<std::pair<int, hipStream_t>>& pool, hipStream_t s) {
   if (!s) return;
   // filed under the device the stream was created on, not the current one (a
   // solver may be destroyed after the process moved to another device)
@@ -67,17 +69,56 @@ void release_stream(hipStream_t s) {
     return;
   }
   std::lock_guard<std::mutex> g(g_stream_mu);
-  g_idle_streams.emplace_back(dev, s);
+  pool.emplace_back(dev, s);
 }
+}  // namespace
+
+static hipStream_t new_halo_stream() {
+  int least = 0, greatest = 0;
+  PE_HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+  hipStream_t s = nullptr;
+  PE_HIP_CHECK(hipStreamCreateWithPriority(&s, hipStreamNonBlocking, greatest));
+  return s;
+}
+
+hipStream_t acquire_stream() {
+  int dev = 0;
+  PE_HIP_CHECK(hipGetDevice(&dev));
+  if (hipStream_t s = take(g_idle_streams, dev)) return s;
+  hipStream_t s = nullptr;
+  PE_HIP_CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  // (a new solver stream gets its halo stream created right after it: the
+  // pair then holds two hardware queues — see above)
+  bool have_halo = false;
+  {
+    std::lock_guard<std::mutex> g(g_stream_mu);
+    for (const auto& e : g_idle_halo) have_halo = have_halo || e.first == dev;
+  }
+  if (!have_halo) give(g_idle_halo, new_halo_stream());
+  return s;
+}
+
+void release_stream(hipStream_t s) { give(g_idle_streams, s); }
+
+hipStream_t acquire_halo_stream() {
+  int dev = 0;
+  PE_HIP_CHECK(hipGetDevice(&dev));
+  if (hipStream_t s = take(g_idle_halo, dev)) return s;
+  return new_halo_stream();
+}
+
+void release_halo_stream(hipStream_t s) { give(g_idle_halo, s); }
 
 void set_device(int dev) {
   PE_HIP_CHECK(hipSetDevice(dev));
-  bool have = false;
+  bool have = false, have_halo = false;
   {
     std::lock_guard<std::mutex> g(g_stream_mu);
     for (const auto& e : g_idle_streams) have = have || e.first == dev;
+    for (const auto& e : g_idle_halo) have_halo = have_halo || e.first == dev;
   }
-  if (!have) release_stream(acquire_stream());
+  if (!have) release_stream(acquire_stream());  // (creates the halo stream next to it)
+  else if (!have_halo) release_halo_stream(acquire_halo_stream());
 }
 
 int current_device() {

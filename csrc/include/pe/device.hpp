@@ -28,10 +28,13 @@ struct PeerSum;
 
 [[noreturn]] void hip_fail(hipError_t e, const char* expr, const char* file, int line);
 int device_count();
-void set_device(int dev);  // hipSetDevice + one pooled solver stream for that device
+void set_device(int dev);  // hipSetDevice + one pooled solver stream and halo stream for that device
 // Solver streams (non-blocking) from / back to the per-device idle pool.
 hipStream_t acquire_stream();
 void release_stream(hipStream_t s);
+// High-priority halo streams (the overlap's), pooled the same way.
+hipStream_t acquire_halo_stream();
+void release_halo_stream(hipStream_t s);
 std::string device_name(int dev);
 int current_device();
 std::string device_pci_bus_id(int dev);
@@ -197,6 +200,12 @@ class DeviceSolver {
   const std::string& halo_path() const { return halo_path_; }
   const std::vector<std::pair<std::string, double>>& halo_candidates() const { return halo_cands_; }
   const std::string& put_status() const { return put_status_; }
+  // Probes: switch to another halo path after construction (one of the
+  // candidates the construction could pick; the item list is re-laid out for
+  // the overlap) and time `sweeps` sweeps of it from a reset the way the
+  // construction's choice does (ms per sweep, max over ranks; collective).
+  void set_halo_path(const std::string& path, bool overlap);
+  double time_halo_path(int sweeps);
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   int placement_choice() const { return placement_best_; }       // index into placement_ms()
