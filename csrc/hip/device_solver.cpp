@@ -412,7 +412,6 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   int per_cu = fused_ ? dev::resident_blocks_S(k, 2) : dev::resident_blocks_classic(opt_.variant);
   if (per_cu <= 0) per_cu = 4;
   int wave_cap = cus * per_cu * dev::kWPB;
-  if (const char* e = std::getenv("PE_WAVES")) wave_cap = std::max(4, std::atoi(e));
   // PE_TI=-1 (single-sweep): "bands" — one item per resident wave, the rows
   // split into wave_cap/nstrips bands that the waves of a band march down
   // together (halo rows re-read once per band, perfect balance).
@@ -422,7 +421,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
   }
   k.nstrips = int(strips);
   int wave_cap0 = wave_cap;
-  if (fused_ && !std::getenv("PE_WAVES")) {
+  if (fused_) {
     const int per0 = dev::resident_blocks_S(k, 0);
     if (per0 > 0) wave_cap0 = cus * per0 * dev::kWPB;
   }

@@ -53,7 +53,7 @@ void DeviceSolver::set_items(int ti) {
 // st->sig when stored.  A one-wave kernel on a high-priority halo stream waits
 // for the count, then the exchange runs there while the interior items are
 // still being computed.  The sweep keeps its full persistent grid minus
-// `PE_OV_RESERVE` blocks (default 8) left free for the wait / exchange /
+// 8 blocks left free for the wait / exchange /
 // unpack kernels.  PE_OVERLAP=0 disables.
 //
 // Every dynamic (order 3) sweep walks such lists, overlap or not.  Item cost
@@ -91,7 +91,6 @@ void DeviceSolver::setup_items() {
     // timing experiments (PE_OV_DEBUG bits): 2 serial streams, 4 natural item
     // order (no boundary-first list)
     if (const char* d = std::getenv("PE_OV_DEBUG")) ov_debug_ = std::atoi(d);
-    if (const char* r = std::getenv("PE_OV_RESERVE")) ov_reserve_ = std::max(0, std::atoi(r));
   }
   const int gmin = std::max(1, std::min(k.nblocks, k.nblocks0) - (overlap_ ? ov_reserve_ : 0));
   const int nsh = k.order >= 2 ? std::min(8, gmin) : 1;
@@ -224,7 +223,6 @@ void DeviceSolver::setup_items() {
     };
     const double overhead = 3.0;  // per-item prologue / epilogue, in row steps (stamps)
     int waves_avail = std::max(dev::kWPB, wave_cap_ - (overlap_ ? ov_reserve_ * dev::kWPB : 0));
-    if (const char* w = std::getenv("PE_WAVES")) waves_avail = std::max(dev::kWPB, std::atoi(w));
     double total = 0.0;
     for (int id = 0; id < k.nitems; ++id) total += item_cost(id / k.nstrips, id % k.nstrips) + overhead;
     // cut only when there are fewer items than waves (small blocks): with

@@ -124,9 +124,7 @@ bool DeviceSolver::placement_search(bool retry) {
   // with the aligned strips and 112-row items its classes are 0.709-0.722,
   // 0.74, 0.78-0.79 and 0.83-0.85 ms, the first fast one usually the 5th try —
   // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates)
-  const double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9;
-  double max_s = 0.3;
-  if (const char* e = std::getenv("PE_PLACEMENT_MAX_S")) max_s = std::atof(e);
+  const double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (tries <= 1) return true;
   // spacers are transient; never let the search take more than 40 % of the
   // free memory (several solvers may share the device)
@@ -202,7 +200,7 @@ bool DeviceSolver::placement_search(bool retry) {
     }
     // spacer allocations are cheap on fresh memory but can take seconds
     // when the allocator must clear reused memory (profiles/r2_ctor_probe.txt):
-    // the search is capped at PE_PLACEMENT_MAX_S (0.3 s) of wall time
+    // the search is capped at 0.3 s of wall time
     if (secs(clock.t0, clk::now()) > max_s) break;
   }
   (void)hipGetLastError();  // clear a failed search allocation

@@ -80,7 +80,9 @@ class RcclComm final : public DeviceComm {
     PE_NCCL_CHECK(ncclAllReduce(scratch_, scratch_, 1, ncclDouble, ncclSum, comm_, s));
     PE_HIP_CHECK(hipStreamSynchronize(s));
   }
-  bool capturable() const override { return std::getenv("PE_RCCL_GRAPH") != nullptr; }
+  // RCCL calls are not captured into the iteration graphs (the put / push
+  // paths with in-sweep sums replay from graphs without a comm call)
+  bool capturable() const override { return false; }
   std::string name() const override { return "rccl"; }
   void check_async() override {
     if (!comm_) return;

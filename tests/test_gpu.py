@@ -1060,3 +1060,55 @@ def test_halo_path_choice_follows_the_transport(gpu, monkeypatch):
     monkeypatch.setenv("PE_HALO_TUNE", "0")
     s, c = build(400.0)
     assert s.halo_candidates == [] and s.halo_path == "exchange (PE_HALO_TUNE=0)" and not s.overlap
+
+
+def test_diagnostic_knobs(gpu, monkeypatch):
+    """The diagnostic / set-up knobs the knob table keeps (docs/PERFORMANCE.md),
+    each exercised once: PE_STAMPS=1 (three-step stamps) and PE_RES_STAMPS=1
+    (resident kernel) record s_memrealtime stamps; PE_TI_TUNE=0 skips the
+    rows-per-item tuning; PE_PLACEMENT_TRIES=1 skips the placement search;
+    PE_TIMER_SAMPLE=0 turns the sampled phase timers off (T_gpu is then the
+    loop's device span); PE_CTOR_TRACE=1 prints the construction phases."""
+    from poisson_ellipse_openmp_mpi_cuda_amd._loader import native
+    from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D
+
+    nat = native()
+
+    def make(M, N, **env):
+        for k, v in env.items():
+            monkeypatch.setenv(k, v)
+        opt = nat.SolveOptions()
+        opt.check_tol = False
+        s = nat.DeviceSolver(EllipseProblem(M, N).to_native(), D.block(M, N, 1, 0), None, opt)
+        for k in env:
+            monkeypatch.delenv(k)
+        return s
+
+    s = make(1024, 1024, PE_STAMPS="1", PE_RESIDENT="0")
+    assert s.sweep_steps == 3
+    s.reset()
+    s.run_iterations(9, False)
+    st = np.asarray(s.stamps(), dtype=np.uint64)
+    assert st.size > 0 and np.count_nonzero(st) > 0
+    s = make(400, 600, PE_RES_STAMPS="1")
+    assert s.resident
+    s.reset()
+    s.run_iterations(16, False)
+    st = np.asarray(s.stamps(), dtype=np.uint64)
+    assert st.size > 0 and np.count_nonzero(st) > 0
+    tuned = make(1600, 2400)
+    assert len(tuned.ti_tuning_ms) > 0
+    untuned = make(1600, 2400, PE_TI_TUNE="0")
+    assert len(untuned.ti_tuning_ms) == 0
+    one = make(8192, 8192, PE_PLACEMENT_TRIES="1")
+    assert len(one.placement_ms) == 0
+    del one
+    monkeypatch.setenv("PE_TIMER_SAMPLE", "0")
+    rep = solve(EllipseProblem(400, 600), backend="hip", algo="three-step")
+    assert rep.iters == 546 and rep.timers["sampled"] == 0 and rep.timers["gpu"] > 0
+    monkeypatch.delenv("PE_TIMER_SAMPLE")
+    env = dict(os.environ, PE_CTOR_TRACE="1")
+    out = subprocess.run([os.path.join(ROOT, "bin", "pe_hip"), "--json", "400", "600"], cwd=ROOT, env=env,
+                         capture_output=True, text=True, timeout=120)
+    assert out.returncode == 0, out.stderr[-2000:]
+    assert "[pe] ctor" in out.stderr and "halo path" in out.stderr

@@ -2,7 +2,8 @@
 One GPU runs the block of one rank of a multi-GPU decomposition with a
 timing-only transport (stream-ordered busy waits of fixed length stand in
 for the RCCL exchange and allreduce), with PE_OVERLAP=0 and 1
-(PROBE_OV=0,1:8,1:32:1 → overlap:reserved blocks[:PE_OV_DEBUG]).
+(PROBE_OV=0,1,1::2 → overlap[::PE_OV_DEBUG]; 8 blocks stay free for the
+halo stream).
 
     python tools/overlap_probe.py [exchange_us allreduce_us]"""
 import os
@@ -28,7 +29,6 @@ for P, spec in configs:
     for delays in [(0.0, 0.0), (ex_us, ar_us)]:
         for ov in os.environ.get("PROBE_OV", "0,1:8").split(","):
             os.environ["PE_OVERLAP"] = ov.split(":")[0]
-            os.environ["PE_OV_RESERVE"] = ov.split(":")[1] if ":" in ov else "8"
             os.environ["PE_OV_DEBUG"] = ov.split(":")[2] if ov.count(":") > 1 else "0"
             opt = nat.SolveOptions()
             opt.check_tol = False
