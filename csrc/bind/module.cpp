@@ -483,8 +483,8 @@ PYBIND11_MODULE(_native, m) {
       .def_property_readonly("graphs_usable", &DeviceSolver::graphs_usable)
       .def("set_halo_path", &DeviceSolver::set_halo_path, py::arg("path"), py::arg("overlap"),
            "probe: switch to another halo path candidate (exchange / put / push, overlap)")
-      .def("time_halo_path", &DeviceSolver::time_halo_path, py::arg("sweeps") = 4,
-           "probe: ms per sweep of the current halo path, timed as the construction's choice does")
+      .def("time_halo_path", &DeviceSolver::time_halo_path, py::arg("sweeps") = 4, py::arg("warm") = 2,
+           py::arg("from_reset") = true, "probe: ms per sweep of the current halo path")
       .def_property_readonly("put_status", &DeviceSolver::put_status, "peer put: available / off: why / fallback: why")
       .def("save_checkpoint", &DeviceSolver::save_checkpoint, py::arg("path"))
       .def("load_checkpoint", &DeviceSolver::load_checkpoint, py::arg("path"))

@@ -970,7 +970,12 @@ void DeviceSolver::xfer(const std::vector<Exchange>& ex, hipStream_t s) {
   PE_HIP_CHECK(hipGetLastError());
 }
 
-void DeviceSolver::apply_halo_path(const std::string& path, bool overlap) {
+void DeviceSolver::apply_halo_path(const std::string& path, bool overlap, bool live) {
+  const bool was_push = push_, was_ov = overlap_;
+  if (live) {  // (the state carries on: nothing of the old path may still be in flight)
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (hs_) PE_HIP_CHECK(hipStreamSynchronize(hs_));
+  }
   push_ = path == "push" && push_ok_;
   put_ = path == "put" && put_ok_;
   kp_->push = push_ ? 1 : 0;
@@ -981,6 +986,17 @@ void DeviceSolver::apply_halo_path(const std::string& path, bool overlap) {
   // the overlap's boundary-first list, or the plain one (the exchange, the put
   // and the push share the plain layout: no re-layout between them)
   if (relay || overlap_ != (overlap && !push_)) setup_items();
+  if (!live) return;
+  // The next sweep (parity par_) reads x[par_ ^ 1]'s halo: the push keeps it in
+  // the receive buffer, the exchange and the put in x — move it across.
+  if (was_push && !push_)
+    for (int b = 0; b < 2; ++b) dev::launch_halo_import(*kp_, b, stream_);
+  if (!was_push && push_) dev::launch_halo_seed(*kp_, par_ ^ 1, stream_);
+  if (overlap_ != was_ov) {  // a fresh boundary-item count for the overlap's targets
+    PE_HIP_CHECK(hipMemsetAsync(&st_->sig, 0, sizeof(st_->sig), stream_));
+    ov_epoch_ = 0;
+  }
+  PE_HIP_CHECK(hipGetLastError());
 }
 
 // The multi-rank halo path, chosen on the job's own transport.  Candidates:
@@ -988,10 +1004,13 @@ void DeviceSolver::apply_halo_path(const std::string& path, bool overlap) {
 // after the sweep), the same through the peer-put kernel (setup_halo_put), each
 // with and without the halo/interior overlap (the exchange on the halo stream
 // under the interior items), and — row slabs with in-sweep P2P sums — the
-// sweep's own halo push.  Each runs 2 + kTimed sweeps of the real iteration
-// (cross-rank sums included, the stop test off) from the initial state; the
-// two fastest are timed once more (min of the two); every time is the max over
-// ranks, so every rank keeps the same path.  Until round 5 the choice was a
+// sweep's own halo push.  From one reset, the candidates take turns on the
+// live iteration (cross-rank sums included, the stop test off; the halo is
+// moved between x and the push's receive buffer at a switch): 1 + 3 sweeps
+// each, the last 3 timed, then the two fastest once more (min of the two);
+// every time is the max over ranks, so every rank keeps the same path.  (A
+// reset per candidate and 2 + 4 sweeps cost 27-30 ms at the 8-rank slab of
+// 8192², round 6.)  Until round 5 the choice was a
 // fixed rule (exchange; overlap when a measured exchange exceeded 12 µs) set
 // from one-GPU probes with simulated 15 / 8 µs delays; the first cross-device
 // run must not rest on a simulation.  PE_HALO=exchange / put / push and
@@ -1045,9 +1064,25 @@ void DeviceSolver::choose_halo_path() {
   Range range("pe.choose_halo_path");
   const int keep_tol = kp_->check_tol;
   kp_->check_tol = 0;
+  // (PE_CTOR_TRACE=1: rank 0's candidate times; 2: every rank's, with the
+  // host-side split of each candidate into switch and timing)
+  const int trace_lvl = std::getenv("PE_CTOR_TRACE") ? std::atoi(std::getenv("PE_CTOR_TRACE")) : 0;
+  const bool trace = trace_lvl >= 2 || (trace_lvl == 1 && blk_.rank == 0);
+  const auto t_reset = clk::now();
+  reset();
+  if (trace_lvl >= 2) {
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    std::fprintf(stderr, "[pe] halo path reset %6.3f ms\n", 1e3 * secs(t_reset, clk::now()));
+  }
   auto time_path = [&](const Cand& c) {
-    apply_halo_path(c.path, c.ov);
-    return time_halo_path(4);
+    const auto ta = clk::now();
+    apply_halo_path(c.path, c.ov, true);
+    const auto tb = clk::now();
+    const double ms = time_halo_path(3, 1, false);
+    if (trace_lvl >= 2)
+      std::fprintf(stderr, "[pe] halo path %-18s apply %6.3f ms, timing %6.3f ms\n", (c.path + (c.ov ? "+overlap" : "")).c_str(),
+                   1e3 * secs(ta, tb), 1e3 * secs(tb, clk::now()));
+    return ms;
   };
   for (Cand& c : cands) {
     c.ms = time_path(c);
@@ -1066,10 +1101,11 @@ void DeviceSolver::choose_halo_path() {
   size_t best = 0;
   for (size_t i = 1; i < cands.size(); ++i)
     if (cands[i].ms < cands[best].ms) best = i;
-  apply_halo_path(cands[best].path, cands[best].ov);
+  apply_halo_path(cands[best].path, cands[best].ov, true);
+  PE_HIP_CHECK(hipStreamSynchronize(stream_));  // (the solve resets the state)
   halo_path_ = name(cands[best]);
   kp_->check_tol = keep_tol;
-  if (std::getenv("PE_CTOR_TRACE") && blk_.rank == 0) {
+  if (trace) {
     for (const auto& c : halo_cands_) std::fprintf(stderr, "[pe] halo path %-24s %8.2f us/sweep\n", c.first.c_str(), c.second);
     std::fprintf(stderr, "[pe] halo path chosen: %s\n", halo_path_.c_str());
   }
@@ -1081,18 +1117,18 @@ void DeviceSolver::set_halo_path(const std::string& path, bool overlap) {
       (path != "push" && path != "put" && path != "exchange"))
     throw std::invalid_argument("set_halo_path: '" + path + "' is not available (push: " + push_status_ +
                                 ", put: " + put_status_ + ")");
-  PE_HIP_CHECK(hipStreamSynchronize(stream_));
-  apply_halo_path(path, overlap);
+  apply_halo_path(path, overlap, true);
   halo_path_ = path + (overlap_ ? "+overlap" : "") + " (set)";
 }
 
-// 2 + `sweeps` sweeps of the real iteration from the initial state (the stop
-// test off), the last `sweeps` timed; ms per sweep, max over ranks.
-double DeviceSolver::time_halo_path(int sweeps) {
+// `warm` + `sweeps` sweeps of the real iteration (the stop test off), from the
+// initial state when `from_reset`, else from the current one; the last
+// `sweeps` timed; ms per sweep, max over ranks.
+double DeviceSolver::time_halo_path(int sweeps, int warm, bool from_reset) {
   const int keep_tol = kp_->check_tol;
   kp_->check_tol = 0;
-  reset();
-  run_iterations(2 * steps_, false);
+  if (from_reset) reset();
+  if (warm > 0) run_iterations(int64_t(warm) * steps_, false);
   PE_HIP_CHECK(hipEventRecord(t0_, stream_));
   run_iterations(int64_t(sweeps) * steps_, false);
   PE_HIP_CHECK(hipEventRecord(t1_, stream_));

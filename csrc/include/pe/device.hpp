@@ -202,10 +202,11 @@ class DeviceSolver {
   const std::string& put_status() const { return put_status_; }
   // Probes: switch to another halo path after construction (one of the
   // candidates the construction could pick; the item list is re-laid out for
-  // the overlap) and time `sweeps` sweeps of it from a reset the way the
-  // construction's choice does (ms per sweep, max over ranks; collective).
+  // the overlap), and time `sweeps` sweeps of the current path after `warm`
+  // ones, from a reset or from the current state (ms per sweep, max over
+  // ranks; collective).
   void set_halo_path(const std::string& path, bool overlap);
-  double time_halo_path(int sweeps);
+  double time_halo_path(int sweeps, int warm = 2, bool from_reset = true);
   uintptr_t fields_address() const { return reinterpret_cast<uintptr_t>(fields_); }
   const std::vector<float>& placement_ms() const { return placement_ms_; }
   int placement_choice() const { return placement_best_; }       // index into placement_ms()
@@ -280,7 +281,8 @@ class DeviceSolver {
   // collective: time the available halo paths (exchange / put / push, with and
   // without the overlap) for a few sweeps each and keep the fastest (max over ranks)
   void choose_halo_path();
-  void apply_halo_path(const std::string& path, bool overlap);  // switch path + re-lay the items
+  // switch path + re-lay the items; live: the iteration state carries on (halo moved between x and the push buffer)
+  void apply_halo_path(const std::string& path, bool overlap, bool live = false);
   // one halo phase through the put kernel (put_) or the comm
   void xfer(const std::vector<Exchange>& ex, hipStream_t s);
   void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
