@@ -837,7 +837,7 @@ void DeviceSolver::setup_halo_put() {
   // (every rank takes part in the collectives below, a rank without
   // neighbours too: its buffer simply stays unused)
   cmax = std::max<int64_t>({cmax, 2 * int64_t(hdep_) * blk_.nx, int64_t(hdep_) * kp_->pitch});
-  put_stride_ = (cmax + 31) / 32 * 32;
+  put_stride_ = (cmax + dev::kPutBoxOff + 31) / 32 * 32;  // (+ the slot's 16-B phase offset)
   const size_t flag_bytes = sizeof(unsigned long long) * 4 * dev::kPutParts * dev::kPutFlagStride;
   const size_t bytes = flag_bytes + sizeof(double) * 4 * 2 * size_t(put_stride_);
   void* buf = nullptr;
@@ -866,7 +866,7 @@ void DeviceSolver::setup_halo_put() {
   // values each) with rank-coded data, checked on arrival; every rank keeps
   // the comm's exchange if any check failed anywhere.
   {
-    const int64_t n = std::min<int64_t>(4096, put_stride_);
+    const int64_t n = std::min<int64_t>(4096, put_stride_ - dev::kPutBoxOff);
     double *sbuf = nullptr, *rbuf = nullptr, *codes = nullptr;
     int* bad = nullptr;
     PE_HIP_CHECK(hipMalloc(&sbuf, sizeof(double) * 4 * n));
@@ -958,7 +958,7 @@ void DeviceSolver::xfer(const std::vector<Exchange>& ex, hipStream_t s) {
   a.parts = want_overlap_ ? 8 : dev::kPutParts;
   for (size_t m = 0; m < ex.size(); ++m) {
     const Exchange& e = ex[m];
-    if (e.count > put_stride_) throw std::logic_error("put: message larger than the inbox");
+    if (e.count + dev::kPutBoxOff > put_stride_) throw std::logic_error("put: message larger than the inbox");
     void* peer = put_peers_[size_t(put_loop_ ? blk_.rank : e.peer)];
     // the peer files this rank's message under the direction it sees us in;
     // a loopback rank under the message's own direction (send → own receive)

@@ -112,6 +112,7 @@ struct PeerSum {
 // a non-finite status) instead of hanging.
 constexpr int kPutParts = 64;  // most blocks per message (PutArgs::parts); each waits only on its own part's flag
 constexpr int kPutFlagStride = 16;  // u64 words per part flag (one 128-B line each)
+constexpr int kPutBoxOff = 1;       // element i of a message at inbox slot[1 + i]: 16-B phase of the x rows (pitch even, column −7 first)
 struct PutMsg {
   const double* src;                  // local send buffer
   double* rbox;                       // the peer's inbox slot for this message (parity 0)

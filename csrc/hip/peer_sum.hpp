@@ -49,13 +49,16 @@ __device__ __forceinline__ void peer_sum_block(const PeerSum& ps, double* v, int
     const unsigned long long* flag = reinterpret_cast<const unsigned long long*>(
         ps.peers[ps.me] + (set * size_t(ps.P) + size_t(t)) * kP2PSlot + kP2PSlot - 1);
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
+    // relaxed spin, one acquire after it (an acquire load per spin would
+    // invalidate the caches on every poll)
+    while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != seq) {
       __builtin_amdgcn_s_sleep(1);
       if ((long long)(__builtin_amdgcn_s_memrealtime() - t0) > ps.timeout_ticks) {
         *sok = 0;  // a peer never arrived: poison instead of hanging
         break;
       }
     }
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
   }
   __syncthreads();
   if (threadIdx.x == 0 && ps.wait_acc) {
