@@ -821,7 +821,6 @@ void DeviceSolver::setup_halo_put() {
   put_ = put_ok_ = false;
   const char* hm = std::getenv("PE_HALO");
   const bool allowed = !hm || std::string(hm) == "put";
-  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
   const char* lb = std::getenv("PE_PUT_LOOPBACK");
   put_loop_ = lb && std::atoi(lb) == 1;
   put_status_ = comm_->size() < 2 ? "off: one rank" : !fused_ ? "off: classic path" : !allowed
@@ -928,7 +927,6 @@ void DeviceSolver::setup_halo_put() {
       return;
     }
   }
-  (void)nb;
   put_ok_ = true;
   put_status_ = put_loop_ ? "loopback (diagnostic)" : "available";
 }
@@ -1018,7 +1016,6 @@ void DeviceSolver::apply_halo_path(const std::string& path, bool overlap, bool l
 // left (exchange, no overlap, when allowed) without timing.
 void DeviceSolver::choose_halo_path() {
   halo_cands_.clear();
-  const bool nb = blk_.has(LEFT) || blk_.has(RIGHT) || blk_.has(DOWN) || blk_.has(UP);
   if (comm_->size() < 2 || !fused_ || resident_) {
     halo_path_ = comm_->size() < 2 ? "none: one rank" : !fused_ ? "exchange (classic path)" : "none: resident";
     apply_halo_path("exchange", false);
@@ -1058,7 +1055,6 @@ void DeviceSolver::choose_halo_path() {
   if (cands.size() == 1 || !tune) {
     apply_halo_path(cands[0].path, cands[0].ov);
     halo_path_ = name(cands[0]) + (cands.size() == 1 ? " (only candidate)" : " (PE_HALO_TUNE=0)");
-    (void)nb;
     return;
   }
   Range range("pe.choose_halo_path");
@@ -1109,7 +1105,6 @@ void DeviceSolver::choose_halo_path() {
     for (const auto& c : halo_cands_) std::fprintf(stderr, "[pe] halo path %-24s %8.2f us/sweep\n", c.first.c_str(), c.second);
     std::fprintf(stderr, "[pe] halo path chosen: %s\n", halo_path_.c_str());
   }
-  (void)nb;
 }
 
 void DeviceSolver::set_halo_path(const std::string& path, bool overlap) {
