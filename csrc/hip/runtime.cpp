@@ -37,11 +37,9 @@ int device_count() {
 // while binding the process to its GPU (like the RCCL / P2P set-up, before any
 // solver), one right after the other: the process has few hardware queues
 // (GPU_MAX_HW_QUEUES, 4 by default) and streams take them in turn, so the
-// pair gets two different queues.  A halo stream created later could land on
-// the solver stream's queue, which serialises the overlap: a fresh solver
-// with the overlap ran the 8-rank slab of 8192² at 52 µs per iteration, the
-// same overlap switched on in a solver whose halo stream had been created
-// early 42.5 (profiles/r6_overlap_steady.txt).  A solver returns its streams
+// pair gets two different queues.  (The overlap's run-to-run variance at the
+// 8-rank slab of 8192² is the boundary-first sweep kernel's own duration, not
+// the queues: profiles/r6_overlap_trace.txt.)  A solver returns its streams
 // here when it is destroyed.
 namespace {
 std::mutex g_stream_mu;
