@@ -618,6 +618,15 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
       best = w.ti;
       keep = w.lay;
     }
+    // the three best heights (any layout), for the overlap's own layout: its
+    // boundary-first filling list ranks them differently (8-rank slab of
+    // 8192²: 64, 80 and 96 rows tie within 1 % on the plain layout, 117-119 µs
+    // per sweep, but the overlapped sweep runs 146, 157 and 128 µs —
+    // profiles/r6_overlap_ti.txt)
+    std::stable_sort(tried.begin(), tried.end(), [](const Tried& a, const Tried& b) { return a.ms < b.ms; });
+    ti_alt_ = {best};
+    for (const Tried& t : tried)
+      if (ti_alt_.size() < 3 && std::find(ti_alt_.begin(), ti_alt_.end(), t.ti) == ti_alt_.end()) ti_alt_.push_back(t.ti);
     lay_name_ = keep;
     set_items(best);
     setup_items();
@@ -968,7 +977,7 @@ void DeviceSolver::xfer(const std::vector<Exchange>& ex, hipStream_t s) {
   PE_HIP_CHECK(hipGetLastError());
 }
 
-void DeviceSolver::apply_halo_path(const std::string& path, bool overlap, bool live) {
+void DeviceSolver::apply_halo_path(const std::string& path, bool overlap, bool live, int ti) {
   const bool was_push = push_, was_ov = overlap_;
   if (live) {  // (the state carries on: nothing of the old path may still be in flight)
     PE_HIP_CHECK(hipStreamSynchronize(stream_));
@@ -977,20 +986,34 @@ void DeviceSolver::apply_halo_path(const std::string& path, bool overlap, bool l
   push_ = path == "push" && push_ok_;
   put_ = path == "put" && put_ok_;
   kp_->push = push_ ? 1 : 0;
-  const bool relay = overlap != want_overlap_;
+  bool relay = overlap != want_overlap_;
   want_overlap_ = overlap;
   for (auto& g : graphs_) PE_HIP_CHECK(hipGraphExecDestroy(g.second));  // captured on the old path
   graphs_.clear();
+  if (ti > 0 && ti != kp_->ti) {  // (another height for the overlap's layout)
+    set_items(ti);
+    relay = true;
+  }
   // the overlap's boundary-first list, or the plain one (the exchange, the put
   // and the push share the plain layout: no re-layout between them)
-  if (relay || overlap_ != (overlap && !push_)) setup_items();
+  const bool relaid = relay || overlap_ != (overlap && !push_);
+  if (relaid) {
+    const auto t0 = clk::now();
+    const double up0 = copy_setup_s_;
+    setup_items();
+    if (live && std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) >= 2)
+      std::fprintf(stderr, "[pe] halo path re-layout %s at %d rows: %6.3f ms (list upload %6.3f ms)\n",
+                   overlap_ ? "overlap" : "plain", kp_->ti, 1e3 * secs(t0, clk::now()), 1e3 * (copy_setup_s_ - up0));
+  }
   if (!live) return;
   // The next sweep (parity par_) reads x[par_ ^ 1]'s halo: the push keeps it in
   // the receive buffer, the exchange and the put in x — move it across.
   if (was_push && !push_)
     for (int b = 0; b < 2; ++b) dev::launch_halo_import(*kp_, b, stream_);
   if (!was_push && push_) dev::launch_halo_seed(*kp_, par_ ^ 1, stream_);
-  if (overlap_ != was_ov) {  // a fresh boundary-item count for the overlap's targets
+  // a fresh boundary-item count for the overlap's targets (epoch × boundary
+  // items of the list: another list — another height — has another count)
+  if (overlap_ != was_ov || (relaid && overlap_)) {
     PE_HIP_CHECK(hipMemsetAsync(&st_->sig, 0, sizeof(st_->sig), stream_));
     ov_epoch_ = 0;
   }
@@ -1031,33 +1054,51 @@ void DeviceSolver::choose_halo_path() {
     std::string path;
     bool ov;
     double ms;
+    int ti;  // rows per item (0: the construction's)
   };
   std::vector<Cand> cands;
+  // The overlapped candidates run at each of the rows-per-item tuning's three
+  // best heights (its boundary-first layout ranks them differently); with the
+  // exchange among the candidates the put's overlap runs only at the height
+  // the exchange's overlap timed best (the halo path does not move that rank).
+  const int ti0 = kp_->ti;
+  std::vector<int> heights = ti_alt_.empty() ? std::vector<int>{ti0} : ti_alt_;
   auto add = [&](const char* path, bool o) {
     if (o && !ov_able) return;
     if (ov && (std::atoi(ov) != 0) != o) return;
-    cands.push_back(Cand{path, o, 0.0});
+    if (!o) {
+      cands.push_back(Cand{path, o, 0.0, 0});
+      return;
+    }
+    for (int h : heights) cands.push_back(Cand{path, o, 0.0, h});
   };
-  // (the plain-layout candidates first, then the overlapped ones: one re-layout)
+  // (the plain-layout candidates first, then the overlapped ones, height by height)
   const bool ex_ok = !hm || std::string(hm) == "exchange";
   if (ex_ok) add("exchange", false);
   if (put_ok_) add("put", false);
-  if (push_ok_ && !(ov && std::atoi(ov) != 0)) cands.push_back(Cand{"push", false, 0.0});
+  if (push_ok_ && !(ov && std::atoi(ov) != 0)) cands.push_back(Cand{"push", false, 0.0, 0});
   if (ex_ok) add("exchange", true);
   // (not when ranks share a GPU — test jobs: put blocks spinning on the halo
   // stream under another process's persistent sweep can starve it of CUs; a
   // 6-process 2×3 job on one GPU stalled past 3 minutes, round 6)
   const bool put_ov_forced = hm && std::string(hm) == "put" && ov && std::atoi(ov) != 0;
-  if (put_ok_ && (!shared_dev_ || put_ov_forced)) add("put", true);
-  if (cands.empty()) cands.push_back(Cand{"exchange", ov && std::atoi(ov) != 0 && ov_able, 0.0});
+  const bool put_ov = put_ok_ && (!shared_dev_ || put_ov_forced) && ov_able && !(ov && std::atoi(ov) == 0);
+  const bool put_ov_late = put_ov && ex_ok && !cands.empty() && cands.back().ov;  // (after the exchange's heights)
+  if (put_ov && !put_ov_late) add("put", true);
+  if (cands.empty()) cands.push_back(Cand{"exchange", ov && std::atoi(ov) != 0 && ov_able, 0.0, 0});
   auto name = [](const Cand& c) { return c.path + (c.ov ? "+overlap" : ""); };
+  // (the overlap at the tuning's second height is reported as "exchange+overlap @96")
+  auto label = [&](const Cand& c) { return name(c) + (c.ov && c.ti != ti0 ? " @" + std::to_string(c.ti) : std::string()); };
   const bool tune = !(std::getenv("PE_HALO_TUNE") && std::atoi(std::getenv("PE_HALO_TUNE")) == 0);
-  if (cands.size() == 1 || !tune) {
-    apply_halo_path(cands[0].path, cands[0].ov);
+  if ((cands.size() == 1 && !put_ov_late) || !tune) {
+    apply_halo_path(cands[0].path, cands[0].ov, false, cands[0].ti);
     halo_path_ = name(cands[0]) + (cands.size() == 1 ? " (only candidate)" : " (PE_HALO_TUNE=0)");
     return;
   }
   Range range("pe.choose_halo_path");
+  lay_cache_.clear();
+  lay_cache_on_ = true;
+  if (fused_) lay_cache_[{kp_->ti, overlap_}] = snap_layout();  // (the construction's)
   const int keep_tol = kp_->check_tol;
   kp_->check_tol = 0;
   // (PE_CTOR_TRACE=1: rank 0's candidate times; 2: every rank's, with the
@@ -1072,17 +1113,26 @@ void DeviceSolver::choose_halo_path() {
   }
   auto time_path = [&](const Cand& c) {
     const auto ta = clk::now();
-    apply_halo_path(c.path, c.ov, true);
+    apply_halo_path(c.path, c.ov, true, c.ov ? c.ti : ti0);
     const auto tb = clk::now();
     const double ms = time_halo_path(3, 1, false);
     if (trace_lvl >= 2)
-      std::fprintf(stderr, "[pe] halo path %-18s apply %6.3f ms, timing %6.3f ms\n", (c.path + (c.ov ? "+overlap" : "")).c_str(),
+      std::fprintf(stderr, "[pe] halo path %-24s apply %6.3f ms, timing %6.3f ms\n", label(c).c_str(),
                    1e3 * secs(ta, tb), 1e3 * secs(tb, clk::now()));
     return ms;
   };
   for (Cand& c : cands) {
     c.ms = time_path(c);
-    halo_cands_.emplace_back(name(c), 1e3 * c.ms);
+    halo_cands_.emplace_back(label(c), 1e3 * c.ms);
+  }
+  if (put_ov_late) {  // the put's overlap at the exchange overlap's best height
+    int h = ti0;
+    double bms = 1e300;
+    for (const Cand& c : cands)
+      if (c.ov && c.ms < bms) bms = c.ms, h = c.ti;
+    cands.push_back(Cand{"put", true, 0.0, h});
+    cands.back().ms = time_path(cands.back());
+    halo_cands_.emplace_back(label(cands.back()), 1e3 * cands.back().ms);
   }
   // finalists: the two fastest once more (the clock ramps during construction)
   std::vector<size_t> order(cands.size());
@@ -1091,15 +1141,17 @@ void DeviceSolver::choose_halo_path() {
   for (size_t f = 0; f < 2 && f < order.size(); ++f) {
     Cand& c = cands[order[f]];
     const double ms = time_path(c);
-    halo_cands_.emplace_back(name(c) + " (again)", 1e3 * ms);
+    halo_cands_.emplace_back(label(c) + " (again)", 1e3 * ms);
     c.ms = std::min(c.ms, ms);
   }
   size_t best = 0;
   for (size_t i = 1; i < cands.size(); ++i)
     if (cands[i].ms < cands[best].ms) best = i;
-  apply_halo_path(cands[best].path, cands[best].ov, true);
+  apply_halo_path(cands[best].path, cands[best].ov, true, cands[best].ov ? cands[best].ti : ti0);
   PE_HIP_CHECK(hipStreamSynchronize(stream_));  // (the solve resets the state)
   halo_path_ = name(cands[best]);
+  lay_cache_on_ = false;
+  lay_cache_.clear();
   kp_->check_tol = keep_tol;
   if (trace) {
     for (const auto& c : halo_cands_) std::fprintf(stderr, "[pe] halo path %-24s %8.2f us/sweep\n", c.first.c_str(), c.second);

@@ -1008,9 +1008,21 @@ __global__ void kWFlushDone(KParams k) { k.st->wpend = 0; }
 // its XCD's L2 back (agent-scope release).  Targets are cumulative per solve.
 __global__ void kWaitSig(DevState* st, unsigned long long target) {
   if (threadIdx.x == 0) {
+    // (polled every ≈1 µs: the boundary items take tens of µs, and a
+    // tighter poll of the state's line competes with the sweep's traffic)
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
     while (__hip_atomic_load(&st->sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target &&
-           !__hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-      __builtin_amdgcn_s_sleep(4);
+           !__hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+      __builtin_amdgcn_s_sleep(40);
+      // a target the sweeps never reach (a host-side count error) ends the
+      // solve as an internal error (status 5) after 30 s instead of hanging
+      // the stream: every later kernel is then a no-op
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 3000000000ull) {
+        __hip_atomic_store(&st->status, 5, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(&st->done, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        break;
+      }
+    }
     __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "agent");
   }
 }

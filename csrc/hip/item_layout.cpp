@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <exception>
 #include <map>
 #include <limits>
 #include <mutex>
@@ -78,6 +79,24 @@ void DeviceSolver::setup_items() {
   // heavy items split, below) and the overlap; orders 1 / 2 are plain
   // tuning walks.
   if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
+  if (lay_cache_on_) {
+    auto it = lay_cache_.find({k.ti, overlap_});
+    if (it != lay_cache_.end()) {
+      restore_layout(it->second);
+      return;
+    }
+  }
+  struct Keep {  // (files the finished layout in the cache on every return below)
+    DeviceSolver* s;
+    ~Keep() {
+      if (s->lay_cache_on_ && std::uncaught_exceptions() == 0) s->lay_cache_[{s->kp_->ti, s->overlap_}] = s->snap_layout();
+    }
+  } keep{this};
+  const bool trace3 = std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) >= 3;
+  const auto tl0 = clk::now();
+  auto lap = [&](const char* what) {
+    if (trace3) std::fprintf(stderr, "[pe]   layout %-14s %7.3f ms\n", what, 1e3 * secs(tl0, clk::now()));
+  };
   // (re-laid out by the rows-per-item tuning: the list buffer is reused while
   // it is large enough — a free per candidate synchronised the device)
   auto list_alloc = [&](size_t n) {
@@ -144,6 +163,7 @@ void DeviceSolver::setup_items() {
   // re-lays out up to 11 times, and evaluating the rows one by one per item
   // took 4.5-5.7 ms per layout at 4096², inside T_solver).
   const int64_t q0 = 1 - H, R = blk_.nx + 2 * H;
+  lap("start");
   if (pgen_.empty()) {
     pgen_.assign(size_t(k.nstrips) * size_t(R + 1), 0);
     pmix_.assign(size_t(k.nstrips) * size_t(R + 1), 0);
@@ -250,6 +270,7 @@ void DeviceSolver::setup_items() {
           pcs.push_back(Piece{a0, a1 - a0, s, rows_cost(a0, a1 - 1, s) + overhead, bnd});
         }
       }
+    lap("pieces");
     // Three-step sweep: a filling layout instead.  The sweep's time per row
     // step depends on the item's kind — a boundary-band item ≈2.2×, a mixed
     // one ≈1.3× a uniform one (tools/stamp_probe.py, profiles/r4_stamps.txt)
@@ -537,50 +558,59 @@ void DeviceSolver::setup_items() {
       W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(total / minc)) / dev::kWPB) * dev::kWPB);
       const double cut_cost = double(2 * H) + overhead;  // a cut's extra (uniform) row steps
       int cuts = 0;
+      // each piece's wave (pcs order; the per-wave lists are built once, after
+      // the last pass: W vectors grown per pass were most of the layout's time)
+      std::vector<int> own;
       for (int pass = 0; pass < 4; ++pass) {
         const double T = (total + cuts * cut_cost) / W;
         pcs.clear();
-        per.assign(size_t(W), {});
+        own.clear();
         load.assign(size_t(W), 0.0);
         nbnd = 0;
         int ncut = 0;
+        // (queued pieces by index into qp: a heap of 16-byte entries)
         struct QE {
           double cost;
-          int seq;
-          Piece p;
+          int seq, idx;
           bool operator<(const QE& o) const { return cost < o.cost || (cost == o.cost && seq > o.seq); }
         };
-        std::priority_queue<QE> q;
+        std::vector<Piece> qp;
+        qp.reserve(whole.size() + whole.size() / 2);
+        std::vector<QE> qv;
+        qv.reserve(whole.size());
         for (int i = 0; i < int(whole.size()); ++i) {
           const Piece& p = whole[size_t(i)];
           if (p.bnd) {  // boundary pieces: positions 0, 1, … in order (first round)
-            per[size_t(nbnd % W)].push_back(int(pcs.size()));
+            own.push_back(nbnd % W);
             load[size_t(nbnd % W)] += p.cost;
             pcs.push_back(p);
             ++nbnd;
           } else {
-            q.push(QE{p.cost, i, p});
+            qv.push_back(QE{p.cost, i, int(qp.size())});
+            qp.push_back(p);
           }
         }
+        std::priority_queue<QE> q(std::less<QE>(), std::move(qv));
         using LW = std::pair<double, int>;
         std::priority_queue<LW, std::vector<LW>, std::greater<LW>> heap;
         double csum = 0.0;
         for (int w = 0; w < W; ++w) csum += capw(w, W);
         for (int w = 0; w < W; ++w) heap.push(LW{load[size_t(w)] / capw(w, W), wrank(w, W)});
         while (!q.empty()) {
-          QE e = q.top();
+          const QE e = q.top();
           q.pop();
+          const Piece ep = qp[size_t(e.idx)];
           const LW t = heap.top();
           heap.pop();
           const int tw = wfrom(t.second, W);
           const double room = (rho == 1.0 ? T : T * W * capw(tw, W) / csum) - load[size_t(tw)];
-          Piece give = e.p;
-          if (e.p.cost > room && room >= minc && e.p.rows >= 2 * minr) {
-            // the most rows of e.p that fit the room (binary search; cost grows with rows)
-            int64_t lo = minr, hi = e.p.rows - minr, best = 0;
+          Piece give = ep;
+          if (ep.cost > room && room >= minc && ep.rows >= 2 * minr) {
+            // the most rows of ep that fit the room (binary search; cost grows with rows)
+            int64_t lo = minr, hi = ep.rows - minr, best = 0;
             while (lo <= hi) {
               const int64_t mid = (lo + hi) / 2;
-              if (pcost(e.p.ib, mid, e.p.s) <= room) {
+              if (pcost(ep.ib, mid, ep.s) <= room) {
                 best = mid;
                 lo = mid + 1;
               } else {
@@ -588,13 +618,14 @@ void DeviceSolver::setup_items() {
               }
             }
             if (best > 0) {
-              give = Piece{e.p.ib, best, e.p.s, pcost(e.p.ib, best, e.p.s), false};
-              const Piece rest{e.p.ib + best, e.p.rows - best, e.p.s, pcost(e.p.ib + best, e.p.rows - best, e.p.s), false};
-              q.push(QE{rest.cost, e.seq, rest});
+              give = Piece{ep.ib, best, ep.s, pcost(ep.ib, best, ep.s), false};
+              const Piece rest{ep.ib + best, ep.rows - best, ep.s, pcost(ep.ib + best, ep.rows - best, ep.s), false};
+              q.push(QE{rest.cost, e.seq, int(qp.size())});
+              qp.push_back(rest);
               ++ncut;
             }
           }
-          per[size_t(tw)].push_back(int(pcs.size()));
+          own.push_back(tw);
           pcs.push_back(give);
           load[size_t(tw)] += give.cost;
           heap.push(LW{load[size_t(tw)] / capw(tw, W), t.second});
@@ -602,6 +633,11 @@ void DeviceSolver::setup_items() {
         if (ncut == cuts) break;
         cuts = ncut;
       }
+      std::vector<int> cnt(size_t(W), 0);
+      for (int w : own) ++cnt[size_t(w)];
+      per.assign(size_t(W), {});
+      for (int w = 0; w < W; ++w) per[size_t(w)].reserve(size_t(cnt[size_t(w)]));
+      for (size_t i = 0; i < own.size(); ++i) per[size_t(own[i])].push_back(int(i));
       lay_cuts_ = cuts;
     } else {
     // Three-step LPT.  A band item runs EVERY row step on the band path
@@ -650,6 +686,7 @@ void DeviceSolver::setup_items() {
     }
     lay_cuts_ = 0;
     }
+    lap(lay_used_.c_str());
     size_t rounds = 0;
     for (const auto& v : per) rounds = std::max(rounds, v.size());
     lay_max_ = 0.0;
@@ -711,6 +748,7 @@ void DeviceSolver::setup_items() {
     // the blocks the overlap keeps free for the halo stream)
     k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
     if (overlap_) create_halo_stream();
+    lap("list");
     return;
   }
   lay_max_ = lay_mean_ = 0.0;
@@ -783,6 +821,56 @@ void DeviceSolver::setup_items() {
   k.nslots = int(all.size());
   for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
   for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
+  if (overlap_) create_halo_stream();
+}
+
+DeviceSolver::LayoutSnap DeviceSolver::snap_layout() const {
+  const KParams& k = *kp_;
+  LayoutSnap v;
+  v.list = ilist_host_;
+  v.static_waves = static_waves_;
+  v.ov_nb = ov_nb_;
+  v.ov_lnsh = ov_lnsh_;
+  std::copy(ov_lbase_, ov_lbase_ + 9, v.ov_lbase);
+  std::copy(ov_lnb_, ov_lnb_ + 8, v.ov_lnb);
+  v.lay_items = lay_items_;
+  v.lay_cuts = lay_cuts_;
+  v.lay_max = lay_max_;
+  v.lay_mean = lay_mean_;
+  v.lay_used = lay_used_;
+  v.lnsh = k.lnsh;
+  v.lwaves = k.lwaves;
+  v.nslots = k.nslots;
+  std::copy(k.lbase, k.lbase + 9, v.lbase);
+  std::copy(k.lnb, k.lnb + 8, v.lnb);
+  v.nblocks = k.nblocks;
+  v.nblocks0 = k.nblocks0;
+  return v;
+}
+
+void DeviceSolver::restore_layout(const LayoutSnap& v) {
+  KParams& k = *kp_;
+  if (v.list.size() > ilist_cap_) throw std::logic_error("cached item list larger than the list buffer");
+  upload(ilist_, v.list.data(), sizeof(int2) * v.list.size());
+  ilist_host_ = v.list;
+  static_waves_ = v.static_waves;
+  ov_nb_ = v.ov_nb;
+  ov_lnsh_ = v.ov_lnsh;
+  std::copy(v.ov_lbase, v.ov_lbase + 9, ov_lbase_);
+  std::copy(v.ov_lnb, v.ov_lnb + 8, ov_lnb_);
+  lay_items_ = v.lay_items;
+  lay_cuts_ = v.lay_cuts;
+  lay_max_ = v.lay_max;
+  lay_mean_ = v.lay_mean;
+  lay_used_ = v.lay_used;
+  k.ilist = ilist_;
+  k.lnsh = v.lnsh;
+  k.lwaves = v.lwaves;
+  k.nslots = v.nslots;
+  std::copy(v.lbase, v.lbase + 9, k.lbase);
+  std::copy(v.lnb, v.lnb + 8, k.lnb);
+  k.nblocks = v.nblocks;
+  k.nblocks0 = v.nblocks0;
   if (overlap_) create_halo_stream();
 }
 

@@ -8,6 +8,7 @@
 
 #include <memory>
 #include <stdexcept>
+#include <map>
 #include <string>
 #include <vector>
 
@@ -281,8 +282,21 @@ class DeviceSolver {
   // collective: time the available halo paths (exchange / put / push, with and
   // without the overlap) for a few sweeps each and keep the fastest (max over ranks)
   void choose_halo_path();
+  // Item lists already laid out, by (rows per item, overlap), while the halo
+  // path is chosen (its candidates switch back and forth between a few
+  // layouts: 1.3-2.1 ms of host work each at the 8-rank slab of 8192²)
+  struct LayoutSnap {
+    std::vector<int2> list;
+    int static_waves, ov_nb, ov_lnsh, ov_lbase[9], ov_lnb[8], lay_items, lay_cuts;
+    double lay_max, lay_mean;
+    std::string lay_used;
+    int lnsh, lwaves, nslots, lbase[9], lnb[8], nblocks, nblocks0;
+  };
   // switch path + re-lay the items; live: the iteration state carries on (halo moved between x and the push buffer)
-  void apply_halo_path(const std::string& path, bool overlap, bool live = false);
+  // ti > 0: rows per item of the overlap's layout (another height than the tuning's)
+  void apply_halo_path(const std::string& path, bool overlap, bool live = false, int ti = 0);
+  LayoutSnap snap_layout() const;
+  void restore_layout(const LayoutSnap& v);
   // one halo phase through the put kernel (put_) or the comm
   void xfer(const std::vector<Exchange>& ex, hipStream_t s);
   void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
@@ -382,6 +396,7 @@ class DeviceSolver {
   bool tune_ti_ = false;          // rows per item chosen by timing candidate sweeps
   std::vector<float> ti_ms_;      // their per-sweep times
   std::vector<int> ti_rows_;      // the candidates timed
+  std::vector<int> ti_alt_;       // the tuning's best two heights (the overlap is timed at both)
   double lay_max_ = 0, lay_mean_ = 0;  // static layout: heaviest / mean wave load (row steps)
   int lay_items_ = 0;                  // static layout: most items on one wave
   int lay_cuts_ = 0;                   // three-step filling layout: items cut to fill the waves
@@ -390,6 +405,8 @@ class DeviceSolver {
   std::string lay_name_ = "lpt", lay_used_ = "lpt";
   std::vector<int> peer_access_;
   std::vector<int2> ilist_host_;
+  std::map<std::pair<int, bool>, LayoutSnap> lay_cache_;
+  bool lay_cache_on_ = false;
   std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   int cus_ = 256;                  // compute units of the device (a static layout's first cus_ workgroups run first on their CU)

@@ -31,7 +31,8 @@ for rep in range(int(os.environ.get("PROBE_REPS", "4"))):
     s.reset()
     dt = s.time_iterations(60, False)
     print(f"rep {rep}: {s.halo_path}: {dt / 60 * 1e6:.1f} us/iter  (rows per item {s.ti}, layout {s.layout_name}, "
-          f"tuning {[(r, round(m, 4)) for r, m in zip(s.ti_tuning_rows, s.ti_tuning_ms)]})", flush=True)
+          f"tuning {[(r, round(m, 4)) for r, m in zip(s.ti_tuning_rows, s.ti_tuning_ms)]}; "
+          f"halo candidates {[(n, round(t, 1)) for n, t in s.halo_candidates]})", flush=True)
     s.synchronize()
     time.sleep(0.02)
     del s, comm
