@@ -553,6 +553,7 @@ void DeviceSolver::setup_items() {
             if (r0 <= ie) add_whole(r0, ie - r0 + 1, sx, true);
           }
         }
+      lap("fill: pieces");
       const int64_t minr = 8;  // shortest cut piece (its 2H fill rows cost more than it)
       const double minc = double(minr + 2 * H) + overhead;
       W = std::max(dev::kWPB, (std::min<int>(waves_avail, int(total / minc)) / dev::kWPB) * dev::kWPB);
@@ -561,6 +562,11 @@ void DeviceSolver::setup_items() {
       // each piece's wave (pcs order; the per-wave lists are built once, after
       // the last pass: W vectors grown per pass were most of the layout's time)
       std::vector<int> own;
+      // (on blocks of about one item per wave the passes alternate between
+      // many cuts and few — 8-rank slab of 8192² at 96 rows: 1744 / 175 — and
+      // the fourth pass's is kept; keeping the pass of the lowest estimated
+      // makespan measured the same, whole pieces without cuts 1.5× slower:
+      // profiles/r6_fill_passes.txt)
       for (int pass = 0; pass < 4; ++pass) {
         const double T = (total + cuts * cut_cost) / W;
         pcs.clear();
@@ -630,6 +636,8 @@ void DeviceSolver::setup_items() {
           load[size_t(tw)] += give.cost;
           heap.push(LW{load[size_t(tw)] / capw(tw, W), t.second});
         }
+        if (trace3) std::fprintf(stderr, "[pe]   layout fill pass %d: %zu pieces, %d cuts, W %d\n", pass, pcs.size(), ncut, W);
+        lap("fill: pass");
         if (ncut == cuts) break;
         cuts = ncut;
       }
