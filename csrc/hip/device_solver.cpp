@@ -59,7 +59,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     : prob_(prob), blk_(blk), comm_(comm), opt_(opt), kp_(std::make_unique<KParams>()) {
   const auto t_ctor = clk::now();
   // PE_CTOR_TRACE=1: wall time of each construction phase → stderr
-  const bool ctor_trace = std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) == 1;
+  const bool ctor_trace = std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) >= 1;
   auto t_mark = t_ctor;
   auto mark = [&](const char* phase) {
     if (!ctor_trace) return;
@@ -543,32 +543,61 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // one candidate: S_0 + 1 + kTimed local sweeps on real data, the last
     // kTimed timed (round 3: S_0 + 2 + 6 — construction is inside T_solver)
     constexpr int kTimed = 4;
-    auto time_layout = [&]() {
-      enqueue_init();
-      dev::launch_S(*kp_, 1, stream_);
-      dev::launch_S(*kp_, 0, stream_);
-      PE_HIP_CHECK(hipEventRecord(t0_, stream_));
-      for (int i = 0; i < kTimed; ++i) dev::launch_S(*kp_, (i + 1) & 1, stream_);
-      PE_HIP_CHECK(hipEventRecord(t1_, stream_));
-      PE_HIP_CHECK(hipEventSynchronize(t1_));
-      float ms = 0.f;
-      PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
-      return ms;
+    // Trials run pipelined: the host lays out trial i+1 while the GPU times
+    // trial i (the list upload is stream-ordered after those sweeps), and
+    // layouts already built come from the cache (the finalists, the final
+    // one).  The host layouts were ≈ half of the tuning's time (4096²: 1-2.4
+    // ms each against 1.7-2 ms of timing, PE_CTOR_TRACE=3,
+    // profiles/r6_ctor_tuning.txt).
+    struct Trial {
+      int ti;
+      std::string lay;
     };
-    for (int cand : cands) {
-      const auto tl = clk::now();
-      set_items(cand);
-      setup_items();
-      const auto tg = clk::now();
-      const float ms = time_layout();
-      if (ctor_trace)
-        std::fprintf(stderr, "[pe] ctor   tune %3d rows: layout %7.3f ms, timing %7.3f ms\n", cand,
-                     1e3 * secs(tl, tg), 1e3 * secs(tg, clk::now()));
-      ti_ms_.push_back(ms / float(kTimed));
-      ti_rows_.push_back(cand);
-      if (best_ms == 0.f || ms < best_ms) {
-        best_ms = ms;
-        best = cand;
+    lay_cache_.clear();
+    lay_cache_on_ = true;
+    auto run_trials = [&](const std::vector<Trial>& trials) {
+      std::vector<float> out;
+      for (size_t i = 0; i <= trials.size(); ++i) {
+        const auto tl = clk::now();
+        if (i < trials.size()) {
+          lay_name_ = trials[i].lay;
+          set_items(trials[i].ti);
+          setup_items();  // (its upload waits for trial i-1's sweeps)
+        }
+        const auto tg = clk::now();
+        if (i > 0) {
+          PE_HIP_CHECK(hipEventSynchronize(t1_));
+          float ms = 0.f;
+          PE_HIP_CHECK(hipEventElapsedTime(&ms, t0_, t1_));
+          out.push_back(ms);
+          if (ctor_trace)
+            std::fprintf(stderr, "[pe] ctor   tune %3d rows %-5s %8.4f ms per sweep\n", trials[i - 1].ti,
+                         trials[i - 1].lay.c_str(), ms / float(kTimed));
+        }
+        if (i == trials.size()) break;
+        enqueue_init();
+        dev::launch_S(*kp_, 1, stream_);
+        dev::launch_S(*kp_, 0, stream_);
+        PE_HIP_CHECK(hipEventRecord(t0_, stream_));
+        for (int j = 0; j < kTimed; ++j) dev::launch_S(*kp_, (j + 1) & 1, stream_);
+        PE_HIP_CHECK(hipEventRecord(t1_, stream_));
+        if (ctor_trace)
+          std::fprintf(stderr, "[pe] ctor   tune %3d rows %-5s layout %7.3f ms\n", trials[i].ti, trials[i].lay.c_str(),
+                       1e3 * secs(tl, tg));
+      }
+      return out;
+    };
+    {
+      std::vector<Trial> tr;
+      for (int cand : cands) tr.push_back(Trial{cand, lay_name_});
+      const std::vector<float> ms = run_trials(tr);
+      for (size_t i = 0; i < tr.size(); ++i) {
+        ti_ms_.push_back(ms[i] / float(kTimed));
+        ti_rows_.push_back(tr[i].ti);
+        if (best_ms == 0.f || ms[i] < best_ms) {
+          best_ms = ms[i];
+          best = tr[i].ti;
+        }
       }
     }
     // three-step: the other static layouts at the best height
@@ -582,18 +611,17 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     for (size_t i = 0; i < ti_rows_.size(); ++i) tried.push_back(Tried{ti_rows_[i], lay_name_, ti_ms_[i] * float(kTimed)});
     if (steps_ >= 3 && !std::getenv("PE_LAYOUT")) {
       const std::string base = lay_name_;
-      for (const char* alt : {"equal", "fill", "lpt"}) {
-        if (base == alt) continue;
-        lay_name_ = alt;
-        set_items(best);
-        setup_items();
-        const float ms = time_layout();
-        ti_ms_.push_back(ms / float(kTimed));
+      std::vector<Trial> tr;
+      for (const char* alt : {"equal", "fill", "lpt"})
+        if (base != alt) tr.push_back(Trial{best, alt});
+      const std::vector<float> ms = run_trials(tr);
+      for (size_t i = 0; i < tr.size(); ++i) {
+        ti_ms_.push_back(ms[i] / float(kTimed));
         ti_rows_.push_back(-best);  // (negative: a layout candidate at that height)
-        tried.push_back(Tried{best, alt, ms});
-        if (ms < best_ms) {
-          best_ms = ms;
-          keep = alt;
+        tried.push_back(Tried{best, tr[i].lay, ms[i]});
+        if (ms[i] < best_ms) {
+          best_ms = ms[i];
+          keep = tr[i].lay;
         }
       }
     }
@@ -604,15 +632,12 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     // 96, T_iterate 0.099 vs 0.095 s, profiles/r5_prio.txt).  Three-step only.
     if (steps_ >= 3 && tried.size() >= 2) {
       std::stable_sort(tried.begin(), tried.end(), [](const Tried& a, const Tried& b) { return a.ms < b.ms; });
+      const std::vector<float> ms = run_trials({Trial{tried[0].ti, tried[0].lay}, Trial{tried[1].ti, tried[1].lay}});
       for (int f = 0; f < 2; ++f) {
         Tried& t = tried[size_t(f)];
-        lay_name_ = t.lay;
-        set_items(t.ti);
-        setup_items();
-        const float ms = time_layout();
-        ti_ms_.push_back(ms / float(kTimed));
+        ti_ms_.push_back(ms[size_t(f)] / float(kTimed));
         ti_rows_.push_back(t.lay == keep && t.ti == best ? best : -t.ti);
-        t.ms = std::min(t.ms, ms);
+        t.ms = std::min(t.ms, ms[size_t(f)]);
       }
       const Tried& w = tried[0].ms <= tried[1].ms ? tried[0] : tried[1];
       best = w.ti;
@@ -630,6 +655,8 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     lay_name_ = keep;
     set_items(best);
     setup_items();
+    lay_cache_on_ = false;
+    lay_cache_.clear();
   }
   if (fused_ && std::getenv("PE_STAMPS") && std::atoi(std::getenv("PE_STAMPS")) == 1) {
     const size_t nw = size_t(dev::kWPB) * size_t(std::max(k.nblocks, k.nblocks0));
@@ -668,6 +695,7 @@ DeviceSolver::DeviceSolver(const Problem& prob, const Block& blk, DeviceComm* co
     k.hrecv = hrecv_;
   }
   k.push = 0;
+  mark("ti tuning");
   choose_halo_path();
   mark("halo path");
 
@@ -1098,7 +1126,7 @@ void DeviceSolver::choose_halo_path() {
   Range range("pe.choose_halo_path");
   lay_cache_.clear();
   lay_cache_on_ = true;
-  if (fused_) lay_cache_[{kp_->ti, overlap_}] = snap_layout();  // (the construction's)
+  if (fused_) lay_cache_[{kp_->ti, overlap_, lay_name_}] = snap_layout();  // (the construction's)
   const int keep_tol = kp_->check_tol;
   kp_->check_tol = 0;
   // (PE_CTOR_TRACE=1: rank 0's candidate times; 2: every rank's, with the

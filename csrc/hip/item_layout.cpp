@@ -5,6 +5,7 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <array>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -80,7 +81,7 @@ void DeviceSolver::setup_items() {
   // tuning walks.
   if (!fused_ || ((k.order == 1 || k.order == 2) && !overlap_)) return;
   if (lay_cache_on_) {
-    auto it = lay_cache_.find({k.ti, overlap_});
+    auto it = lay_cache_.find({k.ti, overlap_, lay_name_});
     if (it != lay_cache_.end()) {
       restore_layout(it->second);
       return;
@@ -89,7 +90,8 @@ void DeviceSolver::setup_items() {
   struct Keep {  // (files the finished layout in the cache on every return below)
     DeviceSolver* s;
     ~Keep() {
-      if (s->lay_cache_on_ && std::uncaught_exceptions() == 0) s->lay_cache_[{s->kp_->ti, s->overlap_}] = s->snap_layout();
+      if (s->lay_cache_on_ && std::uncaught_exceptions() == 0)
+        s->lay_cache_[{s->kp_->ti, s->overlap_, s->lay_name_}] = s->snap_layout();
     }
   } keep{this};
   const bool trace3 = std::getenv("PE_CTOR_TRACE") && std::atoi(std::getenv("PE_CTOR_TRACE")) >= 3;
@@ -101,6 +103,9 @@ void DeviceSolver::setup_items() {
   // it is large enough — a free per candidate synchronised the device)
   auto list_alloc = [&](size_t n) {
     if (n <= ilist_cap_) return;
+    // (the rows-per-item tuning lays out while the previous candidate's
+    // sweeps, which read the old list, may still run)
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
     if (ilist_) PE_HIP_CHECK(hipFree(ilist_));
     ilist_cap_ = std::max(n, ilist_cap_ + ilist_cap_ / 2);
     PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * ilist_cap_));
@@ -362,26 +367,36 @@ void DeviceSolver::setup_items() {
         bool bnd;
         int n;
       };
-      std::vector<Seg> segs;
-      for (int sx = 0; sx < ns; ++sx) {
-        auto kind = [&](int64_t q) {  // 2 band, 1 mixed, 0 uniform (window q-H .. q+H)
-          return ngen(q - H, q + H, sx) > 0 ? 2 : nmix(q - H, q + H, sx) > 0 ? 1 : 0;
-        };
-        int64_t a = 1;
-        int ka = kind(1);
-        for (int64_t q = 2; q <= nx + 1; ++q) {
-          const int kq = q <= nx ? kind(q) : -1;
-          // (pieces: also split where a neighbour's halo rows begin, so the push /
-          // overlap boundary pieces stay small)
-          const bool cut_b = (push_first || overlap_) && ((blk_.has(LEFT) && q == H + 1) || (blk_.has(RIGHT) && q == nx - H + 1));
-          if (kq != ka || cut_b) {
-            segs.push_back(Seg{a, q - a, sx, ka == 2 ? fband : ka == 1 ? fmixed : 1.0, false, 1});
-            a = q;
-            ka = kq;
+      // (the runs do not depend on the rows per item: found once per solver
+      // and overlap setting — the scan of every row of every strip was a
+      // quarter of each of the tuning's layouts)
+      std::vector<std::array<int64_t, 4>>& runs = eq_runs_[overlap_ ? 1 : 0];
+      if (runs.empty()) {
+        for (int sx = 0; sx < ns; ++sx) {
+          auto kind = [&](int64_t q) {  // 2 band, 1 mixed, 0 uniform (window q-H .. q+H)
+            return ngen(q - H, q + H, sx) > 0 ? 2 : nmix(q - H, q + H, sx) > 0 ? 1 : 0;
+          };
+          int64_t a = 1;
+          int ka = kind(1);
+          for (int64_t q = 2; q <= nx + 1; ++q) {
+            const int kq = q <= nx ? kind(q) : -1;
+            // (pieces: also split where a neighbour's halo rows begin, so the push /
+            // overlap boundary pieces stay small)
+            const bool cut_b = (push_first || overlap_) && ((blk_.has(LEFT) && q == H + 1) || (blk_.has(RIGHT) && q == nx - H + 1));
+            if (kq != ka || cut_b) {
+              runs.push_back({a, q - a, sx, ka});
+              a = q;
+              ka = kq;
+            }
           }
         }
       }
-      for (Seg& g : segs) g.bnd = is_boundary(g.a, g.a + g.rows - 1, g.s);
+      std::vector<Seg> segs;
+      segs.reserve(runs.size());
+      for (const auto& r : runs)
+        segs.push_back(Seg{r[0], r[1], int(r[2]), r[3] == 2 ? fband : r[3] == 1 ? fmixed : 1.0,
+                           is_boundary(r[0], r[0] + r[1] - 1, int(r[2])), 1});
+      lap("equal: runs");
       const int64_t minr = 8, maxr = 128;  // (pieces of the tuned heights' range)
       auto Fk = [&](double f) { return double(2 * H) * f + overhead; };  // a piece's fill rows + overhead
       // pieces of a run for a piece cost X: rows·f / (X − F) rounded, within [rows/maxr, rows/minr]
@@ -413,6 +428,7 @@ void DeviceSolver::setup_items() {
         (count(mid) > P ? lo : hi) = mid;
       }
       for (Seg& g : segs) g.n = nfor(g, hi);
+      lap("equal: bisect");
       // exactly P: add pieces where they are largest, remove where the merge is cheapest
       int64_t have = count(hi);
       auto pc = [&](const Seg& g, int n) { return double(g.rows) * g.f / n + Fk(g.f); };
@@ -433,6 +449,8 @@ void DeviceSolver::setup_items() {
         segs[size_t(best)].n += have < P ? 1 : -1;
         have += have < P ? 1 : -1;
       }
+      lap("equal: exact P");
+      if (trace3) std::fprintf(stderr, "[pe]   layout equal: %zu runs, %lld pieces\n", segs.size(), (long long)P);
       pcs.clear();
       for (const Seg& g : segs)
         for (int j = 0; j < g.n; ++j) {
@@ -465,6 +483,7 @@ void DeviceSolver::setup_items() {
       // waves so far, heaviest first, and the rest (within ±15 %) the
       // remaining waves in order, so neighbouring strips stay on
       // neighbouring waves.
+      lap("equal: sorted");
       per.assign(size_t(W), {});
       std::vector<double> wl(size_t(W), 0.0);
       std::vector<char> taken(size_t(W), 0);

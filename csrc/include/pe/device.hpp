@@ -8,7 +8,9 @@
 
 #include <memory>
 #include <stdexcept>
+#include <array>
 #include <map>
+#include <tuple>
 #include <string>
 #include <vector>
 
@@ -282,9 +284,9 @@ class DeviceSolver {
   // collective: time the available halo paths (exchange / put / push, with and
   // without the overlap) for a few sweeps each and keep the fastest (max over ranks)
   void choose_halo_path();
-  // Item lists already laid out, by (rows per item, overlap), while the halo
-  // path is chosen (its candidates switch back and forth between a few
-  // layouts: 1.3-2.1 ms of host work each at the 8-rank slab of 8192²)
+  // Item lists already laid out, while the rows per item are tuned and the
+  // halo path is chosen (their candidates come back to layouts already built:
+  // 0.3-2.6 ms of host work each)
   struct LayoutSnap {
     std::vector<int2> list;
     int static_waves, ov_nb, ov_lnsh, ov_lbase[9], ov_lnb[8], lay_items, lay_cuts;
@@ -359,6 +361,7 @@ class DeviceSolver {
   int2* ilist_ = nullptr;  // per shard: boundary items, heavy items, the rest (dev::KParams::ilist)
   size_t ilist_cap_ = 0;   // entries allocated at ilist_
   std::vector<int> pgen_, pmix_;  // item layout: per strip, prefix counts of band / mixed rows (item_layout.cpp)
+  std::vector<std::array<int64_t, 4>> eq_runs_[2];  // equal-cost layout: runs {first row, rows, strip, kind} (no overlap / overlap)
   int nslot_cap_ = 0;      // item-sum slots allocated
   int ov_lnsh_ = 1, ov_nb_ = 0, ov_reserve_ = 8, ov_debug_ = 0;
   int wave_cap_ = 0;     // resident waves of the sweep grid (occupancy)
@@ -405,7 +408,7 @@ class DeviceSolver {
   std::string lay_name_ = "lpt", lay_used_ = "lpt";
   std::vector<int> peer_access_;
   std::vector<int2> ilist_host_;
-  std::map<std::pair<int, bool>, LayoutSnap> lay_cache_;
+  std::map<std::tuple<int, bool, std::string>, LayoutSnap> lay_cache_;  // (rows per item, overlap, layout name)
   bool lay_cache_on_ = false;
   std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
