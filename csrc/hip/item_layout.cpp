@@ -579,13 +579,21 @@ void DeviceSolver::setup_items() {
       const double cut_cost = double(2 * H) + overhead;  // a cut's extra (uniform) row steps
       int cuts = 0;
       // each piece's wave (pcs order; the per-wave lists are built once, after
-      // the last pass: W vectors grown per pass were most of the layout's time)
+      // the last pass)
       std::vector<int> own;
       // (on blocks of about one item per wave the passes alternate between
       // many cuts and few — 8-rank slab of 8192² at 96 rows: 1744 / 175 — and
       // the fourth pass's is kept; keeping the pass of the lowest estimated
       // makespan measured the same, whole pieces without cuts 1.5× slower:
-      // profiles/r6_fill_passes.txt)
+      // profiles/r6_fill_passes.txt.  Once the cut count returns to an
+      // earlier pass's input the rest of the passes repeat earlier ones, so
+      // the loop stops there with the result the fourth pass would give.)
+      struct PassRes {
+        std::vector<Piece> pcs;
+        std::vector<int> own;
+        int nbnd = 0, ncut = 0;
+      } prev;
+      int in_prev = -1;
       for (int pass = 0; pass < 4; ++pass) {
         const double T = (total + cuts * cut_cost) / W;
         pcs.clear();
@@ -658,6 +666,18 @@ void DeviceSolver::setup_items() {
         if (trace3) std::fprintf(stderr, "[pe]   layout fill pass %d: %zu pieces, %d cuts, W %d\n", pass, pcs.size(), ncut, W);
         lap("fill: pass");
         if (ncut == cuts) break;
+        if (pass >= 1 && ncut == in_prev) {  // inputs now alternate: pass 3 repeats pass 1
+          if (pass % 2 == 0) {
+            pcs = std::move(prev.pcs);
+            own = std::move(prev.own);
+            nbnd = prev.nbnd;
+            ncut = prev.ncut;
+          }
+          cuts = ncut;
+          break;
+        }
+        if (pass < 3) prev = PassRes{pcs, own, nbnd, ncut};
+        in_prev = cuts;
         cuts = ncut;
       }
       std::vector<int> cnt(size_t(W), 0);
