@@ -143,3 +143,53 @@ def test_priority_turns_and_wave_map_keep_the_sums(gpu, nat, monkeypatch):
     # the first rows staged into LDS at kernel entry (default) or loaded by the march (PE_STAGE=0): same bits
     assert np.array_equal(ws["off"], ws["nostage"])
     assert np.abs(ws["off"] - ws["perm"]).max() <= 1e-9 * scale
+
+
+@pytest.mark.parametrize("M,N", [(2048, 2048), (2400, 3200)])
+def test_tuned_layout_is_a_fresh_layout(gpu, nat, monkeypatch, M, N):
+    """The rows-per-item tuning runs its trials pipelined and ends on a layout
+    from its cache (the finalists', the final one; the equal-cost layout's
+    runs are cached too): that list is the one a fresh construction builds at
+    the same height and layout, entry for entry."""
+    for k in ("PE_TI", "PE_LAYOUT", "PE_TI_TUNE"):
+        monkeypatch.delenv(k, raising=False)
+    prob = EllipseProblem(M, N).to_native()
+    blk = D.block(M, N, 1, 0)
+    s1 = nat.DeviceSolver(prob, blk, None, nat.SolveOptions())
+    assert len(s1.ti_tuning_ms) > 0
+    ti, lay, ent1 = s1.ti, s1.layout_name, [tuple(e) for e in s1.layout_entries]
+    del s1
+    monkeypatch.setenv("PE_TI", str(ti))
+    monkeypatch.setenv("PE_LAYOUT", lay)
+    s2 = nat.DeviceSolver(prob, blk, None, nat.SolveOptions())
+    assert len(s2.ti_tuning_ms) == 0 and s2.ti == ti and s2.layout_name == lay
+    assert [tuple(e) for e in s2.layout_entries] == ent1
+
+
+def test_halo_choice_layout_is_a_fresh_layout(gpu, nat, monkeypatch):
+    """The halo-path choice switches between cached layouts (the overlap at the
+    tuning's three best heights); the overlapped list it ends on is the one a
+    fresh construction lays out at that height, entry for entry.  One rank's
+    block of the 8-rank slab of 8192², delay transport, the exchange's overlap
+    forced (PE_HALO=exchange PE_OVERLAP=1)."""
+    M = N = 8192
+    prob = EllipseProblem(M, N).to_native()
+    blk = nat.decompose(M, N, D.grid(8, M, N, "rows"), 4)
+    for k in ("PE_TI", "PE_LAYOUT", "PE_HALO_TUNE"):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("PE_HALO", "exchange")
+    monkeypatch.setenv("PE_OVERLAP", "1")
+    opt = nat.SolveOptions()
+    opt.check_tol = False
+    c1 = nat.make_delay_comm(8, 0.0, 0.0, True)
+    s1 = nat.DeviceSolver(prob, blk, c1, opt)
+    assert s1.overlap and s1.halo_path == "exchange+overlap"
+    assert len([n for n, _ in s1.halo_candidates if "(again)" not in n]) >= 2  # (several heights timed)
+    ti, ent1, nb1 = s1.ti, [tuple(e) for e in s1.layout_entries], s1.layout_boundary
+    del s1, c1
+    monkeypatch.setenv("PE_TI", str(ti))
+    c2 = nat.make_delay_comm(8, 0.0, 0.0, True)
+    s2 = nat.DeviceSolver(prob, blk, c2, opt)
+    assert s2.overlap and s2.ti == ti
+    assert s2.layout_boundary == nb1
+    assert [tuple(e) for e in s2.layout_entries] == ent1
