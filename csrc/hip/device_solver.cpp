@@ -1113,7 +1113,13 @@ void DeviceSolver::choose_halo_path() {
   const bool put_ov = put_ok_ && (!shared_dev_ || put_ov_forced) && ov_able && !(ov && std::atoi(ov) == 0);
   const bool put_ov_late = put_ov && ex_ok && !cands.empty() && cands.back().ov;  // (after the exchange's heights)
   if (put_ov && !put_ov_late) add("put", true);
-  if (cands.empty()) cands.push_back(Cand{"exchange", ov && std::atoi(ov) != 0 && ov_able, 0.0, 0});
+  if (cands.empty()) {  // (the forced path is not available here: the exchange, at every height when overlapped)
+    if (ov && std::atoi(ov) != 0 && ov_able) {
+      for (int h : heights) cands.push_back(Cand{"exchange", true, 0.0, h});
+    } else {
+      cands.push_back(Cand{"exchange", false, 0.0, 0});
+    }
+  }
   auto name = [](const Cand& c) { return c.path + (c.ov ? "+overlap" : ""); };
   // (the overlap at the tuning's second height is reported as "exchange+overlap @96")
   auto label = [&](const Cand& c) { return name(c) + (c.ov && c.ti != ti0 ? " @" + std::to_string(c.ti) : std::string()); };

@@ -20,6 +20,8 @@ M = N = 8192
 P, spec = 8, os.environ.get("PROBE_SPEC", "rows")
 blk = nat.decompose(M, N, D.grid(P, M, N, spec), P // 2)
 os.environ["PE_HALO"] = os.environ.get("PROBE_HALO", "exchange")
+if os.environ["PE_HALO"] == "put":  # (the delay transport maps no peer inboxes: the loopback put)
+    os.environ["PE_PUT_LOOPBACK"] = "1"
 os.environ["PE_OVERLAP"] = "1"
 for rep in range(int(os.environ.get("PROBE_REPS", "4"))):
     comm = nat.make_delay_comm(P, 0.0, 0.0, True)
