@@ -83,7 +83,7 @@ void DeviceSolver::setup_items() {
   if (lay_cache_on_) {
     auto it = lay_cache_.find({k.ti, overlap_, lay_name_});
     if (it != lay_cache_.end()) {
-      restore_layout(it->second);
+      if (!lay_dry_) restore_layout(it->second);
       return;
     }
   }
@@ -780,9 +780,11 @@ void DeviceSolver::setup_items() {
     for (int x = 1; x <= 8; ++x) ov_lbase_[x] = int(all.size());
     ov_lnb_[0] = nbnd;
     for (int x = 1; x < 8; ++x) ov_lnb_[x] = 0;
-    list_alloc(all.size());
     const auto tc = clk::now();
-    upload(ilist_, all.data(), sizeof(int2) * all.size());
+    if (!lay_dry_) {  // (a dry layout only fills the cache: prepare_layout)
+      list_alloc(all.size());
+      upload(ilist_, all.data(), sizeof(int2) * all.size());
+    }
     ilist_host_.assign(all.begin(), all.end());
     copy_setup_s_ += secs(tc, clk::now());
     k.ilist = ilist_;
@@ -794,7 +796,7 @@ void DeviceSolver::setup_items() {
     // static list walk: the grid is the one the list was laid out for (plus
     // the blocks the overlap keeps free for the halo stream)
     k.nblocks = k.nblocks0 = static_waves_ / dev::kWPB + (overlap_ ? ov_reserve_ : 0);
-    if (overlap_) create_halo_stream();
+    if (overlap_ && !lay_dry_) create_halo_stream();
     lap("list");
     return;
   }
@@ -856,9 +858,11 @@ void DeviceSolver::setup_items() {
   }
   ov_lbase_[nsh] = int(all.size());
   if (int(all.size()) < k.nitems || int(all.size()) > nslot_cap_) throw std::logic_error("item list does not fit");
-  list_alloc(all.size());
   const auto tc = clk::now();
-  upload(ilist_, all.data(), sizeof(int2) * all.size());
+  if (!lay_dry_) {
+    list_alloc(all.size());
+    upload(ilist_, all.data(), sizeof(int2) * all.size());
+  }
   ilist_host_.assign(all.begin(), all.end());
   copy_setup_s_ += secs(tc, clk::now());
   // Every dynamic sweep walks the list (the plain one counts no boundary
@@ -868,7 +872,7 @@ void DeviceSolver::setup_items() {
   k.nslots = int(all.size());
   for (int x = 0; x <= 8; ++x) k.lbase[x] = x <= nsh ? ov_lbase_[x] : ov_lbase_[nsh];
   for (int x = 0; x < 8; ++x) k.lnb[x] = 0;
-  if (overlap_) create_halo_stream();
+  if (overlap_ && !lay_dry_) create_halo_stream();
 }
 
 DeviceSolver::LayoutSnap DeviceSolver::snap_layout() const {
@@ -897,7 +901,13 @@ DeviceSolver::LayoutSnap DeviceSolver::snap_layout() const {
 
 void DeviceSolver::restore_layout(const LayoutSnap& v) {
   KParams& k = *kp_;
-  if (v.list.size() > ilist_cap_) throw std::logic_error("cached item list larger than the list buffer");
+  if (v.list.size() > ilist_cap_) {  // (laid out dry, ahead: prepare_layout)
+    PE_HIP_CHECK(hipStreamSynchronize(stream_));
+    if (ilist_) PE_HIP_CHECK(hipFree(ilist_));
+    ilist_cap_ = v.list.size() + v.list.size() / 2;
+    PE_HIP_CHECK(hipMalloc(&ilist_, sizeof(int2) * ilist_cap_));
+  }
+  nslot_cap_ = std::max<int>(nslot_cap_, int(v.list.size()));
   upload(ilist_, v.list.data(), sizeof(int2) * v.list.size());
   ilist_host_ = v.list;
   static_waves_ = v.static_waves;
@@ -919,6 +929,46 @@ void DeviceSolver::restore_layout(const LayoutSnap& v) {
   k.nblocks = v.nblocks;
   k.nblocks0 = v.nblocks0;
   if (overlap_) create_halo_stream();
+}
+
+// Lays out (ti, overlap) into the layout cache without touching the live
+// iteration — host work only, no list upload, every member it sets restored —
+// so that the halo-path choice can build its next candidates' layouts while
+// the GPU times the current one.
+void DeviceSolver::prepare_layout(int ti, bool overlap) {
+  if (!fused_ || !lay_cache_on_) return;
+  const KParams keep_k = *kp_;
+  const bool keep_want = want_overlap_, keep_ov = overlap_, keep_push = push_;
+  const LayoutSnap keep = snap_layout();
+  auto back = [&]() {
+    lay_dry_ = false;
+    *kp_ = keep_k;
+    want_overlap_ = keep_want;
+    overlap_ = keep_ov;
+    push_ = keep_push;
+    ilist_host_ = keep.list;
+    static_waves_ = keep.static_waves;
+    ov_nb_ = keep.ov_nb;
+    ov_lnsh_ = keep.ov_lnsh;
+    std::copy(keep.ov_lbase, keep.ov_lbase + 9, ov_lbase_);
+    std::copy(keep.ov_lnb, keep.ov_lnb + 8, ov_lnb_);
+    lay_items_ = keep.lay_items;
+    lay_cuts_ = keep.lay_cuts;
+    lay_max_ = keep.lay_max;
+    lay_mean_ = keep.lay_mean;
+    lay_used_ = keep.lay_used;
+  };
+  lay_dry_ = true;
+  want_overlap_ = overlap;
+  push_ = false;  // (the overlap's list: the push never overlaps)
+  try {
+    set_items(ti);
+    setup_items();
+  } catch (...) {
+    back();
+    throw;
+  }
+  back();
 }
 
 // LDS-resident geometry: tiles of one 124-column strip × R rows (the

@@ -9,6 +9,7 @@
 #include <memory>
 #include <stdexcept>
 #include <array>
+#include <functional>
 #include <map>
 #include <tuple>
 #include <string>
@@ -299,6 +300,7 @@ class DeviceSolver {
   void apply_halo_path(const std::string& path, bool overlap, bool live = false, int ti = 0);
   LayoutSnap snap_layout() const;
   void restore_layout(const LayoutSnap& v);
+  void prepare_layout(int ti, bool overlap);  // into the cache, host only (item_layout.cpp)
   // one halo phase through the put kernel (put_) or the comm
   void xfer(const std::vector<Exchange>& ex, hipStream_t s);
   void import_halos();     // halo push: x's halo rows <- the receive buffers (enqueued)
@@ -410,6 +412,8 @@ class DeviceSolver {
   std::vector<int2> ilist_host_;
   std::map<std::tuple<int, bool, std::string>, LayoutSnap> lay_cache_;  // (rows per item, overlap, layout name)
   bool lay_cache_on_ = false;
+  bool lay_dry_ = false;                   // setup_items lays out for the cache only (no upload)
+  std::function<void()> halo_idle_;        // host work while time_halo_path's sweeps run (the choice's next layouts)
   std::string push_status_ = "off", xr_status_ = "none";
   int wave_caps_[2] = {0, 0};     // resident waves of the applying / deferring sweep
   int cus_ = 256;                  // compute units of the device (a static layout's first cus_ workgroups run first on their CU)
