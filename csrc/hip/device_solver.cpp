@@ -1091,6 +1091,13 @@ void DeviceSolver::choose_halo_path() {
   // the exchange's overlap timed best (the halo path does not move that rank).
   const int ti0 = kp_->ti;
   std::vector<int> heights = ti_alt_.empty() ? std::vector<int>{ti0} : ti_alt_;
+  {  // every rank times as many candidates (and calls host_max as often): each
+     // rank tunes its own block's rows per item — or none, when its block is
+     // past the tuning's size — so the number of heights can differ
+    double v[1] = {-double(heights.size())};
+    comm_->host_max(v, 1, stream_);
+    heights.resize(size_t(std::max(1.0, -v[0])));
+  }
   auto add = [&](const char* path, bool o) {
     if (o && !ov_able) return;
     if (ov && (std::atoi(ov) != 0) != o) return;

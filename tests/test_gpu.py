@@ -306,6 +306,32 @@ def test_two_process_device_path_host_staged(gpu):
     assert d["n_gpus"] == 2 and d["valid"] and d["converged"]
 
 
+def test_halo_choice_agrees_when_ranks_tune_differently(gpu):
+    """Each rank tunes its own rows per item — or not at all past 2²⁵ nodes —
+    so the overlap's candidate heights can differ in number between ranks;
+    the halo-path choice agrees on one count first (every rank then times as
+    many candidates and calls the cross-rank max as often).  8194×8192 on 2
+    row slabs: rank 0's block is 4096×8191 (tuned: three heights), rank 1's
+    4097×8191 (2²⁵ nodes and more: not tuned, one height).  Before the
+    agreement the job hung in the choice's collectives.  Host-staged transport,
+    P2P sums (the put candidates too), 30 iterations."""
+    from conftest import free_port
+
+    base = {k: v for k, v in os.environ.items() if k not in ("PE_HALO", "PE_OVERLAP", "PE_STEPS", "PE_TI", "PE_TI_TUNE")}
+    env = dict(base, PE_COMM="host", PE_ALLREDUCE="p2p", PE_P2P_TIMEOUT_S="60", PE_XR="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), "-m",
+           "poisson_ellipse_openmp_mpi_cuda_amd", "--json", "--quiet", "--decomp", "rows", "--max-iter", "30",
+           "8194", "8192"]
+    out = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert out.returncode == 0, out.stderr[-3000:]
+    d = json.loads([l for l in out.stdout.splitlines() if l.startswith("{")][0])
+    assert d["ranks"] == 2 and d["iters"] == 30
+    names = [n for n, _ in d["halo_candidates"] if "(again)" not in n]
+    assert sum(1 for n in names if n.startswith("exchange+overlap")) == 1, names  # (the agreed count: rank 1's one)
+    assert "exchange" in names and "put" in names, names
+
+
 @pytest.mark.parametrize("nproc,decomp,allreduce,env", [
     # the default path (no PE_HALO / PE_OVERLAP): chosen at construction by timing
     (4, "aspect", "p2p", {}), (3, "rows", "p2p", {}), (4, "rows", "p2p", {}), (2, "aspect", "p2p", {}),
