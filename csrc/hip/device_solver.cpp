@@ -1128,7 +1128,7 @@ void DeviceSolver::choose_halo_path() {
     }
   }
   auto name = [](const Cand& c) { return c.path + (c.ov ? "+overlap" : ""); };
-  // (the overlap at the tuning's second height is reported as "exchange+overlap @96")
+  // (an overlap at another height than the tuned one is reported as "exchange+overlap @96")
   auto label = [&](const Cand& c) { return name(c) + (c.ov && c.ti != ti0 ? " @" + std::to_string(c.ti) : std::string()); };
   const bool tune = !(std::getenv("PE_HALO_TUNE") && std::atoi(std::getenv("PE_HALO_TUNE")) == 0);
   if ((cands.size() == 1 && !put_ov_late) || !tune) {
