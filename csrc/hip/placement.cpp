@@ -123,8 +123,11 @@ bool DeviceSolver::placement_search(bool retry) {
   // three-step sweep's 48 B/node per sweep at ≥ 4.4 TB/s (8192²: ≤ 0.732 ms;
   // with the aligned strips and 112-row items its classes are 0.709-0.722,
   // 0.74, 0.78-0.79 and 0.83-0.85 ms, the first fast one usually the 5th try —
-  // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates)
-  const double fast_tbs = steps_ >= 3 ? 4.4 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
+  // profiles/r4_bench112.txt; 4.2 stopped at 0.743 ms candidates) — 4.45 TB/s
+  // (≤ 0.724 ms) since round 6: 4.4 accepted a 0.7295 ms candidate and the
+  // bench ran 3876 it/s against 4011-4136 with 0.701-0.722 ms picks
+  // (profiles/r6_placement.txt)
+  const double fast_tbs = steps_ >= 3 ? 4.45 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (tries <= 1) return true;
   // spacers are transient; never let the search take more than 40 % of the
   // free memory (several solvers may share the device)
