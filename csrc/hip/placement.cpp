@@ -113,6 +113,13 @@ bool DeviceSolver::placement_search(bool retry) {
   // process found its best-class candidate at the 9th try (1838 it/s,
   // profiles/r2_validate_final.txt); a try costs ≈6 ms, and the search
   // stops at the first best-class candidate.
+  // (Multi-GPU blocks of 4-24 M nodes have no search: their job runs at its
+  // worst rank's placement — 8-rank slab block of 8192² 37.5-40.0 µs per
+  // iteration over fresh solvers, 37.0-38.2 with a search — but the search
+  // that found their fast placements took 0.5 s of construction in a fresh
+  // process (8 tries past 12 GB spacers), and 4 tries past 8 GB stayed in one
+  // slow run of allocations: profiles/r6_placement.txt, measured in round 6,
+  // not adopted.)
   int tries = pts >= 24.0e6 ? 12 : 1;
   if (retry) tries = std::max(1, tries / 2 + 1);  // the kept candidate + half a round
   if (const char* e = std::getenv("PE_PLACEMENT_TRIES")) tries = std::max(1, std::atoi(e));
