@@ -26,7 +26,7 @@ HIPFLAGS  += $(COMMON) --offload-arch=$(ARCH) -ffp-contract=off -mcode-object-ve
 LDLIBS    := -L$(ROCM)/lib -lamdhip64 -lrccl -lrocprofiler-sdk-roctx -lgomp -lpthread -Wl,-rpath,$(ROCM)/lib
 
 CORE_SRC  := csrc/core/decomp.cpp csrc/core/thread_comm.cpp csrc/core/report.cpp csrc/cpu/pcg_cpu.cpp
-HOST_SRC  := csrc/hip/device_solver.cpp csrc/hip/item_layout.cpp csrc/hip/placement.cpp csrc/hip/checkpoint.cpp csrc/hip/rccl_comm.cpp csrc/hip/p2p_comm.cpp csrc/hip/runtime.cpp csrc/core/row_classes.cpp
+HOST_SRC  := csrc/hip/device_solver.cpp csrc/hip/item_layout.cpp csrc/hip/placement.cpp csrc/hip/checkpoint.cpp csrc/hip/halo_path.cpp csrc/hip/rccl_comm.cpp csrc/hip/p2p_comm.cpp csrc/hip/runtime.cpp csrc/core/row_classes.cpp
 HIP_SRC   := csrc/hip/kernels.hip csrc/hip/fused.hip csrc/hip/fused2.hip csrc/hip/fused3.hip csrc/hip/resident.hip csrc/hip/p2p.hip
 BIND_SRC  := csrc/bind/module.cpp
 
