@@ -134,7 +134,14 @@ bool DeviceSolver::placement_search(bool retry) {
   // (≤ 0.724 ms) since round 6: 4.4 accepted a 0.7295 ms candidate and the
   // bench ran 3876 it/s against 4011-4136 with 0.701-0.722 ms picks
   // (profiles/r6_placement.txt)
-  const double fast_tbs = steps_ >= 3 ? 4.45 : sstep_ ? 4.7 : 4.9, max_s = 0.3;
+  // Blocks of 24-50 M nodes (the 2-rank split of 8192²) stream slower per
+  // byte: their best candidates are 0.396-0.400 ms per sweep at 33.5 M nodes =
+  // 4.03-4.06 TB/s, so the three-step rate there is 4.0 TB/s — at 4.45 no
+  // candidate ever qualified, every rank then ran the retry round, and its
+  // spacer past the first round's memory took 1-4 s of construction
+  // (profiles/r6_placement.txt)
+  const bool mid_large = pts < 50.0e6;
+  const double fast_tbs = steps_ >= 3 ? (mid_large ? 4.0 : 4.45) : sstep_ ? 4.7 : 4.9, max_s = 0.3;
   if (tries <= 1) return true;
   // spacers are transient; never let the search take more than 40 % of the
   // free memory (several solvers may share the device)
@@ -229,7 +236,8 @@ bool DeviceSolver::placement_search(bool retry) {
   // a retry appends its candidates (its first is the first round's pick, re-timed)
   placement_best_ = int(placement_ms_.size() + best);
   for (const Cand& x : c) placement_ms_.push_back(x.ms / 6.0f);
-  return fast || (sstep_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
+  // (below 50 M nodes no retry round: the best of this round stands)
+  return fast || mid_large || (sstep_ ? 48.0 : 40.0) * pts / (double(c[best].ms) / 6.0 * 1e-3) / 1e12 >= fast_tbs;
 }
 
 }  // namespace pe

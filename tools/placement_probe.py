@@ -1,6 +1,6 @@
-"""Memory-placement spread of one rank's block: fresh solvers with the
-placement search forced on (PE_PLACEMENT_TRIES, default 12; the search runs
-by itself only from 24 M nodes per block), each printing its candidates' ms
+"""Memory-placement spread of one rank's block: fresh solvers, the placement
+search forced with PE_PLACEMENT_TRIES (else the solver's own rule: a search
+from 24 M nodes per block), each printing its candidates' ms
 per sweep and the chosen one, then 300 timed iterations of the solver as
 constructed.  One rank's block of a P-rank split of 8192² on one GPU (delay
 transport, zero delays: no communication cost).
@@ -18,7 +18,6 @@ from poisson_ellipse_openmp_mpi_cuda_amd.parallel import decomp as D  # noqa: E4
 
 nat = native()
 nat.set_device(0)
-os.environ.setdefault("PE_PLACEMENT_TRIES", "12")
 os.environ.setdefault("PE_HALO", "exchange")
 os.environ.setdefault("PE_OVERLAP", "0")
 M = N = 8192
